@@ -1,0 +1,335 @@
+"""Benchmark of the accdfl FedAvg aggregation reduce on MI355X.
+
+Metric (BASELINE.json): aggregated-model GB/s (device-resident), N-peer reduce.
+Workload per GPU (north star, BASELINE.json north_star): 8 peers x 25,000,000 fp32
+parameters, inputs resident in HBM.  With --gpus G (one process per GPU, launched by
+torch.distributed.run) the model is G x 25 M parameters, bucket-sharded: every rank
+reduces its own 25 M-parameter bucket of all 8 peers (weak scaling, no data-path
+collective; the optional all-gather that reassembles the model is timed separately).
+
+One step = one launch of the libdlagg kernel over one rank's bucket.
+Algorithmic bytes per step per rank = (N + 1) * P * 4 (N peer reads + 1 output write).
+value = sum over ranks of bytes / max-over-ranks step time.
+
+Extra objects on the JSON line:
+  roofline      dominant kernel (wsum_stream_kernel): achieved GB/s from HIP events on
+                the launch stream over the timed region vs 8 TB/s HBM peak; traffic =
+                PMC HBM bytes per launch from profiles/ (null if not collected)
+  cpu_baseline  the reference's torch-CPU op sequence (oracle/fedavg_oracle.py, kind
+                "port") on this host's cores, rank 0 at N=1 only, bounded sample
+  host_inclusive  FedAvg.aggregate on CPU modules (the reference call sites'
+                situation): pack + H2D + reduce + D2H, rank 0 at N=1 only
+  small_configs device-resident rates of the BASELINE configs 1-2 model sizes
+                (cache-resident / launch-bound; informational)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "decentralized-learning_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "aggregated-model GB/s (device-resident), N-peer reduce; 1/2/4/8 GPU"
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (/opt/skills/guides/MI355X_MICROARCH.md)
+NS_PEERS = 8
+NS_PARAMS = 25_000_000
+PMC_FILE = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+
+SMALL = {  # BASELINE configs[1] / configs[2] parameter counts
+    "cifar10_gnlenet_n8": (8, 85_354),
+    "femnist_cnn_n32": (32, 1_690_046),
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--peers", type=int, default=NS_PEERS)
+    ap.add_argument("--params", type=int, default=NS_PARAMS)
+    ap.add_argument("--dtype", default="f32", choices=["f32", "bf16"])
+    ap.add_argument("--variant", type=int, default=0)
+    ap.add_argument("--chunks", type=int, default=0)
+    ap.add_argument("--grid", type=int, default=0)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample budget")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-host-inclusive", action="store_true")
+    ap.add_argument("--no-small", action="store_true")
+    ap.add_argument("--allgather", action="store_true", help="also time the RCCL all-gather of the buckets")
+    ap.add_argument("--sweep", action="store_true", help="interleaved A/B of launch variants, then exit")
+    return ap.parse_args()
+
+
+def setup_dist():
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    return rank, world, torch.device("cuda", local)
+
+
+def barrier(world):
+    if world > 1:
+        dist.barrier()
+
+
+def make_slab(n, p, dtype, device, seed_base):
+    """Synthetic peers (BASELINE.md plan): per-peer seed, normal(0, 0.05)."""
+    slab = torch.empty((n, p), dtype=dtype, device=device)
+    for k in range(n):
+        g = torch.Generator(device=device).manual_seed(seed_base + k)
+        slab[k].normal_(0.0, 0.05, generator=g)
+    return slab
+
+
+def time_kernel(fn, steps, warmup, world):
+    """Warmup, then exactly `steps` calls bracketed by barrier + synchronize; returns
+    (wall seconds max over ranks, HIP-event seconds on the launch stream)."""
+    for _ in range(warmup):
+        fn()
+    stream = torch.cuda.current_stream()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    barrier(world)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(steps):
+        fn()
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    barrier(world)
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    ev_s = ev0.elapsed_time(ev1) / 1e3
+    if world > 1:
+        t = torch.tensor([wall, ev_s], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        wall, ev_s = float(t[0]), float(t[1])
+    return wall, ev_s
+
+
+def cpu_baseline(n, p, budget_s):
+    """The reference op sequence (deepcopy -> mul_(0) -> add_(w*p)) on torch-CPU, timed on
+    a bounded sample of the same workload: repeated full NS reduces until ~budget_s."""
+    sys.path.insert(0, ROOT)
+    from oracle.fedavg_oracle import fedavg_flat_torch  # timed CPU baseline (kind "port")
+
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    gen = torch.Generator().manual_seed(1000)
+    peers = [torch.randn(p, generator=gen) * 0.05 for _ in range(n)]
+    w = [float(x) for x in np.random.default_rng(0).dirichlet(np.ones(n))]
+    out = torch.empty(p)
+    fedavg_flat_torch(peers, w, out)  # warm-up
+    times = []
+    start = time.perf_counter()
+    while (time.perf_counter() - start < budget_s and len(times) < 200) or len(times) < 3:
+        t0 = time.perf_counter()
+        fedavg_flat_torch(peers, w, out)
+        times.append(time.perf_counter() - t0)
+    med = statistics.median(times)
+    return {
+        "value": round((n + 1) * p * 4 / med / 1e9, 3),
+        "unit": "GB/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": "%d full reduces of %d peers x %d fp32 (torch-CPU op sequence of fedavg.py:20-25), median "
+                  "%.1f ms, %.1f s total" % (len(times), n, p, med * 1e3, sum(times)),
+        "cpu": _cpu_model(),
+    }
+
+
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
+def host_inclusive(n, p, reps=5):
+    """FedAvg.aggregate on CPU modules (the reference call sites) end to end."""
+    from torch import nn
+
+    from accdfl_amd.core.gradient_aggregation.fedavg import FedAvg
+
+    gen = torch.Generator().manual_seed(2000)
+    models = []
+    for _ in range(n):
+        m = nn.Module()
+        m.w = nn.Parameter(torch.randn(p, generator=gen) * 0.05)
+        models.append(m)
+    w = [float(1.0 / n)] * n
+    FedAvg.aggregate(models, w)
+    times = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        FedAvg.aggregate(models, w)
+        times.append(time.perf_counter() - t0)
+    med = statistics.median(times)
+    return {"value": round((n + 1) * p * 4 / med / 1e9, 3), "unit": "GB/s", "ms": round(med * 1e3, 2),
+            "path": "FedAvg.aggregate(CPU nn.Modules): deepcopy + pinned pack + H2D + reduce + D2H + unpack"}
+
+
+def small_configs(device, steps=200):
+    from accdfl_amd.core import wsum
+
+    res = {}
+    for name, (n, p) in SMALL.items():
+        slab = make_slab(n, (p + 63) // 64 * 64, torch.float32, device, 1000)
+        w = [float(1.0 / n)] * n
+        out = torch.empty(p, dtype=torch.float32, device=device)
+        wall, ev = time_kernel(lambda: wsum.wsum_rows(slab, w, p, out=out), steps, 20, 1)
+        res[name] = {"GB/s": round((n + 1) * p * 4 / (ev / steps) / 1e9, 1), "us_per_reduce": round(ev / steps * 1e6, 2),
+                     "bytes": (n + 1) * p * 4, "note": "fits the 256 MiB Infinity Cache; launch/latency-bound"}
+        del slab
+    return res
+
+
+def sweep(args, device):
+    from accdfl_amd import _lib
+    from accdfl_amd.core import wsum
+
+    dt = torch.float32 if args.dtype == "f32" else torch.bfloat16
+    es = 4 if args.dtype == "f32" else 2
+    slab = make_slab(args.peers, args.params, dt, device, 1000)
+    out = torch.empty(args.params, dtype=dt, device=device)
+    w = [float(1.0 / args.peers)] * args.peers
+    ptrs = [slab[k].data_ptr() for k in range(args.peers)]
+    code = wsum.dtype_code(dt)
+    sp = torch.cuda.current_stream().cuda_stream
+    cfgs = [(v, c, g) for v in (1, 2) for c in (1, 2, 4) for g in (0, 1024, 2048, 4096)]
+    res = {c: [] for c in cfgs}
+    for rnd in range(5):
+        for c in cfgs:
+            cfg = _lib.LaunchCfg(*c)
+            fn = lambda: _lib.wsum_ptrs(code, ptrs, w, args.params, out.data_ptr(), sp, cfg)  # noqa: E731
+            _, ev = time_kernel(fn, 50, 5, 1)
+            res[c].append(ev / 50)
+    byts = (args.peers + 1) * args.params * es
+    rows = sorted(((statistics.median(v), c) for c, v in res.items()))
+    for t, c in rows:
+        print(json.dumps({"variant": c[0], "chunks": c[1], "grid": c[2], "us": round(t * 1e6, 2),
+                          "GB/s": round(byts / t / 1e9, 1), "min_us": round(min(res[c]) * 1e6, 2)}))
+    # measured device copy peak (torch copy kernel) for reference
+    a = torch.empty(512 * 1024 * 1024 // 4, dtype=torch.float32, device=device)
+    b = torch.empty_like(a)
+    _, ev = time_kernel(lambda: b.copy_(a), 50, 5, 1)
+    print(json.dumps({"torch_copy_GBps": round(2 * a.numel() * 4 / (ev / 50) / 1e9, 1)}))
+
+
+def main():
+    args = parse()
+    rank, world, device = setup_dist()
+    from accdfl_amd import _lib
+    from accdfl_amd.core import wsum
+
+    _lib.lib()  # fail loudly here if the HIP library is missing
+    if args.sweep:
+        sweep(args, device)
+        return
+    dt = torch.float32 if args.dtype == "f32" else torch.bfloat16
+    es = 4 if args.dtype == "f32" else 2
+    n, p = args.peers, args.params
+    # this rank's bucket of every peer: rows of one [n, pitch] slab (16-B aligned rows)
+    pitch = (p + 63) // 64 * 64
+    slab = make_slab(n, pitch, dt, device, 1000 + 97 * rank)
+    out = torch.empty(p, dtype=dt, device=device)
+    w = [float(x) for x in np.random.default_rng(0).dirichlet(np.ones(n))]
+    cfg = None
+    if args.variant or args.chunks or args.grid:
+        cfg = _lib.LaunchCfg(args.variant, args.chunks, args.grid)
+    ptrs = [slab[k].data_ptr() for k in range(n)]
+    code = wsum.dtype_code(dt)
+
+    def step():
+        _lib.wsum_ptrs(code, ptrs, w, p, out.data_ptr(), torch.cuda.current_stream().cuda_stream, cfg)
+
+    wall, ev = time_kernel(step, args.steps, args.warmup, world)
+    bytes_step = (n + 1) * p * es
+    ms_per_step = wall / args.steps * 1e3
+    value = world * bytes_step / (wall / args.steps) / 1e9
+    kern_s = ev / args.steps
+    achieved = bytes_step / kern_s / 1e9
+    traffic = None
+    if os.path.exists(PMC_FILE):
+        try:
+            pm = json.load(open(PMC_FILE))
+            if pm.get("workload") == "ns" and pm.get("peers") == n and pm.get("params") == p:
+                traffic = pm.get("hbm_bytes_per_launch")
+        except (OSError, ValueError):
+            traffic = None
+
+    result = {
+        "metric": METRIC,
+        "value": round(value, 2),
+        "unit": "GB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 5),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": args.dtype,
+        "data": "synthetic (per-peer seeded normal(0, 0.05), Dirichlet(1) weights), inputs resident in HBM",
+        "config": {
+            "workload": "north-star FedAvg reduce: %d peers x %d %s params per GPU (one parameter bucket per "
+                        "GPU of a %d-GPU bucket-sharded model)" % (n, p, args.dtype, world),
+            "n_peers": n,
+            "params_per_gpu": p,
+            "global_params": p * world,
+            "parallelism": "bucket-sharded x%d (no data-path collective)" % world,
+        },
+        "roofline": {
+            "bound": "hbm",
+            "kernel": "wsum_stream_kernel",
+            "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBPS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBPS, 4),
+            "traffic": traffic,
+            "bytes_per_launch": bytes_step,
+            "us_per_launch": round(kern_s * 1e6, 2),
+        },
+    }
+    if args.allgather and world > 1:
+        from accdfl_amd.core.sharding import BucketShardedFedAvg
+
+        sh = BucketShardedFedAvg(p * world, dt, device=device)
+        bucket = torch.zeros(sh.bucket_len, dtype=dt, device=device)
+        full = torch.empty(p * world, dtype=dt, device=device)
+        wall_ag, _ = time_kernel(lambda: sh.all_gather(bucket, full), 20, 3, world)
+        result["allgather"] = {"ms": round(wall_ag / 20 * 1e3, 3), "bytes_per_rank_out": p * world * es}
+    if rank == 0 and world == 1:
+        if not args.no_small:
+            result["small_configs"] = small_configs(device)
+        del slab
+        torch.cuda.empty_cache()
+        if not args.no_host_inclusive and args.dtype == "f32":
+            result["host_inclusive"] = host_inclusive(n, p)
+        if not args.no_cpu_baseline and args.dtype == "f32":
+            result["cpu_baseline"] = cpu_baseline(n, p, args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,174 @@
+"""ctypes binding of libdlagg.so (C ABI declared in include/dlagg.h).
+
+This is the only way the package reaches the GPU reduce.  There is no CPU or
+PyTorch fallback: if the library is missing, fails to load, or no HIP device is
+visible, every entry point raises.  (The reference's CPU path is the thing being
+replaced; a silent fallback would report reference numbers as ours.)
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+import threading
+from typing import Optional, Sequence
+
+PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))  # decentralized-learning_amd/
+REPO_ROOT = os.path.dirname(PKG_ROOT)
+CSRC = os.path.join(PKG_ROOT, "csrc", "dlagg.hip")
+INCLUDE = os.path.join(REPO_ROOT, "include")
+LIB_PATH = os.environ.get("DLAGG_LIB", os.path.join(PKG_ROOT, "lib", "libdlagg.so"))
+
+# dtype codes (include/dlagg.h)
+DLA_F32, DLA_BF16, DLA_F16, DLA_F64 = 0, 1, 2, 3
+ABI_VERSION = 1
+
+HIPCC_FLAGS = [
+    "--offload-arch=gfx950",
+    "-O3",
+    "-std=c++17",
+    "-ffp-contract=off",  # bit parity: no FMA contraction of w*p + acc
+    "-fno-fast-math",
+    "-fPIC",
+    "-shared",
+]
+
+EXPORTED = (
+    "dla_version",
+    "dla_last_error",
+    "dla_max_peers_per_pass",
+    "dla_wsum",
+    "dla_wsum_ex",
+    "dla_wsum_slab",
+    "dla_wsum_multi",
+)
+
+
+class DlaggError(RuntimeError):
+    """A libdlagg call returned a non-zero status."""
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    """Compile csrc/dlagg.hip for gfx950 into lib/libdlagg.so (in-tree)."""
+    out = os.path.join(PKG_ROOT, "lib", "libdlagg.so")
+    if not force and os.path.exists(out):
+        src_m = max(os.path.getmtime(CSRC), os.path.getmtime(os.path.join(INCLUDE, "dlagg.h")))
+        if os.path.getmtime(out) >= src_m:
+            return out
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+    tmp = out + ".tmp"
+    cmd = [hipcc, *HIPCC_FLAGS, "-I", INCLUDE, "-o", tmp, CSRC]
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, out)
+    return out
+
+
+class _Lib:
+    def __init__(self, path: str):
+        if not os.path.exists(path):
+            raise RuntimeError(
+                "libdlagg.so not found at %s — build it first "
+                "(python -c 'import __graft_entry__ as g; g.build()')" % path)
+        self.path = path
+        self.so = ctypes.CDLL(path)
+        so = self.so
+        vp = ctypes.c_void_p
+        so.dla_version.restype = ctypes.c_int
+        so.dla_last_error.restype = ctypes.c_char_p
+        so.dla_max_peers_per_pass.restype = ctypes.c_int
+        so.dla_wsum.argtypes = [ctypes.c_int, ctypes.POINTER(vp), ctypes.POINTER(ctypes.c_double), ctypes.c_int,
+                                ctypes.c_int64, vp, vp]
+        so.dla_wsum.restype = ctypes.c_int
+        so.dla_wsum_ex.argtypes = so.dla_wsum.argtypes + [ctypes.POINTER(LaunchCfg)]
+        so.dla_wsum_ex.restype = ctypes.c_int
+        so.dla_wsum_slab.argtypes = [ctypes.c_int, vp, ctypes.c_int64, ctypes.POINTER(ctypes.c_double), ctypes.c_int,
+                                     ctypes.c_int64, vp, vp]
+        so.dla_wsum_slab.restype = ctypes.c_int
+        so.dla_wsum_multi.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(vp), ctypes.POINTER(vp),
+                                      ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_double), ctypes.c_int,
+                                      vp]
+        so.dla_wsum_multi.restype = ctypes.c_int
+        v = so.dla_version()
+        if v != ABI_VERSION:
+            raise RuntimeError("libdlagg ABI version %d, expected %d" % (v, ABI_VERSION))
+        self.max_peers_per_pass = so.dla_max_peers_per_pass()
+
+    def check(self, rc: int, what: str):
+        if rc != 0:
+            msg = self.so.dla_last_error().decode(errors="replace")
+            raise DlaggError("%s failed (status %d): %s" % (what, rc, msg))
+
+
+class LaunchCfg(ctypes.Structure):
+    """dla_launch_cfg_t (include/dlagg.h)."""
+    _fields_ = [("variant", ctypes.c_int), ("chunks", ctypes.c_int), ("grid_blocks", ctypes.c_int)]
+
+
+_lib: Optional[_Lib] = None
+_lock = threading.Lock()
+
+
+def lib() -> _Lib:
+    """The loaded library (loads on first use; raises if it cannot)."""
+    global _lib
+    if _lib is None:
+        with _lock:
+            if _lib is None:
+                _lib = _Lib(LIB_PATH)
+    return _lib
+
+
+def loaded_path() -> Optional[str]:
+    return _lib.path if _lib is not None else None
+
+
+# ------------------------------------------------------------------ typed calls
+def _ptr_array(ptrs: Sequence[int]):
+    arr = (ctypes.c_void_p * len(ptrs))()
+    for i, p in enumerate(ptrs):
+        arr[i] = p
+    return arr
+
+
+def _dbl_array(vals: Sequence[float]):
+    arr = (ctypes.c_double * len(vals))()
+    for i, v in enumerate(vals):
+        arr[i] = float(v)
+    return arr
+
+
+def wsum_ptrs(dtype_code: int, peer_ptrs: Sequence[int], weights: Sequence[float], n_elems: int, out_ptr: int,
+              stream_ptr: int, cfg: Optional[LaunchCfg] = None) -> None:
+    """dla_wsum / dla_wsum_ex on raw device pointers."""
+    L = lib()
+    n = len(peer_ptrs)
+    if cfg is None:
+        rc = L.so.dla_wsum(dtype_code, _ptr_array(peer_ptrs), _dbl_array(weights), n, n_elems, out_ptr, stream_ptr)
+    else:
+        rc = L.so.dla_wsum_ex(dtype_code, _ptr_array(peer_ptrs), _dbl_array(weights), n, n_elems, out_ptr,
+                              stream_ptr, ctypes.byref(cfg))
+    L.check(rc, "dla_wsum")
+
+
+def wsum_slab_ptr(dtype_code: int, base_ptr: int, pitch_elems: int, weights: Sequence[float], n_peers: int,
+                  n_elems: int, out_ptr: int, stream_ptr: int) -> None:
+    L = lib()
+    rc = L.so.dla_wsum_slab(dtype_code, base_ptr, pitch_elems, _dbl_array(weights), n_peers, n_elems, out_ptr,
+                            stream_ptr)
+    L.check(rc, "dla_wsum_slab")
+
+
+def wsum_multi_ptrs(dtype_code: int, peer_ptrs: Sequence[int], out_ptrs: Sequence[int], numels: Sequence[int],
+                    weights: Sequence[float], stream_ptr: int) -> None:
+    """peer_ptrs is [n_tensors * n_peers] (tensor-major)."""
+    L = lib()
+    t = len(out_ptrs)
+    n = len(weights)
+    assert len(peer_ptrs) == t * n
+    num = (ctypes.c_int64 * t)(*[int(x) for x in numels])
+    rc = L.so.dla_wsum_multi(dtype_code, t, _ptr_array(peer_ptrs), _ptr_array(out_ptrs), num, _dbl_array(weights),
+                             n, stream_ptr)
+    L.check(rc, "dla_wsum_multi")

@@ -1,0 +1,194 @@
+"""FedAvg on MI355X — drop-in for accdfl/core/gradient_aggregation/fedavg.py:10-26.
+
+``FedAvg.aggregate(models, weights)`` keeps the reference contract exactly:
+
+* falsy ``weights`` -> uniform ``float(1. / N)`` (fedavg.py:14-15); otherwise
+  ``assert len(weights) == len(models)`` (:16-17); empty ``models`` -> IndexError
+  from ``models[0]`` (:20);
+* the result is ``copy.deepcopy(models[0])`` (:20), so it lives where models[0]
+  lives, keeps ``requires_grad`` and every non-parameter attribute, and carries
+  models[0]'s buffers unaveraged;
+* parameter i is ``R(...R(R(p0*0) + R(w0*p0)) + ... + R(w_{N-1}*p_{N-1}))`` in list
+  order, bit-identical to the reference (fedavg.py:21-25; include/dlagg.h);
+* zip truncation (:24): parameter i only takes terms from models that have an i-th
+  parameter;
+* inputs are never mutated.
+
+Deliberate differences (documented in DESIGN.md): parameters whose shapes or dtypes
+differ between models raise RuntimeError instead of broadcasting / promoting.
+
+Where the arithmetic runs: always on the HIP device (libdlagg.so).  Models already
+on the device are reduced in place of their parameters with no copies; CPU models
+(every reference call site) are packed into a pinned host slab, copied H2D
+row by row on a copy stream (overlapping the packing of the next model), reduced,
+and copied back.  The host-staged path is synchronous like the reference; the
+device-resident path is stream-ordered like any torch op.
+"""
+from __future__ import annotations
+
+import copy
+import threading
+from typing import Dict, List, Tuple
+
+import torch
+from torch import nn
+
+from accdfl_amd.core import wsum as _wsum
+from accdfl_amd.core.gradient_aggregation import GradientAggregation
+
+_ALIGN_BYTES = 256
+
+
+def _round_up(x: int, m: int) -> int:
+    return (x + m - 1) // m * m
+
+
+class _HostStaging:
+    """Pinned host slab + device slab for CPU-resident models, grown on demand and
+    reused across calls (one per (device, dtype))."""
+
+    def __init__(self, device: torch.device, dtype: torch.dtype):
+        self.device = device
+        self.dtype = dtype
+        self.rows = 0
+        self.pitch = 0
+        self.h_in = self.d_in = self.d_out = self.h_out = None
+        self.copy_stream = torch.cuda.Stream(device)
+
+    def ensure(self, rows: int, pitch: int):
+        if rows <= self.rows and pitch <= self.pitch:
+            return
+        rows = max(rows, self.rows)
+        pitch = max(pitch, self.pitch)
+        self.h_in = torch.empty((rows, pitch), dtype=self.dtype, pin_memory=True)
+        self.d_in = torch.empty((rows, pitch), dtype=self.dtype, device=self.device)
+        self.d_out = torch.empty(pitch, dtype=self.dtype, device=self.device)
+        self.h_out = torch.empty(pitch, dtype=self.dtype, pin_memory=True)
+        self.rows, self.pitch = rows, pitch
+
+
+_staging: Dict[Tuple[torch.device, torch.dtype], _HostStaging] = {}
+_staging_lock = threading.Lock()
+
+
+def _get_staging(device: torch.device, dtype: torch.dtype) -> _HostStaging:
+    key = (device, dtype)
+    st = _staging.get(key)
+    if st is None:
+        st = _staging[key] = _HostStaging(device, dtype)
+    return st
+
+
+def release_staging() -> None:
+    """Free the cached host/device staging slabs."""
+    with _staging_lock:
+        _staging.clear()
+
+
+def _reduce_host_staged(device, dtype, center: List[torch.Tensor], peers: List[List[torch.Tensor]], weights):
+    """One dtype group, every model contributing to every tensor: pack -> H2D -> reduce -> D2H."""
+    numels = [c.numel() for c in center]
+    total = sum(numels)
+    if total == 0:
+        return
+    esize = torch.empty((), dtype=dtype).element_size()
+    pitch = _round_up(total, _ALIGN_BYTES // esize)
+    n = len(peers)
+    with _staging_lock:
+        st = _get_staging(device, dtype)
+        st.ensure(n, pitch)
+        compute = torch.cuda.current_stream(device)
+        st.copy_stream.wait_stream(compute)  # previous users of d_in are done
+        for k in range(n):
+            flat = [p.detach().reshape(-1) for p in peers[k]]
+            if all(t.device.type == "cpu" for t in flat):
+                row = st.h_in[k, :total]
+                torch.cat(flat, out=row)
+                with torch.cuda.stream(st.copy_stream):
+                    st.d_in[k, :total].copy_(row, non_blocking=True)
+            else:
+                with torch.cuda.stream(st.copy_stream):
+                    torch.cat([t.to(device, non_blocking=True) for t in flat], out=st.d_in[k, :total])
+        compute.wait_stream(st.copy_stream)
+        _wsum.wsum_rows(st.d_in, weights, total, out=st.d_out)
+        st.h_out[:total].copy_(st.d_out[:total], non_blocking=True)
+        compute.synchronize()
+        for c, o in zip(center, torch.split(st.h_out[:total], numels)):
+            c.copy_(o.view_as(c))
+
+
+def _reduce_device_resident(dtype, center: List[torch.Tensor], peers: List[List[torch.Tensor]], weights):
+    """One dtype group, all tensors on the device: reduce straight into the center params."""
+    outs, tmp = [], []
+    for i, c in enumerate(center):
+        if c.is_contiguous():
+            outs.append(c)
+        else:
+            t = torch.empty(c.shape, dtype=c.dtype, device=c.device)
+            outs.append(t)
+            tmp.append((c, t))
+    _wsum.wsum_multi([[p.detach() if p.is_contiguous() else p.detach().contiguous() for p in pl] for pl in peers],
+                     weights, outs)
+    for c, t in tmp:
+        c.copy_(t)
+
+
+def _reduce_param(device, center: torch.Tensor, terms: List[torch.Tensor], weights: List[float]):
+    """A single parameter with its own contributor set (zip truncation)."""
+    dev_terms = [t.detach().to(device).contiguous() for t in terms]
+    out = _wsum.wsum(dev_terms, weights)
+    center.copy_(out.view_as(center))
+    if center.device.type == "cpu":
+        torch.cuda.current_stream(device).synchronize()
+
+
+def reduce_parameters(center_params: List[torch.Tensor], peer_params: List[List[torch.Tensor]],
+                      weights: List[float]) -> None:
+    """fedavg.py:21-25 on parameter lists: center_params[i] <- FedAvg over the models
+    that have an i-th parameter.  ``center_params`` is a deepcopy of models[0]'s."""
+    n = len(peer_params)
+    if not center_params:
+        return
+    first = center_params[0].device
+    device = _wsum.require_device(first if first.type == "cuda" else None)
+    full: Dict[torch.dtype, List[int]] = {}
+    partial: List[int] = []
+    for i, c in enumerate(center_params):
+        _wsum.dtype_code(c.dtype)
+        ks = [k for k in range(n) if len(peer_params[k]) > i]
+        for k in ks:
+            p = peer_params[k][i]
+            if p.shape != c.shape or p.dtype != c.dtype:
+                raise RuntimeError("FedAvg: parameter %d of model %d has shape/dtype %s/%s, model 0 has %s/%s"
+                                   % (i, k, tuple(p.shape), p.dtype, tuple(c.shape), c.dtype))
+        if len(ks) == n:
+            full.setdefault(c.dtype, []).append(i)
+        else:
+            partial.append(i)
+    for dtype, idx in full.items():
+        center = [center_params[i] for i in idx]
+        peers = [[peer_params[k][i] for i in idx] for k in range(n)]
+        resident = all(t.device == device for t in center) and all(t.device == device for pl in peers for t in pl)
+        if resident:
+            _reduce_device_resident(dtype, center, peers, weights)
+        else:
+            _reduce_host_staged(device, dtype, center, peers, weights)
+    for i in partial:
+        ks = [k for k in range(n) if len(peer_params[k]) > i]
+        _reduce_param(device, center_params[i], [peer_params[k][i] for k in ks], [weights[k] for k in ks])
+
+
+class FedAvg(GradientAggregation):
+
+    @staticmethod
+    def aggregate(models: List[nn.Module], weights: List[float]):
+        if not weights:
+            weights = [float(1. / len(models)) for _ in range(len(models))]
+        else:
+            assert len(weights) == len(models)
+
+        with torch.no_grad():
+            center_model = copy.deepcopy(models[0])
+            reduce_parameters(list(center_model.parameters()), [list(m.parameters()) for m in models],
+                              list(weights))
+            return center_model

@@ -1,0 +1,123 @@
+"""Parameter-bucket sharding of the FedAvg reduce over GPUs (one process per GPU).
+
+The reference has no multi-device code at all (every tensor is CPU,
+"distribution" is pickled state_dicts over pyipv8).  On an MI355X node the reduce
+shards naturally: FedAvg is independent per element, so splitting the flat
+parameter vector (``parameters()`` order, fedavg.py:24) into contiguous buckets and
+giving each rank one bucket of EVERY peer keeps each element's summation order —
+the sharded result is bit-identical to the single-GPU (and reference) result and
+the reduce itself needs no inter-GPU traffic.
+
+Exchange steps exist only where data really has to move:
+
+* ``all_gather``: reassemble the averaged buckets into the full model on every rank
+  (RCCL all-gather over xGMI) when a device copy of the whole model is needed;
+  the host path instead copies each bucket D2H straight into the result.
+* ``transpose_peer_sharded``: when peers arrive whole on different ranks (rank r
+  received peers [r*m, (r+1)*m)), one RCCL all-to-all turns "peer-sharded" into
+  "bucket-sharded" so the reduce stays in list order and bit-exact (a local partial
+  sum + reduce-scatter would change the summation order).
+
+Every collective goes through ``torch.distributed`` (backend "nccl" = RCCL on ROCm;
+"gloo" in the CPU tests).  The per-bucket reduce is the libdlagg kernel by default;
+tests inject a CPU checker instead to exercise the exchange logic without a GPU.
+"""
+from __future__ import annotations
+
+from typing import Callable, List, Optional, Sequence, Tuple
+
+import torch
+import torch.distributed as dist
+
+_ALIGN_BYTES = 256
+
+Reducer = Callable[[Sequence[torch.Tensor], Sequence[float], torch.Tensor], torch.Tensor]
+
+
+def bucket_bounds(n_elems: int, world: int, align_elems: int = 64) -> List[Tuple[int, int]]:
+    """Contiguous [start, end) buckets, one per rank; starts are multiples of
+    ``align_elems`` (16-byte aligned rows for the kernel); trailing buckets may be empty."""
+    if world < 1:
+        raise ValueError("world must be >= 1")
+    per = -(-n_elems // world) if n_elems else 0
+    per = -(-per // align_elems) * align_elems if per else 0
+    return [(min(r * per, n_elems), min((r + 1) * per, n_elems)) for r in range(world)]
+
+
+def _hip_reducer(peers, weights, out):
+    from accdfl_amd.core import wsum as _wsum
+
+    return _wsum.wsum(list(peers), weights, out=out)
+
+
+class BucketShardedFedAvg:
+    """FedAvg of an ``n_elems``-element flat model over the ranks of ``group``."""
+
+    def __init__(self, n_elems: int, dtype: torch.dtype, group: Optional[dist.ProcessGroup] = None,
+                 device: Optional[torch.device] = None, reducer: Optional[Reducer] = None):
+        self.group = group
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.n_elems = int(n_elems)
+        self.dtype = dtype
+        self.device = device if device is not None else torch.device("cpu")
+        esize = torch.empty((), dtype=dtype).element_size()
+        self.bounds = bucket_bounds(self.n_elems, self.world, max(1, _ALIGN_BYTES // esize))
+        start, end = self.bounds[0]
+        self.bucket_len = end - start  # every bucket is padded to this length for the collectives
+        self.reducer = reducer if reducer is not None else _hip_reducer
+
+    @property
+    def local_range(self) -> Tuple[int, int]:
+        return self.bounds[self.rank]
+
+    def reduce_bucket(self, peer_buckets: Sequence[torch.Tensor], weights: Optional[Sequence[float]] = None,
+                      out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """FedAvg of this rank's bucket of every peer (list order), padded to ``bucket_len``."""
+        n = len(peer_buckets)
+        if not weights:
+            weights = [float(1. / n) for _ in range(n)]
+        else:
+            assert len(weights) == n
+        start, end = self.local_range
+        m = end - start
+        if out is None:
+            out = torch.zeros(self.bucket_len, dtype=self.dtype, device=self.device)
+        if m > 0:
+            self.reducer([p[:m] for p in peer_buckets], weights, out[:m])
+        return out
+
+    def all_gather(self, bucket_out: torch.Tensor, full: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Reassemble the full averaged model on every rank (RCCL all-gather)."""
+        if bucket_out.numel() != self.bucket_len:
+            raise ValueError("bucket_out must hold bucket_len elements")
+        gathered = torch.empty(self.bucket_len * self.world, dtype=self.dtype, device=bucket_out.device)
+        if self.world == 1:
+            gathered.copy_(bucket_out)
+        else:
+            dist.all_gather_into_tensor(gathered, bucket_out.contiguous(), group=self.group)
+        if full is None:
+            return gathered[: self.n_elems]
+        full.copy_(gathered[: self.n_elems])
+        return full
+
+    def transpose_peer_sharded(self, local_peers: torch.Tensor) -> torch.Tensor:
+        """[m, n_elems] peers held by this rank -> [world * m, bucket_len] bucket rows of
+        ALL peers in global list order (rank r's peers are peers r*m .. r*m+m-1)."""
+        m = local_peers.shape[0]
+        padded = torch.zeros((m, self.world * self.bucket_len), dtype=self.dtype, device=local_peers.device)
+        padded[:, : self.n_elems] = local_peers
+        send = padded.view(m, self.world, self.bucket_len).transpose(0, 1).contiguous()  # [dest, m, len]
+        recv = torch.empty_like(send)  # [src, m, len]
+        if self.world == 1:
+            recv.copy_(send)
+        else:
+            dist.all_to_all_single(recv, send, group=self.group)
+        return recv.view(self.world * m, self.bucket_len)
+
+    def aggregate_peer_sharded(self, local_peers: torch.Tensor, weights: Optional[Sequence[float]] = None,
+                               gather: bool = True) -> torch.Tensor:
+        """Peers split across ranks -> all-to-all -> bucket reduce -> (all-gather)."""
+        rows = self.transpose_peer_sharded(local_peers)
+        out = self.reduce_bucket(list(rows), weights)
+        return self.all_gather(out) if gather else out

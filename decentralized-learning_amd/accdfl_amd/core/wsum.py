@@ -1,0 +1,135 @@
+"""Torch-facing wrappers of the libdlagg reduce (device tensors in, device tensors out).
+
+The arithmetic is the reference's FedAvg inner loop
+(accdfl/core/gradient_aggregation/fedavg.py:21-25) executed by the gfx950 kernel in
+csrc/dlagg.hip; these helpers only validate tensors, pick the stream and pass raw
+pointers across the C ABI.  Work is enqueued on the current HIP stream of the
+tensors' device and is NOT synchronised (torch stream semantics).
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Sequence
+
+import torch
+
+from .. import _lib
+
+_CODES = {
+    torch.float32: _lib.DLA_F32,
+    torch.bfloat16: _lib.DLA_BF16,
+    torch.float16: _lib.DLA_F16,
+    torch.float64: _lib.DLA_F64,
+}
+
+SUPPORTED_DTYPES = tuple(_CODES)
+
+
+def dtype_code(dtype: torch.dtype) -> int:
+    try:
+        return _CODES[dtype]
+    except KeyError:
+        raise TypeError("accdfl_amd FedAvg supports float32/bfloat16/float16/float64 parameters, got %s" % dtype)
+
+
+def require_device(device: Optional[torch.device] = None) -> torch.device:
+    """The HIP device the reduce runs on; raises when there is none (no CPU fallback)."""
+    if not torch.cuda.is_available():
+        raise RuntimeError("accdfl_amd: no HIP device visible — the aggregation reduce runs only on the GPU "
+                           "(MI355X); there is no CPU fallback")
+    if device is None or device.type != "cuda":
+        return torch.device("cuda", torch.cuda.current_device())
+    return device
+
+
+def _stream_ptr(device: torch.device, stream: Optional[torch.cuda.Stream]) -> int:
+    s = stream if stream is not None else torch.cuda.current_stream(device)
+    return int(s.cuda_stream)
+
+
+def _check_dev(t: torch.Tensor, device: torch.device, what: str):
+    if t.device != device:
+        raise ValueError("%s is on %s, expected %s" % (what, t.device, device))
+    if not t.is_contiguous():
+        raise ValueError("%s must be contiguous" % what)
+
+
+def wsum(peers: Sequence[torch.Tensor], weights: Sequence[float], out: Optional[torch.Tensor] = None,
+         stream: Optional[torch.cuda.Stream] = None, cfg: Optional[_lib.LaunchCfg] = None) -> torch.Tensor:
+    """out = FedAvg(peers, weights) element-wise, one device buffer per peer.
+
+    ``peers``: N contiguous device tensors of one dtype and numel (list order =
+    summation order); ``weights``: N numbers (already defaulted).  ``out`` may alias
+    ``peers[0]``.
+    """
+    n = len(peers)
+    if n < 1:
+        raise IndexError("list index out of range")
+    if len(weights) != n:
+        raise AssertionError("len(weights) != len(peers)")
+    p0 = peers[0]
+    device = require_device(p0.device)
+    code = dtype_code(p0.dtype)
+    numel = p0.numel()
+    for k, p in enumerate(peers):
+        _check_dev(p, device, "peer %d" % k)
+        if p.dtype != p0.dtype or p.numel() != numel:
+            raise ValueError("peer %d: dtype/numel %s/%d differs from peer 0 %s/%d" % (k, p.dtype, p.numel(),
+                                                                                        p0.dtype, numel))
+    if out is None:
+        out = torch.empty_like(p0)
+    _check_dev(out, device, "out")
+    if out.dtype != p0.dtype or out.numel() != numel:
+        raise ValueError("out dtype/numel mismatch")
+    _lib.wsum_ptrs(code, [p.data_ptr() for p in peers], weights, numel, out.data_ptr(),
+                   _stream_ptr(device, stream), cfg)
+    return out
+
+
+def wsum_rows(slab: torch.Tensor, weights: Sequence[float], n_elems: Optional[int] = None,
+              out: Optional[torch.Tensor] = None, stream: Optional[torch.cuda.Stream] = None) -> torch.Tensor:
+    """FedAvg over the first len(weights) rows of a 2-D device slab [rows, pitch]."""
+    if slab.dim() != 2 or slab.stride(1) != 1:
+        raise ValueError("slab must be a 2-D row-major tensor")
+    n = len(weights)
+    if n < 1 or n > slab.shape[0]:
+        raise ValueError("need 1 <= len(weights) <= slab rows")
+    device = require_device(slab.device)
+    if slab.device != device:
+        raise ValueError("slab is not on a HIP device")
+    code = dtype_code(slab.dtype)
+    n_elems = slab.shape[1] if n_elems is None else int(n_elems)
+    if out is None:
+        out = torch.empty(n_elems, dtype=slab.dtype, device=device)
+    _check_dev(out, device, "out")
+    if out.numel() < n_elems or out.dtype != slab.dtype:
+        raise ValueError("out too small or wrong dtype")
+    _lib.wsum_slab_ptr(code, slab.data_ptr(), slab.stride(0), weights, n, n_elems, out.data_ptr(),
+                       _stream_ptr(device, stream))
+    return out
+
+
+def wsum_multi(peer_params: Sequence[Sequence[torch.Tensor]], weights: Sequence[float],
+               outs: Sequence[torch.Tensor], stream: Optional[torch.cuda.Stream] = None) -> None:
+    """Multi-tensor FedAvg: outs[i] = FedAvg([peer_params[k][i] for k], weights).
+
+    All tensors device-resident and contiguous; outs[i] may alias peer_params[0][i].
+    One dtype per call (the caller groups tensors by dtype).
+    """
+    if not outs:
+        return
+    n = len(peer_params)
+    device = require_device(outs[0].device)
+    code = dtype_code(outs[0].dtype)
+    ptrs: List[int] = []
+    for i, o in enumerate(outs):
+        _check_dev(o, device, "out %d" % i)
+        if o.dtype != outs[0].dtype:
+            raise ValueError("wsum_multi: one dtype per call")
+        for k in range(n):
+            p = peer_params[k][i]
+            _check_dev(p, device, "peer %d tensor %d" % (k, i))
+            if p.numel() != o.numel() or p.dtype != o.dtype:
+                raise ValueError("peer %d tensor %d: numel/dtype mismatch" % (k, i))
+            ptrs.append(p.data_ptr())
+    _lib.wsum_multi_ptrs(code, ptrs, [o.data_ptr() for o in outs], [o.numel() for o in outs], weights,
+                         _stream_ptr(device, stream))

@@ -1,0 +1,517 @@
+// dlagg.hip — the accdfl FedAvg weighted N-peer reduce for MI355X (gfx950, CDNA4).
+//
+// Replaces the torch-CPU loop of accdfl/core/gradient_aggregation/fedavg.py:20-25:
+//     center = deepcopy(models[0]); p.mul_(0)           (:20-22)
+//     for m, w in zip(models, weights):                  (:23)
+//         for c1, p1 in zip(center.parameters(), m.parameters()):  (:24)
+//             c1.add_(w * p1)                            (:25)
+// as ONE streaming pass over HBM: every peer byte is read once, every output byte
+// written once, the running sum lives in VGPRs.  Per element the peers are folded
+// in list order with separately rounded multiply and add (no FMA), which is the
+// reference's rounding sequence bit for bit (see include/dlagg.h).
+//
+// Roofline: 2 flop per 4..8 B read -> far below the MFMA ridge; the kernel is
+// HBM-bound and deliberately has no MFMA.  Algorithmic bytes per launch =
+// (n_peers + 1) * n_elems * sizeof(T).
+//
+// Layout of the work: one 16-byte chunk per lane per peer (global_load_dwordx4,
+// 1 KiB per wave instruction, fully coalesced), CH chunks per lane per tile,
+// peers loaded in groups of 8 so each lane keeps 8*CH*16 B in flight before the
+// first add.  Variant 3 stages each peer group's tile through LDS with
+// global_load_lds_dwordx4 (LDS-DMA: no VGPR landing, deeper MLP per wave), then
+// folds it in list order from LDS.
+//
+// Compiled with -ffp-contract=off; the pragma below repeats it so no build line
+// can re-enable FMA contraction for these functions.
+#pragma clang fp contract(off)
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstring>
+#include <string>
+
+#include "dlagg.h"
+
+namespace {
+
+constexpr int kBlock = 256;           // 4 waves of 64 lanes
+constexpr int kGroup = 8;             // peers loaded together before folding
+constexpr int kMaxPeersPerPass = 128; // pointer table in the kernel-argument block
+
+thread_local std::string g_last_error;
+
+int fail(int code, const std::string& msg) {
+  g_last_error = msg;
+  return code;
+}
+
+// ---------------------------------------------------------------- element ops
+// One 16-byte chunk = E elements.  acc_t is the op-math type; values of acc are
+// always exactly representable in the storage dtype (the reference stores the
+// running sum in the parameter tensor after every add).
+
+template <int DT> struct Ops;
+
+template <> struct Ops<DLA_F32> {
+  using acc_t = float;
+  using w_t = float;
+  using elem_t = float;
+  static constexpr int E = 4;
+  __device__ static void unpack(const uint4& v, acc_t* x) {
+    x[0] = __uint_as_float(v.x); x[1] = __uint_as_float(v.y);
+    x[2] = __uint_as_float(v.z); x[3] = __uint_as_float(v.w);
+  }
+  __device__ static uint4 pack(const acc_t* a) {
+    return make_uint4(__float_as_uint(a[0]), __float_as_uint(a[1]),
+                      __float_as_uint(a[2]), __float_as_uint(a[3]));
+  }
+  __device__ static acc_t to_acc(elem_t e) { return e; }
+  __device__ static elem_t from_acc(acc_t a) { return a; }
+  __device__ static acc_t zero_mul(acc_t x) { return x * 0.0f; }                 // fedavg.py:22
+  __device__ static acc_t step(acc_t acc, w_t w, acc_t x) { return acc + w * x; } // fedavg.py:25
+};
+
+template <> struct Ops<DLA_F64> {
+  using acc_t = double;
+  using w_t = double;
+  using elem_t = double;
+  static constexpr int E = 2;
+  __device__ static void unpack(const uint4& v, acc_t* x) {
+    x[0] = __hiloint2double(v.y, v.x);
+    x[1] = __hiloint2double(v.w, v.z);
+  }
+  __device__ static uint4 pack(const acc_t* a) {
+    return make_uint4(__double2loint(a[0]), __double2hiint(a[0]),
+                      __double2loint(a[1]), __double2hiint(a[1]));
+  }
+  __device__ static acc_t to_acc(elem_t e) { return e; }
+  __device__ static elem_t from_acc(acc_t a) { return a; }
+  __device__ static acc_t zero_mul(acc_t x) { return x * 0.0; }
+  __device__ static acc_t step(acc_t acc, w_t w, acc_t x) { return acc + w * x; }
+};
+
+// bf16: op-math float, every product and every sum rounded RNE to bf16
+// (torch-CPU reduced-float kernels: float(a) * float(w) -> bf16; float(c) + float(t) -> bf16).
+__device__ inline float bf16_bits_to_f(uint32_t h) { return __uint_as_float(h << 16); }
+__device__ inline float round_bf16(float f) {
+  // Plain cast: v_cvt_pk_bf16_f32 on gfx950, round-to-nearest-even, NaN stays NaN.
+  __bf16 b = static_cast<__bf16>(f);
+  return static_cast<float>(b);
+}
+
+template <> struct Ops<DLA_BF16> {
+  using acc_t = float;
+  using w_t = float;
+  using elem_t = uint16_t;
+  static constexpr int E = 8;
+  __device__ static void unpack(const uint4& v, acc_t* x) {
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      x[2 * i] = __uint_as_float(w[i] << 16);
+      x[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+    }
+  }
+  // acc values are exact bf16 values: their upper 16 bits are the bf16 bits.
+  __device__ static uint4 pack(const acc_t* a) {
+    uint32_t w[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      w[i] = (__float_as_uint(a[2 * i]) >> 16) | (__float_as_uint(a[2 * i + 1]) & 0xffff0000u);
+    return make_uint4(w[0], w[1], w[2], w[3]);
+  }
+  __device__ static acc_t to_acc(elem_t e) { return bf16_bits_to_f(e); }
+  __device__ static elem_t from_acc(acc_t a) { return static_cast<uint16_t>(__float_as_uint(a) >> 16); }
+  __device__ static acc_t zero_mul(acc_t x) { return x * 0.0f; }  // +-0 or NaN: already bf16-exact
+  __device__ static acc_t step(acc_t acc, w_t w, acc_t x) {
+    return round_bf16(acc + round_bf16(w * x));
+  }
+};
+
+__device__ inline float half_bits_to_f(uint32_t h) {
+  _Float16 v;
+  uint16_t s = static_cast<uint16_t>(h);
+  __builtin_memcpy(&v, &s, 2);
+  return static_cast<float>(v);
+}
+__device__ inline uint32_t f_to_half_bits(float f) {
+  _Float16 v = static_cast<_Float16>(f);  // RNE
+  uint16_t s;
+  __builtin_memcpy(&s, &v, 2);
+  return s;
+}
+// The empty asm pins the op-math product/sum as a rounded f32 in a VGPR before the
+// f16 rounding: without it the backend folds fptrunc(fmul) into one
+// v_fma_mixlo_f16 (a single rounding), which differs from the reference's
+// f32-then-f16 double rounding on rare ties.
+__device__ inline float pin(float f) {
+  asm("" : "+v"(f));
+  return f;
+}
+__device__ inline float round_f16(float f) { return static_cast<float>(static_cast<_Float16>(pin(f))); }
+
+template <> struct Ops<DLA_F16> {
+  using acc_t = float;
+  using w_t = float;
+  using elem_t = uint16_t;
+  static constexpr int E = 8;
+  __device__ static void unpack(const uint4& v, acc_t* x) {
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      x[2 * i] = half_bits_to_f(w[i] & 0xffffu);
+      x[2 * i + 1] = half_bits_to_f(w[i] >> 16);
+    }
+  }
+  __device__ static uint4 pack(const acc_t* a) {
+    uint32_t w[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) w[i] = f_to_half_bits(a[2 * i]) | (f_to_half_bits(a[2 * i + 1]) << 16);
+    return make_uint4(w[0], w[1], w[2], w[3]);
+  }
+  __device__ static acc_t to_acc(elem_t e) { return half_bits_to_f(e); }
+  __device__ static elem_t from_acc(acc_t a) { return static_cast<uint16_t>(f_to_half_bits(a)); }
+  __device__ static acc_t zero_mul(acc_t x) { return x * 0.0f; }  // +-0 or NaN: already f16-exact
+  __device__ static acc_t step(acc_t acc, w_t w, acc_t x) { return round_f16(acc + round_f16(w * x)); }
+};
+
+// ------------------------------------------------------------ kernel arguments
+
+template <typename W, int KMAX>
+struct PeerTable {
+  const void* p[KMAX];
+  W w[KMAX];
+};
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+template <bool NT>
+__device__ inline uint4 load16(const uint4* p) {
+  const u32x4* q = reinterpret_cast<const u32x4*>(p);
+  u32x4 v;
+  if constexpr (NT) {
+    v = __builtin_nontemporal_load(q);  // global_load_dwordx4 ... nt
+  } else {
+    v = *q;
+  }
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+// ------------------------------------------------ register-stream kernel (v1/v2)
+//
+// Tile = kBlock * CH chunks; lane l of the block owns chunks tile_base + c*kBlock + l.
+// ACC_IN: the running sum starts from `out` (second and later passes of a
+// reduce with more than KMAX peers) instead of p0 * 0.
+template <int DT, int KMAX, int CH, bool NT, bool ACC_IN>
+__global__ __launch_bounds__(kBlock) void wsum_stream_kernel(
+    const PeerTable<typename Ops<DT>::w_t, KMAX> tab, int n_peers, int64_t n_chunks,
+    int64_t n_elems, void* __restrict__ out_v) {
+  using O = Ops<DT>;
+  using acc_t = typename O::acc_t;
+  using elem_t = typename O::elem_t;
+  constexpr int E = O::E;
+  uint4* __restrict__ out = static_cast<uint4*>(out_v);
+  const int64_t tile_chunks = static_cast<int64_t>(kBlock) * CH;
+  const int64_t n_tiles = (n_chunks + tile_chunks - 1) / tile_chunks;
+
+  for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
+    const int64_t base = tile * tile_chunks + threadIdx.x;
+    // Lanes past the end of the last (partial) tile load a clamped, valid chunk
+    // and skip the store: loads stay unpredicated, so a group's 8*CH loads all
+    // issue before the first wait.
+    bool live[CH];
+    int64_t idx[CH];
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      live[c] = base + c * kBlock < n_chunks;
+      idx[c] = live[c] ? base + c * kBlock : n_chunks - 1;
+    }
+
+    acc_t acc[CH][E];
+    int k0 = 0;
+    if constexpr (ACC_IN) {
+#pragma unroll
+      for (int c = 0; c < CH; ++c) {
+        O::unpack(out[idx[c]], acc[c]);
+      }
+    }
+    // Full groups of kGroup peers: all loads of the group issue before the first add.
+    for (; k0 + kGroup <= n_peers; k0 += kGroup) {
+      uint4 v[kGroup][CH];
+#pragma unroll
+      for (int g = 0; g < kGroup; ++g) {
+        const uint4* src = static_cast<const uint4*>(tab.p[k0 + g]);
+#pragma unroll
+        for (int c = 0; c < CH; ++c)
+          v[g][c] = load16<NT>(src + idx[c]);
+      }
+#pragma unroll
+      for (int g = 0; g < kGroup; ++g) {
+        const typename O::w_t w = tab.w[k0 + g];
+#pragma unroll
+        for (int c = 0; c < CH; ++c) {
+          acc_t x[E];
+          O::unpack(v[g][c], x);
+#pragma unroll
+          for (int e = 0; e < E; ++e) {
+            if (!ACC_IN && g == 0 && k0 == 0) acc[c][e] = O::zero_mul(x[e]);
+            acc[c][e] = O::step(acc[c][e], w, x[e]);
+          }
+        }
+      }
+    }
+    // Remaining peers (< kGroup), one at a time, same order.
+    for (; k0 < n_peers; ++k0) {
+      const uint4* src = static_cast<const uint4*>(tab.p[k0]);
+      const typename O::w_t w = tab.w[k0];
+      uint4 v[CH];
+#pragma unroll
+      for (int c = 0; c < CH; ++c)
+        v[c] = load16<NT>(src + idx[c]);
+#pragma unroll
+      for (int c = 0; c < CH; ++c) {
+        acc_t x[E];
+        O::unpack(v[c], x);
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          if (!ACC_IN && k0 == 0) acc[c][e] = O::zero_mul(x[e]);
+          acc[c][e] = O::step(acc[c][e], w, x[e]);
+        }
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < CH; ++c)
+        if (live[c]) out[idx[c]] = O::pack(acc[c]);
+  }
+
+  // Ragged tail (n_elems not a multiple of E): one element per lane of block 0.
+  const int64_t tail0 = n_chunks * E;
+  if (blockIdx.x == 0 && tail0 + threadIdx.x < n_elems) {
+    const int64_t j = tail0 + threadIdx.x;
+    elem_t* o = static_cast<elem_t*>(out_v);
+    acc_t acc = ACC_IN ? O::to_acc(o[j]) : acc_t(0);
+    for (int k = 0; k < n_peers; ++k) {
+      const acc_t x = O::to_acc(static_cast<const elem_t*>(tab.p[k])[j]);
+      if (!ACC_IN && k == 0) acc = O::zero_mul(x);
+      acc = O::step(acc, tab.w[k], x);
+    }
+    o[j] = O::from_acc(acc);
+  }
+}
+
+// ---------------------------------------------------- scalar kernel (unaligned)
+// Any alignment; one element per lane, grid-stride.  Used only when a buffer is
+// not 16-byte aligned (e.g. an odd-offset view).
+template <int DT, int KMAX, bool ACC_IN>
+__global__ __launch_bounds__(kBlock) void wsum_scalar_kernel(
+    const PeerTable<typename Ops<DT>::w_t, KMAX> tab, int n_peers, int64_t n_elems,
+    void* __restrict__ out_v) {
+  using O = Ops<DT>;
+  using acc_t = typename O::acc_t;
+  using elem_t = typename O::elem_t;
+  elem_t* o = static_cast<elem_t*>(out_v);
+  for (int64_t j = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; j < n_elems;
+       j += static_cast<int64_t>(gridDim.x) * kBlock) {
+    acc_t acc = ACC_IN ? O::to_acc(o[j]) : acc_t(0);
+    for (int k = 0; k < n_peers; ++k) {
+      const acc_t x = O::to_acc(static_cast<const elem_t*>(tab.p[k])[j]);
+      if (!ACC_IN && k == 0) acc = O::zero_mul(x);
+      acc = O::step(acc, tab.w[k], x);
+    }
+    o[j] = O::from_acc(acc);
+  }
+}
+
+// ------------------------------------------------------------------ launching
+
+struct Launch {
+  int variant;
+  int chunks;
+  int grid_blocks;
+};
+
+Launch resolve(const dla_launch_cfg_t* cfg) {
+  Launch l{2, 1, 0};  // default: register stream, nt loads, 1 chunk/lane, 1 WG per tile
+  if (cfg) {
+    if (cfg->variant) l.variant = cfg->variant;
+    if (cfg->chunks) l.chunks = cfg->chunks;
+    l.grid_blocks = cfg->grid_blocks;
+  }
+  return l;
+}
+
+template <int DT, int KMAX, int CH, bool NT, bool ACC_IN>
+hipError_t launch_stream(const PeerTable<typename Ops<DT>::w_t, KMAX>& tab, int n, int64_t n_elems,
+                         void* out, hipStream_t s, int grid_blocks) {
+  constexpr int E = Ops<DT>::E;
+  const int64_t n_chunks = n_elems / E;
+  const int64_t tile_chunks = static_cast<int64_t>(kBlock) * CH;
+  int64_t tiles = (n_chunks + tile_chunks - 1) / tile_chunks;
+  if (tiles < 1) tiles = 1;  // block 0 still handles the ragged tail
+  int64_t grid = grid_blocks > 0 ? grid_blocks : tiles;
+  if (grid > tiles) grid = tiles;
+  if (grid > 0x7fffffff) grid = 0x7fffffff;
+  hipLaunchKernelGGL((wsum_stream_kernel<DT, KMAX, CH, NT, ACC_IN>), dim3(static_cast<unsigned>(grid)),
+                     dim3(kBlock), 0, s, tab, n, n_chunks, n_elems, out);
+  return hipGetLastError();
+}
+
+template <int DT, int KMAX, bool ACC_IN>
+hipError_t launch_pass(const PeerTable<typename Ops<DT>::w_t, KMAX>& tab, int n, int64_t n_elems,
+                       void* out, hipStream_t s, const Launch& l, bool aligned) {
+  if (!aligned) {
+    int64_t blocks = (n_elems + kBlock - 1) / kBlock;
+    if (blocks > 8192) blocks = 8192;
+    if (blocks < 1) blocks = 1;
+    hipLaunchKernelGGL((wsum_scalar_kernel<DT, KMAX, ACC_IN>), dim3(static_cast<unsigned>(blocks)),
+                       dim3(kBlock), 0, s, tab, n, n_elems, out);
+    return hipGetLastError();
+  }
+  const bool nt = l.variant == 2;
+  switch (l.chunks) {
+    case 1:
+      return nt ? launch_stream<DT, KMAX, 1, true, ACC_IN>(tab, n, n_elems, out, s, l.grid_blocks)
+                : launch_stream<DT, KMAX, 1, false, ACC_IN>(tab, n, n_elems, out, s, l.grid_blocks);
+    case 2:
+      return nt ? launch_stream<DT, KMAX, 2, true, ACC_IN>(tab, n, n_elems, out, s, l.grid_blocks)
+                : launch_stream<DT, KMAX, 2, false, ACC_IN>(tab, n, n_elems, out, s, l.grid_blocks);
+    case 4:
+      return nt ? launch_stream<DT, KMAX, 4, true, ACC_IN>(tab, n, n_elems, out, s, l.grid_blocks)
+                : launch_stream<DT, KMAX, 4, false, ACC_IN>(tab, n, n_elems, out, s, l.grid_blocks);
+    default:
+      return hipErrorInvalidValue;
+  }
+}
+
+template <int DT, int KMAX>
+hipError_t run_pass(const void* const* peers, const double* weights, int n, int64_t n_elems,
+                    void* out, hipStream_t s, const Launch& l, bool acc_in) {
+  using W = typename Ops<DT>::w_t;
+  PeerTable<W, KMAX> tab;
+  std::memset(&tab, 0, sizeof(tab));
+  bool aligned = (reinterpret_cast<uintptr_t>(out) & 15u) == 0;
+  for (int k = 0; k < n; ++k) {
+    tab.p[k] = peers[k];
+    tab.w[k] = static_cast<W>(weights[k]);  // RNE double -> op-math (fedavg.py:25 `w * p1`)
+    aligned = aligned && (reinterpret_cast<uintptr_t>(peers[k]) & 15u) == 0;
+  }
+  return acc_in ? launch_pass<DT, KMAX, true>(tab, n, n_elems, out, s, l, aligned)
+                : launch_pass<DT, KMAX, false>(tab, n, n_elems, out, s, l, aligned);
+}
+
+template <int DT>
+hipError_t run(const void* const* peers, const double* weights, int n, int64_t n_elems, void* out,
+               hipStream_t s, const Launch& l) {
+  // Passes of at most kMaxPeersPerPass peers; pass j > 0 folds its peers into
+  // the running sum held in `out`, so the list order is kept exactly.
+  for (int k0 = 0; k0 < n; k0 += kMaxPeersPerPass) {
+    const int m = n - k0 < kMaxPeersPerPass ? n - k0 : kMaxPeersPerPass;
+    hipError_t e;
+    if (m <= 8)
+      e = run_pass<DT, 8>(peers + k0, weights + k0, m, n_elems, out, s, l, k0 > 0);
+    else if (m <= 32)
+      e = run_pass<DT, 32>(peers + k0, weights + k0, m, n_elems, out, s, l, k0 > 0);
+    else
+      e = run_pass<DT, kMaxPeersPerPass>(peers + k0, weights + k0, m, n_elems, out, s, l, k0 > 0);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+int elem_size(int dtype) {
+  switch (dtype) {
+    case DLA_F32: return 4;
+    case DLA_BF16: return 2;
+    case DLA_F16: return 2;
+    case DLA_F64: return 8;
+    default: return 0;
+  }
+}
+
+int wsum_impl(int dtype, const void* const* peers, const double* weights, int n_peers,
+              int64_t n_elems, void* out, void* stream, const dla_launch_cfg_t* cfg) {
+  g_last_error.clear();
+  if (elem_size(dtype) == 0) return fail(DLA_E_INVALID, "dla_wsum: unknown dtype " + std::to_string(dtype));
+  if (n_peers < 1) return fail(DLA_E_INVALID, "dla_wsum: n_peers must be >= 1 (fedavg.py:20 indexes models[0])");
+  if (n_elems < 0) return fail(DLA_E_INVALID, "dla_wsum: n_elems < 0");
+  if (!peers || !weights) return fail(DLA_E_INVALID, "dla_wsum: null peers/weights array");
+  if (n_elems == 0) return DLA_OK;
+  if (!out) return fail(DLA_E_INVALID, "dla_wsum: null out");
+  for (int k = 0; k < n_peers; ++k)
+    if (!peers[k]) return fail(DLA_E_INVALID, "dla_wsum: null peer pointer " + std::to_string(k));
+  if (n_peers > kMaxPeersPerPass) {
+    // Multi-pass reduce: out carries the running sum, so it may alias only peers[0].
+    for (int k = 1; k < n_peers; ++k)
+      if (peers[k] == out)
+        return fail(DLA_E_ALIAS, "dla_wsum: out aliases peer " + std::to_string(k) +
+                                     "; only peers[0] may alias out when n_peers > " +
+                                     std::to_string(kMaxPeersPerPass));
+  }
+  const Launch l = resolve(cfg);
+  if (l.variant < 1 || l.variant > 2)
+    return fail(DLA_E_CONFIG, "dla_wsum: unsupported variant " + std::to_string(l.variant));
+  if (l.chunks != 1 && l.chunks != 2 && l.chunks != 4)
+    return fail(DLA_E_CONFIG, "dla_wsum: chunks must be 1, 2 or 4");
+  if (l.grid_blocks < 0) return fail(DLA_E_CONFIG, "dla_wsum: grid_blocks < 0");
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  hipError_t e;
+  switch (dtype) {
+    case DLA_F32: e = run<DLA_F32>(peers, weights, n_peers, n_elems, out, s, l); break;
+    case DLA_BF16: e = run<DLA_BF16>(peers, weights, n_peers, n_elems, out, s, l); break;
+    case DLA_F16: e = run<DLA_F16>(peers, weights, n_peers, n_elems, out, s, l); break;
+    default: e = run<DLA_F64>(peers, weights, n_peers, n_elems, out, s, l); break;
+  }
+  if (e != hipSuccess) return fail(static_cast<int>(e), std::string("dla_wsum: ") + hipGetErrorString(e));
+  return DLA_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int dla_version(void) { return DLA_ABI_VERSION; }
+
+const char* dla_last_error(void) { return g_last_error.c_str(); }
+
+int dla_max_peers_per_pass(void) { return kMaxPeersPerPass; }
+
+int dla_wsum(int dtype, const void* const* peers, const double* weights, int n_peers, int64_t n_elems,
+             void* out, void* stream) {
+  return wsum_impl(dtype, peers, weights, n_peers, n_elems, out, stream, nullptr);
+}
+
+int dla_wsum_ex(int dtype, const void* const* peers, const double* weights, int n_peers,
+                int64_t n_elems, void* out, void* stream, const dla_launch_cfg_t* cfg) {
+  return wsum_impl(dtype, peers, weights, n_peers, n_elems, out, stream, cfg);
+}
+
+int dla_wsum_slab(int dtype, const void* base, int64_t pitch_elems, const double* weights, int n_peers,
+                  int64_t n_elems, void* out, void* stream) {
+  g_last_error.clear();
+  const int es = elem_size(dtype);
+  if (es == 0) return fail(DLA_E_INVALID, "dla_wsum_slab: unknown dtype");
+  if (!base || n_peers < 1 || pitch_elems < n_elems)
+    return fail(DLA_E_INVALID, "dla_wsum_slab: need base, n_peers >= 1 and pitch_elems >= n_elems");
+  std::string ptrs;  // small host table of row pointers
+  ptrs.resize(sizeof(void*) * static_cast<size_t>(n_peers));
+  const void** rows = reinterpret_cast<const void**>(&ptrs[0]);
+  for (int k = 0; k < n_peers; ++k)
+    rows[k] = static_cast<const char*>(base) + static_cast<int64_t>(k) * pitch_elems * es;
+  return wsum_impl(dtype, rows, weights, n_peers, n_elems, out, stream, nullptr);
+}
+
+int dla_wsum_multi(int dtype, int n_tensors, const void* const* peer_ptrs, void* const* outs,
+                   const int64_t* numels, const double* weights, int n_peers, void* stream) {
+  g_last_error.clear();
+  if (n_tensors < 0 || (n_tensors > 0 && (!peer_ptrs || !outs || !numels)))
+    return fail(DLA_E_INVALID, "dla_wsum_multi: bad tensor table");
+  for (int t = 0; t < n_tensors; ++t) {
+    const int rc = wsum_impl(dtype, peer_ptrs + static_cast<int64_t>(t) * n_peers, weights, n_peers,
+                             numels[t], outs[t], stream, nullptr);
+    if (rc != DLA_OK) return rc;
+  }
+  return DLA_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,108 @@
+/*
+ * dlagg.h — C ABI of libdlagg.so, the MI355X (gfx950) implementation of the
+ * accdfl gossip model-aggregation reduce (FedAvg).
+ *
+ * Reference interface replaced:
+ *   accdfl/core/gradient_aggregation/fedavg.py:12-26   FedAvg.aggregate(models, weights)
+ *     - :14-17  weight defaulting (falsy -> uniform 1/N) / length assertion
+ *     - :20-22  center = deepcopy(models[0]); p.mul_(0)       -> acc = p0 * 0
+ *     - :23-25  for m, w: c1.add_(w * p1)                      -> acc = acc + w_k * p_k
+ *   accdfl/core/gradient_aggregation/__init__.py:12-17 GradientAggregation.aggregate
+ *   accdfl/core/model_manager.py:56-58 aggregate_trained_models (list order = summation order)
+ *
+ * The reference has no native code; there is no FFI to bind in it.  The Python
+ * host package (decentralized-learning_amd/accdfl_amd) binds these entry points
+ * with ctypes; INTEGRATION.md shows the binding a maintainer would add to the
+ * reference tree.
+ *
+ * Arithmetic contract ("bit-exact mode", the only mode): for every element j
+ *     acc = p_0[j] * 0                       (keeps -0, turns +-Inf/NaN into NaN)
+ *     for k = 0 .. n_peers-1 (list order):
+ *         acc = R(acc + R(W(w_k) * p_k[j]))
+ * with no fused multiply-add.  W(w) is the weight rounded RNE from double to the
+ * dtype's op-math type (float for F32/BF16/F16, double for F64).  R() is the
+ * op-math result rounded RNE to the storage dtype (identity for F32/F64).  This
+ * equals torch-CPU's `c.add_(w * p)` sequence bit for bit; NaN payload bits are
+ * not part of the contract (torch-CPU itself emits different NaN payloads
+ * depending on vector-lane position).
+ *
+ * Ownership: the caller owns every buffer (device pointers from hipMalloc / the
+ * torch caching allocator).  The library keeps no device allocation across calls.
+ * Errors: return 0 on success, a negative DLA_E_* code or a positive hipError_t;
+ * dla_last_error() returns a thread-local message.  No C++ exception crosses the ABI.
+ * Threading: reentrant; work is enqueued on `stream` (a hipStream_t, NULL = the
+ * default stream) and the call does not synchronise.
+ */
+#ifndef DLAGG_H
+#define DLAGG_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DLA_ABI_VERSION 1
+
+/* element dtypes of the peer buffers and of the output */
+#define DLA_F32 0
+#define DLA_BF16 1
+#define DLA_F16 2
+#define DLA_F64 3
+
+/* error codes (negative; positive values are hipError_t) */
+#define DLA_OK 0
+#define DLA_E_INVALID (-1)    /* bad argument (null pointer, n_peers < 1, n_elems < 0, dtype) */
+#define DLA_E_ALIAS (-2)      /* out aliases a peer other than peers[0] in a multi-pass reduce */
+#define DLA_E_CONFIG (-3)     /* launch configuration not supported */
+
+/* Launch tuning knobs for dla_wsum_ex (0 = library default for each field). */
+typedef struct dla_launch_cfg {
+  int variant;      /* 0 = default, 1 = register stream, 2 = register stream + nt loads,
+                       3 = LDS-DMA staged stream                                       */
+  int chunks;       /* 16-byte chunks per thread per peer per iteration (1, 2 or 4)   */
+  int grid_blocks;  /* workgroups; 0 = one per work tile (no grid-stride loop)        */
+} dla_launch_cfg_t;
+
+/* ABI version (DLA_ABI_VERSION). */
+int dla_version(void);
+
+/* Message describing the last error on this thread ("" if none). */
+const char* dla_last_error(void);
+
+/* Replaces fedavg.py:20-25 for one flat parameter buffer per peer.
+ *   peers    host array of n_peers DEVICE pointers, each to n_elems elements of dtype
+ *   weights  host array of n_peers doubles (already defaulted, fedavg.py:14-17)
+ *   out      DEVICE pointer to n_elems elements; may alias peers[0]
+ * Any n_peers >= 1 is accepted (more than DLA_MAX_PEERS_PER_PASS peers run as
+ * several passes that carry the running sum in `out`, which keeps list order). */
+int dla_wsum(int dtype, const void* const* peers, const double* weights, int n_peers,
+             int64_t n_elems, void* out, void* stream);
+
+/* dla_wsum with explicit launch knobs (benchmarks / tuning). */
+int dla_wsum_ex(int dtype, const void* const* peers, const double* weights, int n_peers,
+                int64_t n_elems, void* out, void* stream, const dla_launch_cfg_t* cfg);
+
+/* Peers stored as rows of one slab: peer k = base + k * pitch_elems elements.
+ * This is the layout of the device staging slab (accdfl_amd PeerSlab). */
+int dla_wsum_slab(int dtype, const void* base, int64_t pitch_elems, const double* weights,
+                  int n_peers, int64_t n_elems, void* out, void* stream);
+
+/* Replaces the per-parameter inner loop of fedavg.py:24-25 for T parameter
+ * tensors at once (one model = T tensors, parameters() order).
+ *   peer_ptrs host array [n_tensors * n_peers]: peer_ptrs[t * n_peers + k] is
+ *             peer k's DEVICE pointer for tensor t
+ *   outs      host array [n_tensors] of DEVICE output pointers
+ *   numels    host array [n_tensors] of element counts
+ * Tensors are packed into as few launches as the kernel-argument block allows. */
+int dla_wsum_multi(int dtype, int n_tensors, const void* const* peer_ptrs, void* const* outs,
+                   const int64_t* numels, const double* weights, int n_peers, void* stream);
+
+/* Largest peer count one kernel pass takes (kernel-argument pointer table). */
+int dla_max_peers_per_pass(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* DLAGG_H */

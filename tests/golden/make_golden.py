@@ -1,0 +1,190 @@
+"""Generate the golden FedAvg vectors from the REFERENCE implementation.
+
+Run in the build container only (the reference tree does not exist on the GPU box):
+
+    PYTHONDONTWRITEBYTECODE=1 PYTHONPATH=/root/reference python3 tests/golden/make_golden.py
+
+It imports ``accdfl.core.gradient_aggregation.fedavg.FedAvg``
+(/root/reference/accdfl/core/gradient_aggregation/fedavg.py:12-26), runs it on seeded
+synthetic peer models and stores inputs and outputs as raw bit patterns in
+``tests/golden/<case>.npz``.  Only data is committed — no reference source, bytecode
+or pickled reference objects.
+
+Each case file holds:
+  meta        JSON: name, dtype, n_peers, per-model parameter shapes, buffer shapes,
+              weights (list of numbers, or null for the reference default)
+  p_{k}_{i}   peer k, parameter i (raw bits: uint32 f32, uint16 bf16/f16, uint64 f64)
+  b_{k}_{j}   peer k, buffer j (not averaged: copied from models[0], fedavg.py:20)
+  out_{i}     reference output parameter i (raw bits)
+  outb_{j}    reference output buffer j
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+from torch import nn
+
+from accdfl.core.gradient_aggregation.fedavg import FedAvg  # the reference, via PYTHONPATH
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+TORCH_DT = {"f32": torch.float32, "bf16": torch.bfloat16, "f16": torch.float16, "f64": torch.float64}
+BITS_DT = {"f32": torch.int32, "bf16": torch.int16, "f16": torch.int16, "f64": torch.int64}
+NP_BITS = {"f32": np.uint32, "bf16": np.uint16, "f16": np.uint16, "f64": np.uint64}
+
+# Parameter layouts of the reference models named by BASELINE.json's configs
+# (shapes read from accdfl/core/models/{linear,cifar10,femnist,resnet_speech}.py).
+SPAMBASE = [(2, 57), (2,)]
+GNLENET = [(32, 3, 5, 5), (32,), (32,), (32,), (32, 32, 5, 5), (32,), (32,), (32,), (64, 32, 5, 5), (64,),
+           (64,), (64,), (10, 576), (10,)]
+FEMNIST_SLICE = [(32, 1, 5, 5), (32,), (512,), (62,)]          # conv1.w/b, fc1.b, fc2.b
+SPEECH_SLICE = [(64, 1, 7, 7), (64,), (64,), (64,)]             # conv1.w, bn1.w/b, layer1.0.bn1.w
+GNLENET_SMALL = [s for s in GNLENET if s not in [(32, 32, 5, 5), (64, 32, 5, 5)]]
+
+
+class Peer(nn.Module):
+    """A model with the given parameter shapes (and optional buffers)."""
+
+    def __init__(self, shapes, dtype, buffers=()):
+        super().__init__()
+        self.ps = nn.ParameterList([nn.Parameter(torch.zeros(s, dtype=dtype)) for s in shapes])
+        for j, (s, bdt) in enumerate(buffers):
+            self.register_buffer("b%d" % j, torch.zeros(s, dtype=bdt))
+
+
+def to_bits(t: torch.Tensor, dt: str) -> np.ndarray:
+    return t.detach().contiguous().view(BITS_DT[dt]).numpy().view(NP_BITS[dt]).copy()
+
+
+def make_peers(n, shapes_per_model, dt, seed, fill=None, buffers=()):
+    models = []
+    for k in range(n):
+        g = torch.Generator().manual_seed(seed + k)
+        m = Peer(shapes_per_model[k], TORCH_DT[dt], buffers)
+        with torch.no_grad():
+            for i, p in enumerate(m.ps):
+                v = torch.randn(p.shape, generator=g, dtype=torch.float64) * 0.05
+                if fill is not None:
+                    v = fill(k, i, v, g)
+                p.copy_(v.to(TORCH_DT[dt]))
+            for b in m.buffers():
+                if b.dtype.is_floating_point:
+                    b.copy_(torch.randn(b.shape, generator=g))
+                else:
+                    b.fill_(k + 7)
+        models.append(m)
+    return models
+
+
+def save_case(name, dt, models, weights):
+    out = FedAvg.aggregate(models, weights)
+    arrays = {}
+    for k, m in enumerate(models):
+        for i, p in enumerate(m.parameters()):
+            arrays["p_%d_%d" % (k, i)] = to_bits(p, dt)
+        for j, b in enumerate(m.buffers()):
+            arrays["b_%d_%d" % (k, j)] = b.detach().numpy().copy()
+    for i, p in enumerate(out.parameters()):
+        arrays["out_%d" % i] = to_bits(p, dt)
+    for j, b in enumerate(out.buffers()):
+        arrays["outb_%d" % j] = b.detach().numpy().copy()
+    meta = {
+        "name": name,
+        "dtype": dt,
+        "n_peers": len(models),
+        "shapes": [[list(p.shape) for p in m.parameters()] for m in models],
+        "buffers": [[list(b.shape), str(b.dtype).replace("torch.", "")] for b in models[0].buffers()],
+        "weights": None if weights is None else [w if isinstance(w, int) else float(w) for w in weights],
+        "requires_grad": [bool(p.requires_grad) for p in out.parameters()],
+    }
+    arrays["meta"] = np.array(json.dumps(meta))
+    path = os.path.join(HERE, name + ".npz")
+    np.savez_compressed(path, **arrays)
+    size = os.path.getsize(path)
+    print("%-28s dtype=%-4s N=%-3d params=%-8d %7.1f KiB" % (
+        name, dt, len(models), sum(p.numel() for p in models[0].parameters()), size / 1024))
+
+
+def dirichlet(n, seed=0):
+    return [float(x) for x in np.random.default_rng(seed).dirichlet(np.ones(n))]
+
+
+def specials(k, i, v, g):
+    """Signed zeros, NaN, +-Inf, subnormals, overflow-prone magnitudes at fixed spots."""
+    shape = v.shape
+    v = v.clone().reshape(-1)
+    if v.numel() >= 16:
+        v[0] = -0.0                          # -0 * 0 = -0 init (fedavg.py:22)
+        v[1] = 0.0
+        v[2] = float("inf") if k == 0 else 1.0   # inf * 0 = NaN init for peer 0
+        v[3] = float("nan") if k == 1 else 2.0
+        v[4] = float("-inf") if k == 2 else -1.0
+        v[5] = 1e-41 * (k + 1)               # f32 subnormal
+        v[6] = 3.0e38                        # f32 overflow in the sum
+        v[7] = -3.0e38 if k % 2 else 3.0e38
+        v[8] = 1.0e-45                       # smallest f32 subnormal
+        v[9] = -0.0                          # all -0 -> stays -0 only if every product is -0
+        v[10] = 9.2e-41                      # bf16 subnormal range
+        v[11] = 6.0e-8                       # f16 subnormal range
+        v[12] = 65500.0                      # f16 near-overflow
+        v[13] = 1.0 + 2.0 ** -9 * (k + 1)    # rounding ties for bf16/f16
+        v[14] = 1.0 + 2.0 ** -12
+        v[15] = -1.0 - 2.0 ** -8
+    return v.reshape(shape)
+
+
+def main():
+    torch.set_num_threads(8)
+    np.random.seed(0)
+    cases = []
+    # configs[0]: spambase LinearModel(57, 2), 4 simulated peers
+    cases.append(("spambase_n4_uniform", "f32", make_peers(4, [SPAMBASE] * 4, "f32", 1000), None))
+    cases.append(("spambase_n4_dirichlet", "f32", make_peers(4, [SPAMBASE] * 4, "f32", 1000), dirichlet(4)))
+    # configs[1]: CIFAR-10 GNLeNet, 8 peers, fp32
+    cases.append(("gnlenet_small_n8_uniform", "f32", make_peers(8, [GNLENET_SMALL] * 8, "f32", 1000), None))
+    cases.append(("gnlenet_n8_dirichlet", "f32", make_peers(8, [GNLENET] * 8, "f32", 2000), dirichlet(8)))
+    # configs[2]: FEMNIST CNN (slice), 32 peers
+    cases.append(("femnist_slice_n32", "f32", make_peers(32, [FEMNIST_SLICE] * 32, "f32", 3000), dirichlet(32, 1)))
+    # configs[4]: google_speech ResNet-34 (slice) in bf16, 16 peers, with BN buffers (not averaged)
+    bufs = [((64,), torch.float32), ((64,), torch.float32), ((), torch.int64)]
+    cases.append(("speech_slice_bf16_n16", "bf16",
+                  make_peers(16, [SPEECH_SLICE] * 16, "bf16", 4000, buffers=bufs), dirichlet(16, 2)))
+    cases.append(("speech_slice_f16_n16", "f16", make_peers(16, [SPEECH_SLICE] * 16, "f16", 4100), dirichlet(16, 3)))
+    cases.append(("speech_slice_f64_n16", "f64", make_peers(16, [SPEECH_SLICE] * 16, "f64", 4200), dirichlet(16, 4)))
+    # GL gossip merge: N=2 [self, remote] with age weights (accdfl/gl/community.py:110-117)
+    cases.append(("gl_n2_age", "f32", make_peers(2, [GNLENET[:4]] * 2, "f32", 5000), [3.0 / 7.0, 4.0 / 7.0]))
+    cases.append(("gl_n2_age_zero", "f32", make_peers(2, [GNLENET[:4]] * 2, "f32", 5100), [0.0, 1.0]))
+    cases.append(("single_n1", "f32", make_peers(1, [GNLENET[:3]], "f32", 5200), None))
+    # weights: integers, negative, not summing to one
+    cases.append(("int_weights_n3", "f32", make_peers(3, [[(1000,)]] * 3, "f32", 5300), [1, 2, -1]))
+    cases.append(("unnormalised_n5", "f32", make_peers(5, [[(777,)]] * 5, "f32", 5400), [0.5, 2.5, -0.25, 1e-3, 7.0]))
+    # IEEE special values in every dtype
+    for dt in ("f32", "bf16", "f16", "f64"):
+        cases.append(("specials_%s_n4" % dt, dt, make_peers(4, [[(64,), (17,)]] * 4, dt, 5500, fill=specials),
+                      dirichlet(4, 5)))
+    # ragged sizes (tails that are not a multiple of the 16-byte chunk) and an empty tensor
+    ragged = [(1,), (3,), (5,), (7,), (0,), (1023,), (4099,), (2, 3, 5)]
+    for dt in ("f32", "bf16", "f16", "f64"):
+        cases.append(("ragged_%s_n3" % dt, dt, make_peers(3, [ragged] * 3, dt, 5600), dirichlet(3, 6)))
+    # zip truncation (fedavg.py:24): peer 1 has fewer parameters than peer 0
+    trunc_shapes = [[(100,), (50,), (30,)], [(100,)], [(100,), (50,), (30,), (9,)]]
+    cases.append(("zip_truncation_n3", "f32", make_peers(3, trunc_shapes, "f32", 5700), [0.2, 0.3, 0.5]))
+    # more peers than one kernel pass takes (multi-pass reduce, list order kept)
+    cases.append(("many_peers_n130", "f32", make_peers(130, [[(1000,)]] * 130, "f32", 6000), None))
+    cases.append(("many_peers_bf16_n200", "bf16", make_peers(200, [[(520,)]] * 200, "bf16", 7000), dirichlet(200, 7)))
+    # larger random bf16 / f16 vectors to exercise double-rounding ties
+    cases.append(("tie_bf16_n16", "bf16", make_peers(16, [[(8000,)]] * 16, "bf16", 8000), dirichlet(16, 8)))
+    cases.append(("tie_f16_n16", "f16", make_peers(16, [[(8000,)]] * 16, "f16", 8100), dirichlet(16, 9)))
+
+    for name, dt, models, weights in cases:
+        save_case(name, dt, models, weights)
+
+
+if __name__ == "__main__":
+    if "accdfl" not in sys.modules and not any("reference" in p for p in sys.path):
+        print("run with PYTHONPATH=/root/reference", file=sys.stderr)
+    main()

@@ -1,0 +1,128 @@
+"""CPU-side checks: the C-ABI library loads and exports every entry point that
+include/dlagg.h declares; host logic mirrors the reference's error behaviour; the
+product path refuses to run without a HIP device (no CPU fallback)."""
+import ctypes
+import os
+import re
+
+import pytest
+import torch
+from torch import nn
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _declared_symbols():
+    text = open(os.path.join(ROOT, "include", "dlagg.h")).read()
+    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(dla_\w+)\s*\(", text, re.M)))
+
+
+@pytest.fixture(scope="module")
+def lib_path():
+    from accdfl_amd import _lib
+
+    return _lib.build()
+
+
+def test_header_declares_entry_points():
+    syms = _declared_symbols()
+    assert {"dla_wsum", "dla_wsum_ex", "dla_wsum_slab", "dla_wsum_multi", "dla_version",
+            "dla_last_error"} <= set(syms)
+
+
+def test_library_exports_every_declared_symbol(lib_path):
+    so = ctypes.CDLL(lib_path)
+    for s in _declared_symbols():
+        assert hasattr(so, s), s
+    from accdfl_amd import _lib
+
+    assert set(_lib.EXPORTED) == set(_declared_symbols())
+
+
+def test_library_version_and_argument_errors(lib_path):
+    """Calls that fail validation never touch the GPU, so they run here."""
+    from accdfl_amd import _lib
+
+    L = _lib.lib()
+    assert L.so.dla_version() == 1
+    assert L.max_peers_per_pass == 128
+    # n_peers = 0 -> DLA_E_INVALID with a message
+    rc = L.so.dla_wsum(0, None, None, 0, 10, None, None)
+    assert rc == -1 and b"n_peers" in L.so.dla_last_error()
+    # unknown dtype
+    rc = L.so.dla_wsum(9, None, None, 1, 10, None, None)
+    assert rc == -1 and b"dtype" in L.so.dla_last_error()
+    with pytest.raises(_lib.DlaggError):
+        _lib.wsum_ptrs(0, [0], [1.0], 10, 0, 0)  # null peer pointer
+    # empty buffers are a no-op (nothing launched)
+    _lib.wsum_ptrs(0, [16], [1.0], 0, 16, 0)
+    # alias of a non-first peer in a multi-pass (>128 peers) reduce is refused
+    ptrs = [4096 * (k + 1) for k in range(130)]
+    with pytest.raises(_lib.DlaggError, match="alias"):
+        _lib.wsum_ptrs(0, ptrs, [1.0] * 130, 64, ptrs[5], 0)
+
+
+def _tiny_models(n):
+    return [nn.Linear(4, 2) for _ in range(n)]
+
+
+def test_fedavg_reference_error_behaviour():
+    from accdfl_amd.core.gradient_aggregation.fedavg import FedAvg
+
+    with pytest.raises(IndexError):          # fedavg.py:20 models[0] on an empty list
+        FedAvg.aggregate([], None)
+    with pytest.raises(AssertionError):      # fedavg.py:17
+        FedAvg.aggregate(_tiny_models(3), [0.5, 0.5])
+
+
+@pytest.mark.skipif(torch.cuda.is_available(), reason="checks the no-GPU refusal")
+def test_no_cpu_fallback():
+    from accdfl_amd.core.gradient_aggregation.fedavg import FedAvg
+
+    with pytest.raises(RuntimeError, match="no HIP device"):
+        FedAvg.aggregate(_tiny_models(2), None)
+
+
+def test_plugin_surface_matches_reference():
+    from accdfl_amd.core.gradient_aggregation import GradientAggregation, GradientAggregationMethod
+    from accdfl_amd.core.gradient_aggregation.fedavg import FedAvg
+
+    assert int(GradientAggregationMethod.FEDAVG) == 1
+    assert issubclass(FedAvg, GradientAggregation)
+    assert isinstance(FedAvg.__dict__["aggregate"], staticmethod)
+
+
+def test_model_manager_registry_semantics():
+    """model_manager.py:42-58: first arrival wins; order = arrival order; selector."""
+    from types import SimpleNamespace
+
+    from accdfl_amd.core.gradient_aggregation import GradientAggregationMethod
+    from accdfl_amd.core.gradient_aggregation.fedavg import FedAvg
+    from accdfl_amd.core.model_manager import ModelManager
+
+    mm = ModelManager(None, SimpleNamespace(gradient_aggregation=GradientAggregationMethod.FEDAVG), 0)
+    a, b, c = _tiny_models(3)
+    mm.process_incoming_trained_model(b"p2", b)
+    mm.process_incoming_trained_model(b"p1", a)
+    mm.process_incoming_trained_model(b"p2", c)  # duplicate peer: ignored
+    assert list(mm.incoming_trained_models.values()) == [b, a]
+    assert mm.get_aggregation_method() is FedAvg
+    mm.reset_incoming_trained_models()
+    assert mm.incoming_trained_models == {}
+    mm2 = ModelManager(None, SimpleNamespace(gradient_aggregation=99), 0)
+    assert mm2.get_aggregation_method() is None
+
+
+def test_bucket_bounds():
+    from accdfl_amd.core.sharding import bucket_bounds
+
+    for n in (0, 1, 63, 64, 65, 1000, 25_000_000, 21_296_355):
+        for world in (1, 2, 3, 4, 8):
+            b = bucket_bounds(n, world, 64)
+            assert len(b) == world
+            assert b[0][0] == 0 and b[-1][1] == n
+            for (s0, e0), (s1, e1) in zip(b, b[1:]):
+                assert e0 == s1
+            for s, e in b:
+                assert s % 64 == 0 or s == n
+                assert s <= e

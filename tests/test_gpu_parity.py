@@ -1,0 +1,224 @@
+"""GPU parity: the HIP reduce (through the C ABI) against the reference's golden vectors
+and the CPU oracle, bit for bit (NaN compared as NaN).  Run on the MI355X: -m gpu."""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import golden_cases as gc
+from oracle.fedavg_oracle import fedavg_bits, same_bits
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CASES = gc.case_names()
+TDT = {"f32": torch.float32, "bf16": torch.bfloat16, "f16": torch.float16, "f64": torch.float64}
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _native():
+    assert torch.cuda.is_available(), "GPU tests need the MI355X"
+    from accdfl_amd import _lib
+
+    _lib.build()
+    _lib.lib()
+    yield
+
+
+def _c_oracle():
+    import subprocess
+
+    so = os.path.join(ROOT, "oracle", "_build", "liboracle_fedavg.so")
+    if not os.path.exists(so):
+        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
+    return ctypes.CDLL(so)
+
+
+def c_wsum(flat_peers, weights, dtype):
+    lib = _c_oracle()
+    n = len(flat_peers)
+    fn = {"f32": lib.oracle_wsum_f32, "f64": lib.oracle_wsum_f64, "bf16": lib.oracle_wsum_bf16,
+          "f16": lib.oracle_wsum_f16}[dtype]
+    arrs = [np.ascontiguousarray(p) for p in flat_peers]
+    ptrs = (ctypes.c_void_p * n)(*[a.ctypes.data for a in arrs])
+    w = (ctypes.c_double * n)(*[float(x) for x in weights])
+    out = np.empty_like(arrs[0])
+    fn(ptrs, w, ctypes.c_int(n), ctypes.c_int64(out.size), ctypes.c_void_p(out.ctypes.data))
+    return out
+
+
+def _check_case_output(c, out_model, device_type):
+    for i, (p, want) in enumerate(zip(out_model.parameters(), c.out)):
+        assert p.device.type == device_type
+        got = gc.from_torch(p, c.dtype)
+        assert got.shape == want.shape
+        assert same_bits(got, want, c.dtype), "%s param %d differs from the reference" % (c.name, i)
+    assert [p.requires_grad for p in out_model.parameters()] == c.requires_grad
+    for j, (b, want) in enumerate(zip(out_model.buffers(), c.out_buffers)):
+        assert np.array_equal(b.detach().cpu().numpy(), want), "%s buffer %d" % (c.name, j)
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_fedavg_cpu_models_match_reference(name):
+    """The reference's situation: CPU modules in, CPU module out (host-staged HIP path)."""
+    from accdfl_amd.core.gradient_aggregation.fedavg import FedAvg
+
+    c = gc.load(name)
+    models = gc.build_models(c, "cpu")
+    before = [[p.detach().clone() for p in m.parameters()] for m in models]
+    out = FedAvg.aggregate(models, c.weights)
+    _check_case_output(c, out, "cpu")
+    for m, b in zip(models, before):  # inputs are not mutated
+        for p, q in zip(m.parameters(), b):
+            assert torch.equal(p.detach().view(torch.uint8), q.view(torch.uint8))
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_fedavg_device_models_match_reference(name):
+    """Models already in HBM: reduced in place into deepcopy(models[0]) with no copies."""
+    from accdfl_amd.core.gradient_aggregation.fedavg import FedAvg
+
+    c = gc.load(name)
+    models = gc.build_models(c, "cuda:0")
+    out = FedAvg.aggregate(models, c.weights)
+    torch.cuda.synchronize()
+    _check_case_output(c, out, "cuda")
+
+
+@pytest.mark.parametrize("name", [n for n in CASES if not n.startswith("zip_truncation")])
+def test_device_model_manager_matches_reference(name):
+    """Peers staged into the HBM PeerSlab on arrival; one device-resident reduce."""
+    from types import SimpleNamespace
+
+    from accdfl_amd.core.gradient_aggregation import GradientAggregationMethod
+    from accdfl_amd.core.model_manager import DeviceModelManager
+
+    c = gc.load(name)
+    models = gc.build_models(c, "cpu")
+    mm = DeviceModelManager(None, SimpleNamespace(gradient_aggregation=GradientAggregationMethod.FEDAVG), 0,
+                            capacity=4)
+    for k, m in enumerate(models):
+        mm.process_incoming_trained_model(b"peer%d" % k, m)
+    out = mm.aggregate_trained_models(c.weights)
+    _check_case_output(c, out, "cpu")
+    # next round reuses the slab
+    mm.reset_incoming_trained_models()
+    for k, m in enumerate(models):
+        mm.process_incoming_trained_model(b"peer%d" % k, m)
+    _check_case_output(c, mm.aggregate_trained_models(c.weights), "cpu")
+
+
+def _random_peers(n, numel, dtype, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    return [(torch.randn(numel, generator=g) * 0.05).to(TDT[dtype]) for _ in range(n)]
+
+
+def _bits(t, dtype):
+    return gc.from_torch(t, dtype)
+
+
+LAUNCH_CFGS = [(1, 1, 0), (2, 1, 0), (1, 2, 0), (2, 2, 0), (1, 4, 0), (2, 4, 0), (2, 1, 512), (1, 2, 300)]
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16", "f16", "f64"])
+def test_every_launch_variant_is_bit_exact(dtype):
+    from accdfl_amd import _lib
+    from accdfl_amd.core import wsum
+
+    numel = (1 << 20) + 3  # ragged tail
+    peers = _random_peers(8, numel, dtype, seed=1)
+    w = [float(x) for x in np.random.default_rng(1).dirichlet(np.ones(8))]
+    want = c_wsum([_bits(p, dtype) for p in peers], w, dtype)
+    dev = [p.cuda() for p in peers]
+    for variant, chunks, grid in LAUNCH_CFGS:
+        cfg = _lib.LaunchCfg(variant, chunks, grid)
+        out = wsum.wsum(dev, w, cfg=cfg)
+        torch.cuda.synchronize()
+        assert same_bits(_bits(out, dtype), want, dtype), (dtype, variant, chunks, grid)
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 7, 8, 9, 16, 31, 32, 33, 64, 127, 128, 129, 257])
+def test_peer_counts(n):
+    from accdfl_amd.core import wsum
+
+    peers = _random_peers(n, 10_007, "f32", seed=n)
+    w = [float(x) for x in np.random.default_rng(n).dirichlet(np.ones(n))]
+    out = wsum.wsum([p.cuda() for p in peers], w)
+    assert same_bits(_bits(out, "f32"), fedavg_bits([p.numpy() for p in peers], w, "f32"), "f32")
+
+
+def test_out_aliases_first_peer_and_streams():
+    from accdfl_amd.core import wsum
+
+    peers = _random_peers(8, 300_001, "bf16", seed=5)
+    w = [0.125] * 8
+    want = c_wsum([_bits(p, "bf16") for p in peers], w, "bf16")
+    dev = [p.cuda() for p in peers]
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        out = wsum.wsum(dev, w, out=dev[0])  # in place into peer 0 (read before write per element)
+    s.synchronize()
+    assert out.data_ptr() == dev[0].data_ptr()
+    assert same_bits(_bits(out, "bf16"), want, "bf16")
+
+
+def test_unaligned_views_use_scalar_path():
+    from accdfl_amd.core import wsum
+
+    base = _random_peers(5, 50_003, "f32", seed=9)
+    views = [torch.cat([torch.zeros(1), b]).cuda()[1:] for b in base]  # 4-byte offset: not 16-B aligned
+    assert all(v.data_ptr() % 16 for v in views)
+    w = [0.1, 0.2, 0.3, 0.15, 0.25]
+    out = wsum.wsum(views, w)
+    assert same_bits(_bits(out, "f32"), fedavg_bits([b.numpy() for b in base], w, "f32"), "f32")
+
+
+def test_peer_slab_staging_orders_and_grows():
+    from accdfl_amd.core.peer_slab import PeerSlab
+
+    shapes = [(33, 7), (5,), (1000,)]
+    slab = PeerSlab(shapes, torch.float32, capacity=2)
+    models = [[(torch.randn(s) * 0.05) for s in shapes] for _ in range(5)]
+    for pl in models:
+        slab.stage(pl)
+    assert slab.n == 5 and slab.capacity >= 5
+    w = [0.3, 0.1, 0.2, 0.25, 0.15]
+    flat = slab.reduce(w)
+    want = fedavg_bits([torch.cat([p.reshape(-1) for p in pl]).numpy() for pl in models], w, "f32")
+    assert same_bits(_bits(flat, "f32"), want, "f32")
+
+
+def test_north_star_full_size_bit_exact():
+    """8 peers x 25 M fp32 (BASELINE north star), device-resident, vs the C oracle."""
+    from accdfl_amd.core import wsum
+
+    n, numel = 8, 25_000_000
+    peers = torch.empty((n, numel), dtype=torch.float32, device="cuda")
+    for k in range(n):
+        g = torch.Generator(device="cuda").manual_seed(1000 + k)
+        peers[k].normal_(0, 0.05, generator=g)
+    w = [float(x) for x in np.random.default_rng(0).dirichlet(np.ones(n))]
+    out = wsum.wsum_rows(peers, w)
+    host = peers.cpu().numpy()
+    want = c_wsum(list(host), w, "f32")
+    assert same_bits(out.cpu().numpy(), want, "f32")
+
+
+def test_google_speech_full_size_bf16_sampled():
+    """configs[4] size on one GPU: 128 peers x 21,296,355 bf16 (5.5 GB); checked on a
+    strided 1/64 sample of elements against the C oracle (elements are independent)."""
+    from accdfl_amd.core import wsum
+
+    n, numel = 128, 21_296_355
+    pitch = (numel + 127) // 128 * 128
+    slab = torch.empty((n, pitch), dtype=torch.bfloat16, device="cuda")
+    g = torch.Generator(device="cuda").manual_seed(7)
+    slab.normal_(0, 0.05, generator=g)
+    w = [float(x) for x in np.random.default_rng(3).dirichlet(np.ones(n))]
+    out = wsum.wsum_rows(slab, w, numel)
+    idx = torch.arange(0, numel, 64, device="cuda")
+    sample = slab[:, :numel].index_select(1, idx).cpu()
+    want = c_wsum([_bits(sample[k].contiguous(), "bf16") for k in range(n)], w, "bf16")
+    assert same_bits(_bits(out[idx], "bf16"), want, "bf16")

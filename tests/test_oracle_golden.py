@@ -1,0 +1,100 @@
+"""Pin the CPU oracle to the reference: every restatement must reproduce the golden
+vectors that make_golden.py produced by running the reference FedAvg
+(accdfl/core/gradient_aggregation/fedavg.py:12-26) in the build container."""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+import pytest
+import torch
+
+import golden_cases as gc
+from oracle.fedavg_oracle import fedavg_bits, fedavg_modules_torch, fedavg_param_lists, same_bits
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CASES = gc.case_names()
+
+
+def test_golden_set_present():
+    # every BASELINE config shape and every edge class is covered by at least one case
+    for required in ("spambase_n4_uniform", "gnlenet_n8_dirichlet", "femnist_slice_n32", "speech_slice_bf16_n16",
+                     "gl_n2_age", "specials_bf16_n4", "ragged_f16_n3", "zip_truncation_n3", "many_peers_n130"):
+        assert required in CASES
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_numpy_oracle_matches_reference(name):
+    c = gc.load(name)
+    got = fedavg_param_lists([[gc.as_float(p, c.dtype) for p in pl] for pl in c.params], c.weights, c.dtype)
+    assert len(got) == len(c.out)
+    for i, (g, w) in enumerate(zip(got, c.out)):
+        assert same_bits(np.asarray(g).view(w.dtype), w, c.dtype), "%s param %d" % (name, i)
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_torch_port_matches_reference(name):
+    """The timed CPU baseline (torch op-sequence restatement) is the reference's arithmetic."""
+    c = gc.load(name)
+    models = gc.build_models(c)
+    out = fedavg_modules_torch(models, c.weights)
+    for i, (p, w) in enumerate(zip(out.parameters(), c.out)):
+        assert same_bits(gc.from_torch(p, c.dtype), w, c.dtype), "%s param %d" % (name, i)
+    for j, (b, w) in enumerate(zip(out.buffers(), c.out_buffers)):
+        assert np.array_equal(b.numpy(), w), "%s buffer %d" % (name, j)
+
+
+def _c_oracle():
+    so = os.path.join(ROOT, "oracle", "_build", "liboracle_fedavg.so")
+    if not os.path.exists(so):
+        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
+    return ctypes.CDLL(so)
+
+
+def c_wsum(lib, flat_peers, weights, dtype):
+    n = len(flat_peers)
+    fn = {"f32": lib.oracle_wsum_f32, "f64": lib.oracle_wsum_f64, "bf16": lib.oracle_wsum_bf16,
+          "f16": lib.oracle_wsum_f16}[dtype]
+    arrs = [np.ascontiguousarray(p) for p in flat_peers]
+    ptrs = (ctypes.c_void_p * n)(*[a.ctypes.data for a in arrs])
+    w = (ctypes.c_double * n)(*[float(x) for x in weights])
+    out = np.empty_like(arrs[0])
+    fn(ptrs, w, ctypes.c_int(n), ctypes.c_int64(out.size), ctypes.c_void_p(out.ctypes.data))
+    return out
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_c_oracle_matches_reference(name):
+    lib = _c_oracle()
+    c = gc.load(name)
+    n = len(c.params)
+    weights = c.weights or [float(1.0 / n)] * n
+    for i, want in enumerate(c.out):
+        ks = [k for k in range(n) if len(c.params[k]) > i]
+        got = c_wsum(lib, [c.params[k][i].reshape(-1) for k in ks], [weights[k] for k in ks], c.dtype)
+        assert same_bits(got, want.reshape(-1), c.dtype), "%s param %d" % (name, i)
+
+
+def test_numpy_and_c_oracle_agree_on_large_random():
+    """Independent restatements agree on a 1 M-element, 8-peer input (fp32 and bf16)."""
+    lib = _c_oracle()
+    rng = np.random.default_rng(11)
+    w = [float(x) for x in rng.dirichlet(np.ones(8))]
+    peers = [(rng.standard_normal(1 << 20) * 0.05).astype(np.float32) for _ in range(8)]
+    assert same_bits(c_wsum(lib, peers, w, "f32"), fedavg_bits(peers, w, "f32"), "f32")
+    bpeers = [(p.view(np.uint32) >> 16).astype(np.uint16) for p in peers]
+    assert same_bits(c_wsum(lib, bpeers, w, "bf16"), fedavg_bits(bpeers, w, "bf16"), "bf16")
+
+
+def test_fma_would_break_parity():
+    """Sanity: the golden vectors really pin the no-FMA rounding (an FMA model differs)."""
+    c = gc.load("gnlenet_n8_dirichlet")
+    n = len(c.params)
+    flat = [np.concatenate([p.reshape(-1).view(np.float32) for p in pl]) for pl in c.params]
+    want = np.concatenate([o.reshape(-1) for o in c.out]).view(np.float32)
+    acc = (flat[0] * np.float32(0)).astype(np.float64)
+    for p, w in zip(flat, c.weights):
+        acc = (acc + np.float64(np.float32(w)) * p.astype(np.float64)).astype(np.float32).astype(np.float64)
+    fma = acc.astype(np.float32)
+    assert not np.array_equal(fma.view(np.uint32), want.view(np.uint32))
+    assert n == 8
