@@ -213,7 +213,7 @@ def sweep(args, device):
     ptrs = [slab[k].data_ptr() for k in range(args.peers)]
     code = wsum.dtype_code(dt)
     sp = torch.cuda.current_stream().cuda_stream
-    cfgs = [(v, c, g) for v in (1, 2) for c in (1, 2, 4) for g in (0, 1024, 2048, 4096)]
+    cfgs = [(v, c, g) for v in (1, 2, 3) for c in (1, 2, 4) for g in (0, 2048, 4096)]
     res = {c: [] for c in cfgs}
     for rnd in range(5):
         for c in cfgs:

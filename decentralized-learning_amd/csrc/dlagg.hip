@@ -198,12 +198,22 @@ __device__ inline uint4 load16(const uint4* p) {
   return make_uint4(v.x, v.y, v.z, v.w);
 }
 
+template <bool NT>
+__device__ inline void store16(uint4* p, const uint4& v) {
+  u32x4 w = {v.x, v.y, v.z, v.w};
+  if constexpr (NT) {
+    __builtin_nontemporal_store(w, reinterpret_cast<u32x4*>(p));  // global_store_dwordx4 ... nt
+  } else {
+    *reinterpret_cast<u32x4*>(p) = w;
+  }
+}
+
 // ------------------------------------------------ register-stream kernel (v1/v2)
 //
 // Tile = kBlock * CH chunks; lane l of the block owns chunks tile_base + c*kBlock + l.
 // ACC_IN: the running sum starts from `out` (second and later passes of a
 // reduce with more than KMAX peers) instead of p0 * 0.
-template <int DT, int KMAX, int CH, bool NT, bool ACC_IN>
+template <int DT, int KMAX, int CH, bool NT, bool NTS, bool ACC_IN>
 __global__ __launch_bounds__(kBlock) void wsum_stream_kernel(
     const PeerTable<typename Ops<DT>::w_t, KMAX> tab, int n_peers, int64_t n_chunks,
     int64_t n_elems, void* __restrict__ out_v) {
@@ -282,7 +292,7 @@ __global__ __launch_bounds__(kBlock) void wsum_stream_kernel(
     }
 #pragma unroll
     for (int c = 0; c < CH; ++c)
-        if (live[c]) out[idx[c]] = O::pack(acc[c]);
+        if (live[c]) store16<NTS>(out + idx[c], O::pack(acc[c]));
   }
 
   // Ragged tail (n_elems not a multiple of E): one element per lane of block 0.
@@ -341,7 +351,7 @@ Launch resolve(const dla_launch_cfg_t* cfg) {
   return l;
 }
 
-template <int DT, int KMAX, int CH, bool NT, bool ACC_IN>
+template <int DT, int KMAX, int CH, bool NT, bool NTS, bool ACC_IN>
 hipError_t launch_stream(const PeerTable<typename Ops<DT>::w_t, KMAX>& tab, int n, int64_t n_elems,
                          void* out, hipStream_t s, int grid_blocks) {
   constexpr int E = Ops<DT>::E;
@@ -352,7 +362,7 @@ hipError_t launch_stream(const PeerTable<typename Ops<DT>::w_t, KMAX>& tab, int 
   int64_t grid = grid_blocks > 0 ? grid_blocks : tiles;
   if (grid > tiles) grid = tiles;
   if (grid > 0x7fffffff) grid = 0x7fffffff;
-  hipLaunchKernelGGL((wsum_stream_kernel<DT, KMAX, CH, NT, ACC_IN>), dim3(static_cast<unsigned>(grid)),
+  hipLaunchKernelGGL((wsum_stream_kernel<DT, KMAX, CH, NT, NTS, ACC_IN>), dim3(static_cast<unsigned>(grid)),
                      dim3(kBlock), 0, s, tab, n, n_chunks, n_elems, out);
   return hipGetLastError();
 }
@@ -368,17 +378,17 @@ hipError_t launch_pass(const PeerTable<typename Ops<DT>::w_t, KMAX>& tab, int n,
                        dim3(kBlock), 0, s, tab, n, n_elems, out);
     return hipGetLastError();
   }
-  const bool nt = l.variant == 2;
+  // variant 1: plain loads/stores; 2: nt loads; 3: nt loads + nt stores
+#define DLA_CH_CASE(CHV)                                                                              \
+  case CHV:                                                                                           \
+    if (l.variant == 1) return launch_stream<DT, KMAX, CHV, false, false, ACC_IN>(tab, n, n_elems, out, s, l.grid_blocks); \
+    if (l.variant == 2) return launch_stream<DT, KMAX, CHV, true, false, ACC_IN>(tab, n, n_elems, out, s, l.grid_blocks);  \
+    return launch_stream<DT, KMAX, CHV, true, true, ACC_IN>(tab, n, n_elems, out, s, l.grid_blocks);
   switch (l.chunks) {
-    case 1:
-      return nt ? launch_stream<DT, KMAX, 1, true, ACC_IN>(tab, n, n_elems, out, s, l.grid_blocks)
-                : launch_stream<DT, KMAX, 1, false, ACC_IN>(tab, n, n_elems, out, s, l.grid_blocks);
-    case 2:
-      return nt ? launch_stream<DT, KMAX, 2, true, ACC_IN>(tab, n, n_elems, out, s, l.grid_blocks)
-                : launch_stream<DT, KMAX, 2, false, ACC_IN>(tab, n, n_elems, out, s, l.grid_blocks);
-    case 4:
-      return nt ? launch_stream<DT, KMAX, 4, true, ACC_IN>(tab, n, n_elems, out, s, l.grid_blocks)
-                : launch_stream<DT, KMAX, 4, false, ACC_IN>(tab, n, n_elems, out, s, l.grid_blocks);
+    DLA_CH_CASE(1)
+    DLA_CH_CASE(2)
+    DLA_CH_CASE(4)
+#undef DLA_CH_CASE
     default:
       return hipErrorInvalidValue;
   }
@@ -449,7 +459,7 @@ int wsum_impl(int dtype, const void* const* peers, const double* weights, int n_
                                      std::to_string(kMaxPeersPerPass));
   }
   const Launch l = resolve(cfg);
-  if (l.variant < 1 || l.variant > 2)
+  if (l.variant < 1 || l.variant > 3)
     return fail(DLA_E_CONFIG, "dla_wsum: unsupported variant " + std::to_string(l.variant));
   if (l.chunks != 1 && l.chunks != 2 && l.chunks != 4)
     return fail(DLA_E_CONFIG, "dla_wsum: chunks must be 1, 2 or 4");

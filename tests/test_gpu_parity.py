@@ -72,7 +72,7 @@ def test_fedavg_cpu_models_match_reference(name):
     _check_case_output(c, out, "cpu")
     for m, b in zip(models, before):  # inputs are not mutated
         for p, q in zip(m.parameters(), b):
-            assert torch.equal(p.detach().view(torch.uint8), q.view(torch.uint8))
+            assert np.array_equal(gc.from_torch(p, c.dtype), gc.from_torch(q, c.dtype))
 
 
 @pytest.mark.parametrize("name", CASES)
@@ -119,7 +119,8 @@ def _bits(t, dtype):
     return gc.from_torch(t, dtype)
 
 
-LAUNCH_CFGS = [(1, 1, 0), (2, 1, 0), (1, 2, 0), (2, 2, 0), (1, 4, 0), (2, 4, 0), (2, 1, 512), (1, 2, 300)]
+LAUNCH_CFGS = [(1, 1, 0), (2, 1, 0), (3, 1, 0), (1, 2, 0), (2, 2, 0), (3, 2, 0), (1, 4, 0), (2, 4, 0), (3, 4, 0),
+               (2, 1, 512), (1, 2, 300), (3, 4, 1000)]
 
 
 @pytest.mark.parametrize("dtype", ["f32", "bf16", "f16", "f64"])
