@@ -57,7 +57,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--peers", type=int, default=NS_PEERS)
     ap.add_argument("--params", type=int, default=NS_PARAMS)
-    ap.add_argument("--dtype", default="f32", choices=["f32", "bf16"])
+    ap.add_argument("--dtype", default="f32", choices=["f32", "bf16", "f16"])
     ap.add_argument("--variant", type=int, default=0)
     ap.add_argument("--chunks", type=int, default=0)
     ap.add_argument("--grid", type=int, default=0)
@@ -67,6 +67,8 @@ def parse():
     ap.add_argument("--no-small", action="store_true")
     ap.add_argument("--allgather", action="store_true", help="also time the RCCL all-gather of the buckets")
     ap.add_argument("--sweep", action="store_true", help="interleaved A/B of launch variants, then exit")
+    ap.add_argument("--sweep-cfgs", default="", help="variant,chunks,grid;... (default: built-in list)")
+    ap.add_argument("--no-ceilings", action="store_true", help="skip the probe ceilings in --sweep")
     return ap.parse_args()
 
 
@@ -205,15 +207,18 @@ def sweep(args, device):
     from accdfl_amd import _lib
     from accdfl_amd.core import wsum
 
-    dt = torch.float32 if args.dtype == "f32" else torch.bfloat16
+    dt = {"f32": torch.float32, "bf16": torch.bfloat16, "f16": torch.float16}[args.dtype]
     es = 4 if args.dtype == "f32" else 2
-    slab = make_slab(args.peers, args.params, dt, device, 1000)
+    slab = make_slab(args.peers, (args.params + 127) // 128 * 128, dt, device, 1000)  # 16-B aligned rows
     out = torch.empty(args.params, dtype=dt, device=device)
     w = [float(1.0 / args.peers)] * args.peers
     ptrs = [slab[k].data_ptr() for k in range(args.peers)]
     code = wsum.dtype_code(dt)
     sp = torch.cuda.current_stream().cuda_stream
-    cfgs = [(v, c, g) for v in (1, 2, 3) for c in (1, 2, 4) for g in (0, 2048, 4096)]
+    if args.sweep_cfgs:
+        cfgs = [tuple(int(x) for x in item.split(",")) for item in args.sweep_cfgs.split(";") if item]
+    else:
+        cfgs = [(v, c, g) for v in (1, 2, 3, 4, 5) for c in (1, 2, 4) for g in (0, 4096)]
     res = {c: [] for c in cfgs}
     for rnd in range(5):
         for c in cfgs:
@@ -222,15 +227,67 @@ def sweep(args, device):
             _, ev = time_kernel(fn, 50, 5, 1)
             res[c].append(ev / 50)
     byts = (args.peers + 1) * args.params * es
+    # in place: the average overwrites peer 0's row (allowed by the ABI: out may alias peers[0])
+    for c in ([] if args.sweep_cfgs else [(2, 4, 0), (4, 4, 4096)]):
+        cfg = _lib.LaunchCfg(*c)
+        key = (c[0], c[1], -1)
+        res[key] = []
+        for rnd in range(5):
+            fn = lambda: _lib.wsum_ptrs(code, ptrs, w, args.params, ptrs[0], sp, cfg)  # noqa: E731
+            _, ev = time_kernel(fn, 50, 5, 1)
+            res[key].append(ev / 50)
     rows = sorted(((statistics.median(v), c) for c, v in res.items()))
     for t, c in rows:
         print(json.dumps({"variant": c[0], "chunks": c[1], "grid": c[2], "us": round(t * 1e6, 2),
                           "GB/s": round(byts / t / 1e9, 1), "min_us": round(min(res[c]) * 1e6, 2)}))
-    # measured device copy peak (torch copy kernel) for reference
-    a = torch.empty(512 * 1024 * 1024 // 4, dtype=torch.float32, device=device)
+    del slab
+    if not args.no_ceilings:
+        for k, v in measured_ceilings(device).items():
+            print(json.dumps({k: v}))
+
+
+def measured_ceilings(device, nbytes=1 << 30):
+    """Streaming ceilings of this chip measured with the csrc/probe.hip kernels (1 GiB,
+    beyond the 256 MiB Infinity Cache) and torch's copy, in GB/s."""
+    import ctypes
+
+    from accdfl_amd import _lib
+
+    so = ctypes.CDLL(_lib.build_probe())
+    so.dlp_read.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                            ctypes.c_void_p]
+    so.dlp_copy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_void_p]
+    a = torch.empty(nbytes // 4, dtype=torch.float32, device=device).normal_()
     b = torch.empty_like(a)
-    _, ev = time_kernel(lambda: b.copy_(a), 50, 5, 1)
-    print(json.dumps({"torch_copy_GBps": round(2 * a.numel() * 4 / (ev / 50) / 1e9, 1)}))
+    sink = torch.zeros(1024, dtype=torch.int32, device=device)
+    sp = lambda: torch.cuda.current_stream().cuda_stream  # noqa: E731
+    res = {}
+    for ch in (1, 4, 8):
+        for nt in (0, 1):
+            _, ev = time_kernel(lambda: so.dlp_read(a.data_ptr(), nbytes, sink.data_ptr(), ch, nt, sp()), 30, 3, 1)
+            res["read_ch%d_nt%d" % (ch, nt)] = round(nbytes / (ev / 30) / 1e9, 1)
+    for nt in (0, 1):
+        _, ev = time_kernel(lambda: so.dlp_copy(a.data_ptr(), b.data_ptr(), nbytes, nt, sp()), 30, 3, 1)
+        res["copy_nt%d" % nt] = round(2 * nbytes / (ev / 30) / 1e9, 1)
+    _, ev = time_kernel(lambda: b.copy_(a), 30, 3, 1)
+    res["torch_copy"] = round(2 * nbytes / (ev / 30) / 1e9, 1)
+    del a, b
+    # the FedAvg access pattern without arithmetic: 8 streams of 100 MB (+ 1 output stream)
+    each = 100_000_000
+    srcs = torch.empty((8, each // 4), dtype=torch.float32, device=device).normal_()
+    dst = torch.empty(each // 4, dtype=torch.float32, device=device)
+    arr = (ctypes.c_void_p * 8)(*[srcs[k].data_ptr() for k in range(8)])
+    so.dlp_mread8.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
+                              ctypes.c_int, ctypes.c_void_p]
+    for ch in (1, 2, 4):
+        for wr in (0, 1):
+            _, ev = time_kernel(lambda: so.dlp_mread8(arr, each, dst.data_ptr(), sink.data_ptr(), ch, wr, sp()),
+                                30, 3, 1)
+            res["mread8_ch%d_write%d" % (ch, wr)] = round((8 + wr) * each / (ev / 30) / 1e9, 1)
+        _, ev = time_kernel(lambda: so.dlp_mread8(arr, each, srcs[0].data_ptr(), sink.data_ptr(), ch, 1, sp()),
+                            30, 3, 1)
+        res["mread8_ch%d_write_inplace" % ch] = round(9 * each / (ev / 30) / 1e9, 1)
+    return res
 
 
 def main():
@@ -243,7 +300,7 @@ def main():
     if args.sweep:
         sweep(args, device)
         return
-    dt = torch.float32 if args.dtype == "f32" else torch.bfloat16
+    dt = {"f32": torch.float32, "bf16": torch.bfloat16, "f16": torch.float16}[args.dtype]
     es = 4 if args.dtype == "f32" else 2
     n, p = args.peers, args.params
     # this rank's bucket of every peer: rows of one [n, pitch] slab (16-B aligned rows)

@@ -66,6 +66,19 @@ def build(force: bool = False, verbose: bool = False) -> str:
     return out
 
 
+def build_probe(force: bool = False) -> str:
+    """Compile the HBM ceiling probes (csrc/probe.hip -> lib/libdlagg_probe.so; diagnostics only)."""
+    src = os.path.join(PKG_ROOT, "csrc", "probe.hip")
+    out = os.path.join(PKG_ROOT, "lib", "libdlagg_probe.so")
+    if not force and os.path.exists(out) and os.path.getmtime(out) >= os.path.getmtime(src):
+        return out
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+    subprocess.run([hipcc, *HIPCC_FLAGS, "-o", out + ".tmp", src], check=True)
+    os.replace(out + ".tmp", out)
+    return out
+
+
 class _Lib:
     def __init__(self, path: str):
         if not os.path.exists(path):

@@ -17,9 +17,12 @@
 // Layout of the work: one 16-byte chunk per lane per peer (global_load_dwordx4,
 // 1 KiB per wave instruction, fully coalesced), CH chunks per lane per tile,
 // peers loaded in groups of 8 so each lane keeps 8*CH*16 B in flight before the
-// first add.  Variant 3 stages each peer group's tile through LDS with
-// global_load_lds_dwordx4 (LDS-DMA: no VGPR landing, deeper MLP per wave), then
-// folds it in list order from LDS.
+// first add.  Loads are non-temporal (each byte is read once); the output is
+// stored sc1 (write-through, not kept in the XCD L2), which measured +3.5 % over
+// plain stores on the 8 x 25 M fp32 north-star reduce (profiles/r01_*).  No LDS:
+// each lane folds only its own elements, so there is no cross-lane exchange to
+// stage, and LDS-DMA staging buys nothing for a pure stream at this occupancy
+// (the register stream already keeps >300 KiB in flight per CU).
 //
 // Compiled with -ffp-contract=off; the pragma below repeats it so no build line
 // can re-enable FMA contraction for these functions.
@@ -198,11 +201,16 @@ __device__ inline uint4 load16(const uint4* p) {
   return make_uint4(v.x, v.y, v.z, v.w);
 }
 
-template <bool NT>
+// Store policy: 0 plain, 1 nt, 2 sc1 (drops the line from the XCD L2), 3 sc0 sc1.
+template <int SP>
 __device__ inline void store16(uint4* p, const uint4& v) {
   u32x4 w = {v.x, v.y, v.z, v.w};
-  if constexpr (NT) {
+  if constexpr (SP == 1) {
     __builtin_nontemporal_store(w, reinterpret_cast<u32x4*>(p));  // global_store_dwordx4 ... nt
+  } else if constexpr (SP == 2) {
+    asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(w) : "memory");
+  } else if constexpr (SP == 3) {
+    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(p), "v"(w) : "memory");
   } else {
     *reinterpret_cast<u32x4*>(p) = w;
   }
@@ -213,7 +221,7 @@ __device__ inline void store16(uint4* p, const uint4& v) {
 // Tile = kBlock * CH chunks; lane l of the block owns chunks tile_base + c*kBlock + l.
 // ACC_IN: the running sum starts from `out` (second and later passes of a
 // reduce with more than KMAX peers) instead of p0 * 0.
-template <int DT, int KMAX, int CH, bool NT, bool NTS, bool ACC_IN>
+template <int DT, int KMAX, int CH, bool NT, int SP, bool ACC_IN>
 __global__ __launch_bounds__(kBlock) void wsum_stream_kernel(
     const PeerTable<typename Ops<DT>::w_t, KMAX> tab, int n_peers, int64_t n_chunks,
     int64_t n_elems, void* __restrict__ out_v) {
@@ -292,7 +300,7 @@ __global__ __launch_bounds__(kBlock) void wsum_stream_kernel(
     }
 #pragma unroll
     for (int c = 0; c < CH; ++c)
-        if (live[c]) store16<NTS>(out + idx[c], O::pack(acc[c]));
+        if (live[c]) store16<SP>(out + idx[c], O::pack(acc[c]));
   }
 
   // Ragged tail (n_elems not a multiple of E): one element per lane of block 0.
@@ -337,12 +345,28 @@ __global__ __launch_bounds__(kBlock) void wsum_scalar_kernel(
 
 struct Launch {
   int variant;
-  int chunks;
+  int chunks;  // 0 = pick by size (chunks_for)
   int grid_blocks;
 };
 
+// Chunks per lane: 4 (most bytes in flight per wave) while that still leaves >= 2048
+// tiles (8 per CU) to spread over the 256 CUs; fewer for small reduces, where
+// CH=4 would leave CUs idle (measured: 128 x 2 M bf16, CH=1 6.49 vs CH=4 5.65 TB/s).
+// Passes of more than 32 peers take CH=1: the per-peer loop already keeps a wave
+// busy, and CH=4's 189 VGPRs halve the waves per SIMD (128 x 21.3 M bf16, the
+// google_speech config: CH=1 6.53 vs CH=4 6.28 TB/s; 32 peers: equal).
+int chunks_for(int64_t n_chunks, int n_peers) {
+  constexpr int64_t kMinTiles = 2048;
+  if (n_peers > 32) return 1;
+  if (n_chunks >= kMinTiles * kBlock * 4) return 4;
+  if (n_chunks >= kMinTiles * kBlock * 2) return 2;
+  return 1;
+}
+
 Launch resolve(const dla_launch_cfg_t* cfg) {
-  Launch l{2, 1, 0};  // default: register stream, nt loads, 1 chunk/lane, 1 WG per tile
+  // default (measured on MI355X, profiles/r01_*): nt loads + sc1 stores, 4 chunks per lane,
+  // one workgroup per tile: 6.43-6.58 TB/s on 8 x 25 M fp32 vs 6.21-6.43 for plain stores.
+  Launch l{4, 0, 0};
   if (cfg) {
     if (cfg->variant) l.variant = cfg->variant;
     if (cfg->chunks) l.chunks = cfg->chunks;
@@ -351,7 +375,7 @@ Launch resolve(const dla_launch_cfg_t* cfg) {
   return l;
 }
 
-template <int DT, int KMAX, int CH, bool NT, bool NTS, bool ACC_IN>
+template <int DT, int KMAX, int CH, bool NT, int SP, bool ACC_IN>
 hipError_t launch_stream(const PeerTable<typename Ops<DT>::w_t, KMAX>& tab, int n, int64_t n_elems,
                          void* out, hipStream_t s, int grid_blocks) {
   constexpr int E = Ops<DT>::E;
@@ -362,7 +386,7 @@ hipError_t launch_stream(const PeerTable<typename Ops<DT>::w_t, KMAX>& tab, int 
   int64_t grid = grid_blocks > 0 ? grid_blocks : tiles;
   if (grid > tiles) grid = tiles;
   if (grid > 0x7fffffff) grid = 0x7fffffff;
-  hipLaunchKernelGGL((wsum_stream_kernel<DT, KMAX, CH, NT, NTS, ACC_IN>), dim3(static_cast<unsigned>(grid)),
+  hipLaunchKernelGGL((wsum_stream_kernel<DT, KMAX, CH, NT, SP, ACC_IN>), dim3(static_cast<unsigned>(grid)),
                      dim3(kBlock), 0, s, tab, n, n_chunks, n_elems, out);
   return hipGetLastError();
 }
@@ -378,13 +402,19 @@ hipError_t launch_pass(const PeerTable<typename Ops<DT>::w_t, KMAX>& tab, int n,
                        dim3(kBlock), 0, s, tab, n, n_elems, out);
     return hipGetLastError();
   }
-  // variant 1: plain loads/stores; 2: nt loads; 3: nt loads + nt stores
+  // variant 1: plain loads/stores; 2: nt loads; 3: nt loads + nt stores;
+  //         4: nt loads + sc1 stores; 5: nt loads + sc0 sc1 stores
 #define DLA_CH_CASE(CHV)                                                                              \
   case CHV:                                                                                           \
-    if (l.variant == 1) return launch_stream<DT, KMAX, CHV, false, false, ACC_IN>(tab, n, n_elems, out, s, l.grid_blocks); \
-    if (l.variant == 2) return launch_stream<DT, KMAX, CHV, true, false, ACC_IN>(tab, n, n_elems, out, s, l.grid_blocks);  \
-    return launch_stream<DT, KMAX, CHV, true, true, ACC_IN>(tab, n, n_elems, out, s, l.grid_blocks);
-  switch (l.chunks) {
+    switch (l.variant) {                                                                              \
+      case 1: return launch_stream<DT, KMAX, CHV, false, 0, ACC_IN>(tab, n, n_elems, out, s, l.grid_blocks); \
+      case 2: return launch_stream<DT, KMAX, CHV, true, 0, ACC_IN>(tab, n, n_elems, out, s, l.grid_blocks);  \
+      case 3: return launch_stream<DT, KMAX, CHV, true, 1, ACC_IN>(tab, n, n_elems, out, s, l.grid_blocks);  \
+      case 4: return launch_stream<DT, KMAX, CHV, true, 2, ACC_IN>(tab, n, n_elems, out, s, l.grid_blocks);  \
+      default: return launch_stream<DT, KMAX, CHV, true, 3, ACC_IN>(tab, n, n_elems, out, s, l.grid_blocks); \
+    }
+  const int chunks = l.chunks ? l.chunks : chunks_for(n_elems / Ops<DT>::E, n);
+  switch (chunks) {
     DLA_CH_CASE(1)
     DLA_CH_CASE(2)
     DLA_CH_CASE(4)
@@ -459,10 +489,10 @@ int wsum_impl(int dtype, const void* const* peers, const double* weights, int n_
                                      std::to_string(kMaxPeersPerPass));
   }
   const Launch l = resolve(cfg);
-  if (l.variant < 1 || l.variant > 3)
+  if (l.variant < 1 || l.variant > 5)
     return fail(DLA_E_CONFIG, "dla_wsum: unsupported variant " + std::to_string(l.variant));
-  if (l.chunks != 1 && l.chunks != 2 && l.chunks != 4)
-    return fail(DLA_E_CONFIG, "dla_wsum: chunks must be 1, 2 or 4");
+  if (l.chunks != 0 && l.chunks != 1 && l.chunks != 2 && l.chunks != 4)
+    return fail(DLA_E_CONFIG, "dla_wsum: chunks must be 0 (auto), 1, 2 or 4");
   if (l.grid_blocks < 0) return fail(DLA_E_CONFIG, "dla_wsum: grid_blocks < 0");
   hipStream_t s = static_cast<hipStream_t>(stream);
   hipError_t e;

@@ -1,0 +1,153 @@
+// probe.hip — HBM ceiling probes for MI355X (diagnostics, not on the product path).
+//
+// bench.py --sweep times these beside the FedAvg kernel so the roofline fraction can
+// be read against what this chip actually streams (measured ceilings), not only
+// against the 8 TB/s datasheet number:
+//   dlp_read  — every lane streams 16-byte chunks (CH per lane, all issued before the
+//               first use), XOR-folds them; one dword per workgroup is written only if
+//               the fold hits a magic value (never), so the loads cannot be removed.
+//   dlp_copy  — dwordx4 copy (read + write, 1:1).
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace {
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+template <int CH, bool NT>
+__global__ __launch_bounds__(256) void read_kernel(const u32x4* __restrict__ src, int64_t n_chunks,
+                                                    uint32_t* __restrict__ sink) {
+  const int64_t base = static_cast<int64_t>(blockIdx.x) * 256 * CH + threadIdx.x;
+  u32x4 acc = {0, 0, 0, 0};
+  u32x4 v[CH];
+#pragma unroll
+  for (int c = 0; c < CH; ++c) {
+    int64_t i = base + c * 256;
+    i = i < n_chunks ? i : n_chunks - 1;
+    v[c] = NT ? __builtin_nontemporal_load(src + i) : src[i];
+  }
+#pragma unroll
+  for (int c = 0; c < CH; ++c) acc ^= v[c];
+  const uint32_t f = acc.x ^ acc.y ^ acc.z ^ acc.w;
+  if (f == 0x9e3779b9u && threadIdx.x == 0) sink[blockIdx.x & 1023] = f;
+}
+
+template <int CH, bool NT>
+__global__ __launch_bounds__(256) void copy_kernel(const u32x4* __restrict__ src, u32x4* __restrict__ dst,
+                                                    int64_t n_chunks) {
+  const int64_t base = static_cast<int64_t>(blockIdx.x) * 256 * CH + threadIdx.x;
+  u32x4 v[CH];
+#pragma unroll
+  for (int c = 0; c < CH; ++c) {
+    const int64_t i = base + c * 256;
+    if (i < n_chunks) v[c] = NT ? __builtin_nontemporal_load(src + i) : src[i];
+  }
+#pragma unroll
+  for (int c = 0; c < CH; ++c) {
+    const int64_t i = base + c * 256;
+    if (i < n_chunks) dst[i] = v[c];
+  }
+}
+
+// The FedAvg access pattern without the arithmetic: each lane loads the same 16-byte
+// chunk offset from N_SRC separate buffers (all issued first), folds them, and
+// (WRITE) stores the fold to dst — isolates multi-stream reads vs the output write.
+template <int N_SRC, int CH, bool WRITE>
+__global__ __launch_bounds__(256) void mread_kernel(const u32x4* const* __restrict__ srcs_unused,
+                                                     const u32x4* s0, const u32x4* s1, const u32x4* s2,
+                                                     const u32x4* s3, const u32x4* s4, const u32x4* s5,
+                                                     const u32x4* s6, const u32x4* s7, int64_t n_chunks,
+                                                     u32x4* __restrict__ dst, uint32_t* __restrict__ sink) {
+  const u32x4* src[8] = {s0, s1, s2, s3, s4, s5, s6, s7};
+  const int64_t base = static_cast<int64_t>(blockIdx.x) * 256 * CH + threadIdx.x;
+  int64_t idx[CH];
+#pragma unroll
+  for (int c = 0; c < CH; ++c) {
+    const int64_t i = base + c * 256;
+    idx[c] = i < n_chunks ? i : n_chunks - 1;
+  }
+  u32x4 v[N_SRC][CH];
+#pragma unroll
+  for (int k = 0; k < N_SRC; ++k)
+#pragma unroll
+    for (int c = 0; c < CH; ++c) v[k][c] = __builtin_nontemporal_load(src[k] + idx[c]);
+#pragma unroll
+  for (int c = 0; c < CH; ++c) {
+    u32x4 acc = v[0][c];
+#pragma unroll
+    for (int k = 1; k < N_SRC; ++k) acc ^= v[k][c];
+    if constexpr (WRITE) {
+      if (base + c * 256 < n_chunks) dst[idx[c]] = acc;
+    } else {
+      const uint32_t f = acc.x ^ acc.y ^ acc.z ^ acc.w;
+      if (f == 0x9e3779b9u) sink[blockIdx.x & 1023] = f;
+    }
+  }
+}
+
+template <int CH>
+int launch_read(const void* src, int64_t bytes, void* sink, int nt, hipStream_t s) {
+  const int64_t n = bytes / 16;
+  const int64_t grid = (n + 256 * CH - 1) / (256 * CH);
+  if (nt)
+    hipLaunchKernelGGL((read_kernel<CH, true>), dim3(grid), dim3(256), 0, s, static_cast<const u32x4*>(src), n,
+                       static_cast<uint32_t*>(sink));
+  else
+    hipLaunchKernelGGL((read_kernel<CH, false>), dim3(grid), dim3(256), 0, s, static_cast<const u32x4*>(src), n,
+                       static_cast<uint32_t*>(sink));
+  return static_cast<int>(hipGetLastError());
+}
+
+}  // namespace
+
+extern "C" {
+
+// Read `bytes` (multiple of 16) from src; `chunks` in {1, 4, 8}; sink >= 4 KiB.
+int dlp_read(const void* src, int64_t bytes, void* sink, int chunks, int nt, void* stream) {
+  if (!src || !sink || bytes < 16) return -1;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  switch (chunks) {
+    case 1: return launch_read<1>(src, bytes, sink, nt, s);
+    case 4: return launch_read<4>(src, bytes, sink, nt, s);
+    case 8: return launch_read<8>(src, bytes, sink, nt, s);
+    default: return -1;
+  }
+}
+
+// Copy `bytes` (multiple of 16) src -> dst with 4 chunks per lane.
+int dlp_copy(const void* src, void* dst, int64_t bytes, int nt, void* stream) {
+  if (!src || !dst || bytes < 16) return -1;
+  const int64_t n = bytes / 16;
+  const int64_t grid = (n + 1023) / 1024;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (nt)
+    hipLaunchKernelGGL((copy_kernel<4, true>), dim3(grid), dim3(256), 0, s, static_cast<const u32x4*>(src),
+                       static_cast<u32x4*>(dst), n);
+  else
+    hipLaunchKernelGGL((copy_kernel<4, false>), dim3(grid), dim3(256), 0, s, static_cast<const u32x4*>(src),
+                       static_cast<u32x4*>(dst), n);
+  return static_cast<int>(hipGetLastError());
+}
+
+// 8-stream read (write = 0) or read + write (write = 1) of `bytes_each` per stream.
+int dlp_mread8(const void* const* srcs, int64_t bytes_each, void* dst, void* sink, int chunks, int write,
+               void* stream) {
+  if (!srcs || bytes_each < 16) return -1;
+  const int64_t n = bytes_each / 16;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const u32x4* p[8];
+  for (int k = 0; k < 8; ++k) p[k] = static_cast<const u32x4*>(srcs[k]);
+#define DLP_L(CHV, W)                                                                                       \
+  hipLaunchKernelGGL((mread_kernel<8, CHV, W>), dim3((n + 256 * CHV - 1) / (256 * CHV)), dim3(256), 0, s,   \
+                     nullptr, p[0], p[1], p[2], p[3], p[4], p[5], p[6], p[7], n, static_cast<u32x4*>(dst), \
+                     static_cast<uint32_t*>(sink))
+  if (chunks == 1) { if (write) DLP_L(1, true); else DLP_L(1, false); }
+  else if (chunks == 2) { if (write) DLP_L(2, true); else DLP_L(2, false); }
+  else if (chunks == 4) { if (write) DLP_L(4, true); else DLP_L(4, false); }
+  else return -1;
+#undef DLP_L
+  return static_cast<int>(hipGetLastError());
+}
+
+}  // extern "C"

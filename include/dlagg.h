@@ -58,10 +58,12 @@ extern "C" {
 
 /* Launch tuning knobs for dla_wsum_ex (0 = library default for each field). */
 typedef struct dla_launch_cfg {
-  int variant;      /* 0 = default, 1 = register stream, 2 = register stream + nt loads,
-                       3 = LDS-DMA staged stream                                       */
-  int chunks;       /* 16-byte chunks per thread per peer per iteration (1, 2 or 4)   */
-  int grid_blocks;  /* workgroups; 0 = one per work tile (no grid-stride loop)        */
+  int variant;      /* 0 = default (4); cache policy of the register stream:
+                       1 = plain loads / plain stores   2 = nt loads / plain stores
+                       3 = nt loads / nt stores         4 = nt loads / sc1 stores
+                       5 = nt loads / sc0 sc1 stores                                      */
+  int chunks;       /* 16-byte chunks per lane per peer per tile: 1, 2, 4; 0 = by size   */
+  int grid_blocks;  /* workgroups; 0 = one per work tile (no grid-stride loop)           */
 } dla_launch_cfg_t;
 
 /* ABI version (DLA_ABI_VERSION). */

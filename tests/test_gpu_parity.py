@@ -120,7 +120,7 @@ def _bits(t, dtype):
 
 
 LAUNCH_CFGS = [(1, 1, 0), (2, 1, 0), (3, 1, 0), (1, 2, 0), (2, 2, 0), (3, 2, 0), (1, 4, 0), (2, 4, 0), (3, 4, 0),
-               (2, 1, 512), (1, 2, 300), (3, 4, 1000)]
+               (4, 4, 0), (5, 2, 0), (5, 4, 0), (2, 1, 512), (1, 2, 300), (3, 4, 1000)]
 
 
 @pytest.mark.parametrize("dtype", ["f32", "bf16", "f16", "f64"])
