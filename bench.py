@@ -66,20 +66,26 @@ def parse():
     ap.add_argument("--no-host-inclusive", action="store_true")
     ap.add_argument("--no-small", action="store_true")
     ap.add_argument("--allgather", action="store_true", help="also time the RCCL all-gather of the buckets")
+    ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) for real runs; gloo only to rehearse "
+                                                             "several ranks on one GPU")
     ap.add_argument("--sweep", action="store_true", help="interleaved A/B of launch variants, then exit")
     ap.add_argument("--sweep-cfgs", default="", help="variant,chunks,grid;... (default: built-in list)")
     ap.add_argument("--no-ceilings", action="store_true", help="skip the probe ceilings in --sweep")
     return ap.parse_args()
 
 
-def setup_dist():
+def setup_dist(backend="nccl"):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local % max(1, torch.cuda.device_count()))
+    torch.cuda.set_device(dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    return rank, world, torch.device("cuda", local)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
+    return rank, world, dev
 
 
 def barrier(world):
@@ -117,7 +123,8 @@ def time_kernel(fn, steps, warmup, world):
     wall = time.perf_counter() - t0
     ev_s = ev0.elapsed_time(ev1) / 1e3
     if world > 1:
-        t = torch.tensor([wall, ev_s], dtype=torch.float64, device="cuda")
+        on_gpu = dist.get_backend() == "nccl"
+        t = torch.tensor([wall, ev_s], dtype=torch.float64, device="cuda" if on_gpu else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         wall, ev_s = float(t[0]), float(t[1])
     return wall, ev_s
@@ -292,7 +299,7 @@ def measured_ceilings(device, nbytes=1 << 30):
 
 def main():
     args = parse()
-    rank, world, device = setup_dist()
+    rank, world, device = setup_dist(args.dist_backend)
     from accdfl_amd import _lib
     from accdfl_amd.core import wsum
 
@@ -365,7 +372,7 @@ def main():
             "us_per_launch": round(kern_s * 1e6, 2),
         },
     }
-    if args.allgather and world > 1:
+    if args.allgather and world > 1 and args.dist_backend == "nccl":
         from accdfl_amd.core.sharding import BucketShardedFedAvg
 
         sh = BucketShardedFedAvg(p * world, dt, device=device)

@@ -6,7 +6,7 @@
 # then summarises them into profiles/<round>_*.  Usage: bash profiles/collect.sh r01 [bench args]
 set -euo pipefail
 ROUND=${1:-r01}; shift || true
-ARGS="--steps 50 --warmup 5 --no-cpu-baseline --no-host-inclusive --no-small $*"
+ARGS="$*"  # default: the exact bench.py command the driver runs
 OUT=gpurun_out/prof_$ROUND
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
