@@ -33,6 +33,7 @@
 #include <cstdint>
 #include <cstring>
 #include <string>
+#include <vector>
 
 #include "dlagg.h"
 
@@ -216,106 +217,143 @@ __device__ inline void store16(uint4* p, const uint4& v) {
   }
 }
 
-// ------------------------------------------------ register-stream kernel (v1/v2)
+// ------------------------------------------------------------ tile bodies
 //
-// Tile = kBlock * CH chunks; lane l of the block owns chunks tile_base + c*kBlock + l.
-// ACC_IN: the running sum starts from `out` (second and later passes of a
-// reduce with more than KMAX peers) instead of p0 * 0.
+// fold_tile: one tile = kBlock * CH chunks; lane l of the block owns chunks
+// base0 + c*kBlock + l.  Peers are folded in list order, loaded in groups of
+// kGroup so a group's kGroup*CH loads all issue before the first wait.
+// ACC_IN: the running sum starts from `out` (second and later passes of a reduce
+// with more than KMAX peers) instead of p0 * 0.
+template <int DT, int CH, bool NT, int SP, bool ACC_IN>
+__device__ __attribute__((always_inline)) inline void fold_tile(
+    const void* const* __restrict__ p, const typename Ops<DT>::w_t* __restrict__ w, int n_peers,
+    int64_t base0, int64_t n_chunks, uint4* __restrict__ out) {
+  using O = Ops<DT>;
+  using acc_t = typename O::acc_t;
+  constexpr int E = O::E;
+  const int64_t base = base0 + threadIdx.x;
+  // Lanes past the end of the last (partial) tile load a clamped, valid chunk and
+  // skip the store: loads stay unpredicated.
+  bool live[CH];
+  int64_t idx[CH];
+#pragma unroll
+  for (int c = 0; c < CH; ++c) {
+    live[c] = base + c * kBlock < n_chunks;
+    idx[c] = live[c] ? base + c * kBlock : n_chunks - 1;
+  }
+  acc_t acc[CH][E];
+  int k0 = 0;
+  if constexpr (ACC_IN) {
+#pragma unroll
+    for (int c = 0; c < CH; ++c) O::unpack(out[idx[c]], acc[c]);
+  }
+  for (; k0 + kGroup <= n_peers; k0 += kGroup) {
+    uint4 v[kGroup][CH];
+#pragma unroll
+    for (int g = 0; g < kGroup; ++g) {
+      const uint4* src = static_cast<const uint4*>(p[k0 + g]);
+#pragma unroll
+      for (int c = 0; c < CH; ++c) v[g][c] = load16<NT>(src + idx[c]);
+    }
+#pragma unroll
+    for (int g = 0; g < kGroup; ++g) {
+      const typename O::w_t wk = w[k0 + g];
+#pragma unroll
+      for (int c = 0; c < CH; ++c) {
+        acc_t x[E];
+        O::unpack(v[g][c], x);
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          if (!ACC_IN && g == 0 && k0 == 0) acc[c][e] = O::zero_mul(x[e]);  // fedavg.py:22
+          acc[c][e] = O::step(acc[c][e], wk, x[e]);                          // fedavg.py:25
+        }
+      }
+    }
+  }
+  for (; k0 < n_peers; ++k0) {  // remaining peers (< kGroup), same order
+    const uint4* src = static_cast<const uint4*>(p[k0]);
+    const typename O::w_t wk = w[k0];
+    uint4 v[CH];
+#pragma unroll
+    for (int c = 0; c < CH; ++c) v[c] = load16<NT>(src + idx[c]);
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      acc_t x[E];
+      O::unpack(v[c], x);
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        if (!ACC_IN && k0 == 0) acc[c][e] = O::zero_mul(x[e]);
+        acc[c][e] = O::step(acc[c][e], wk, x[e]);
+      }
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < CH; ++c)
+    if (live[c]) store16<SP>(out + idx[c], O::pack(acc[c]));
+}
+
+// Ragged tail (n_elems not a multiple of E): one element per lane, lanes < tail.
+template <int DT, bool ACC_IN>
+__device__ __attribute__((always_inline)) inline void fold_tail(
+    const void* const* __restrict__ p, const typename Ops<DT>::w_t* __restrict__ w, int n_peers,
+    int64_t n_chunks, int64_t n_elems, void* __restrict__ out_v) {
+  using O = Ops<DT>;
+  using acc_t = typename O::acc_t;
+  using elem_t = typename O::elem_t;
+  const int64_t j = n_chunks * O::E + threadIdx.x;
+  if (j >= n_elems) return;
+  elem_t* o = static_cast<elem_t*>(out_v);
+  acc_t acc = ACC_IN ? O::to_acc(o[j]) : acc_t(0);
+  for (int k = 0; k < n_peers; ++k) {
+    const acc_t x = O::to_acc(static_cast<const elem_t*>(p[k])[j]);
+    if (!ACC_IN && k == 0) acc = O::zero_mul(x);
+    acc = O::step(acc, w[k], x);
+  }
+  o[j] = O::from_acc(acc);
+}
+
+// ------------------------------------------------ register-stream kernel
+// One flat buffer per peer; tiles dealt to workgroups (grid-stride when the grid
+// is smaller than the tile count); block 0 also folds the ragged tail.
 template <int DT, int KMAX, int CH, bool NT, int SP, bool ACC_IN>
 __global__ __launch_bounds__(kBlock) void wsum_stream_kernel(
     const PeerTable<typename Ops<DT>::w_t, KMAX> tab, int n_peers, int64_t n_chunks,
     int64_t n_elems, void* __restrict__ out_v) {
-  using O = Ops<DT>;
-  using acc_t = typename O::acc_t;
-  using elem_t = typename O::elem_t;
-  constexpr int E = O::E;
-  uint4* __restrict__ out = static_cast<uint4*>(out_v);
   const int64_t tile_chunks = static_cast<int64_t>(kBlock) * CH;
   const int64_t n_tiles = (n_chunks + tile_chunks - 1) / tile_chunks;
+  for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x)
+    fold_tile<DT, CH, NT, SP, ACC_IN>(tab.p, tab.w, n_peers, tile * tile_chunks, n_chunks,
+                                      static_cast<uint4*>(out_v));
+  if (blockIdx.x == 0) fold_tail<DT, ACC_IN>(tab.p, tab.w, n_peers, n_chunks, n_elems, out_v);
+}
 
-  for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
-    const int64_t base = tile * tile_chunks + threadIdx.x;
-    // Lanes past the end of the last (partial) tile load a clamped, valid chunk
-    // and skip the store: loads stay unpredicated, so a group's 8*CH loads all
-    // issue before the first wait.
-    bool live[CH];
-    int64_t idx[CH];
-#pragma unroll
-    for (int c = 0; c < CH; ++c) {
-      live[c] = base + c * kBlock < n_chunks;
-      idx[c] = live[c] ? base + c * kBlock : n_chunks - 1;
-    }
+// ------------------------------------------------ multi-tensor kernel
+// Up to MAXSEG parameter tensors ("segments") of one model in ONE launch
+// (fedavg.py:24 walks them one by one).  Workgroup b finds its segment from the
+// cumulative tile counts (a short uniform scan: scalar code), then folds one CH=1
+// tile of it; the first tile of each segment also folds that segment's tail.
+template <typename W, int NP, int MAXSEG>
+struct SegTable {
+  const void* p[MAXSEG][NP];
+  void* out[MAXSEG];
+  int64_t tile_end[MAXSEG];  // cumulative tiles through segment s
+  int64_t n_elems[MAXSEG];
+  W w[NP];
+};
 
-    acc_t acc[CH][E];
-    int k0 = 0;
-    if constexpr (ACC_IN) {
-#pragma unroll
-      for (int c = 0; c < CH; ++c) {
-        O::unpack(out[idx[c]], acc[c]);
-      }
-    }
-    // Full groups of kGroup peers: all loads of the group issue before the first add.
-    for (; k0 + kGroup <= n_peers; k0 += kGroup) {
-      uint4 v[kGroup][CH];
-#pragma unroll
-      for (int g = 0; g < kGroup; ++g) {
-        const uint4* src = static_cast<const uint4*>(tab.p[k0 + g]);
-#pragma unroll
-        for (int c = 0; c < CH; ++c)
-          v[g][c] = load16<NT>(src + idx[c]);
-      }
-#pragma unroll
-      for (int g = 0; g < kGroup; ++g) {
-        const typename O::w_t w = tab.w[k0 + g];
-#pragma unroll
-        for (int c = 0; c < CH; ++c) {
-          acc_t x[E];
-          O::unpack(v[g][c], x);
-#pragma unroll
-          for (int e = 0; e < E; ++e) {
-            if (!ACC_IN && g == 0 && k0 == 0) acc[c][e] = O::zero_mul(x[e]);
-            acc[c][e] = O::step(acc[c][e], w, x[e]);
-          }
-        }
-      }
-    }
-    // Remaining peers (< kGroup), one at a time, same order.
-    for (; k0 < n_peers; ++k0) {
-      const uint4* src = static_cast<const uint4*>(tab.p[k0]);
-      const typename O::w_t w = tab.w[k0];
-      uint4 v[CH];
-#pragma unroll
-      for (int c = 0; c < CH; ++c)
-        v[c] = load16<NT>(src + idx[c]);
-#pragma unroll
-      for (int c = 0; c < CH; ++c) {
-        acc_t x[E];
-        O::unpack(v[c], x);
-#pragma unroll
-        for (int e = 0; e < E; ++e) {
-          if (!ACC_IN && k0 == 0) acc[c][e] = O::zero_mul(x[e]);
-          acc[c][e] = O::step(acc[c][e], w, x[e]);
-        }
-      }
-    }
-#pragma unroll
-    for (int c = 0; c < CH; ++c)
-        if (live[c]) store16<SP>(out + idx[c], O::pack(acc[c]));
-  }
-
-  // Ragged tail (n_elems not a multiple of E): one element per lane of block 0.
-  const int64_t tail0 = n_chunks * E;
-  if (blockIdx.x == 0 && tail0 + threadIdx.x < n_elems) {
-    const int64_t j = tail0 + threadIdx.x;
-    elem_t* o = static_cast<elem_t*>(out_v);
-    acc_t acc = ACC_IN ? O::to_acc(o[j]) : acc_t(0);
-    for (int k = 0; k < n_peers; ++k) {
-      const acc_t x = O::to_acc(static_cast<const elem_t*>(tab.p[k])[j]);
-      if (!ACC_IN && k == 0) acc = O::zero_mul(x);
-      acc = O::step(acc, tab.w[k], x);
-    }
-    o[j] = O::from_acc(acc);
-  }
+template <int DT, int NP, int MAXSEG, int SP>
+__global__ __launch_bounds__(kBlock) void wsum_multi_kernel(
+    const SegTable<typename Ops<DT>::w_t, NP, MAXSEG> tab, int n_seg, int n_peers) {
+  const int64_t b = blockIdx.x;
+  int s = 0;
+  while (s < n_seg - 1 && tab.tile_end[s] <= b) ++s;
+  const int64_t tile = b - (s ? tab.tile_end[s - 1] : 0);
+  const int64_t n_elems = tab.n_elems[s];
+  const int64_t n_chunks = n_elems / Ops<DT>::E;
+  if (tile * kBlock < n_chunks)
+    fold_tile<DT, 1, true, SP, false>(tab.p[s], tab.w, n_peers, tile * kBlock, n_chunks,
+                                      static_cast<uint4*>(tab.out[s]));
+  if (tile == 0) fold_tail<DT, false>(tab.p[s], tab.w, n_peers, n_chunks, n_elems, tab.out[s]);
 }
 
 // ---------------------------------------------------- scalar kernel (unaligned)
@@ -459,6 +497,48 @@ hipError_t run(const void* const* peers, const double* weights, int n, int64_t n
   return hipSuccess;
 }
 
+// Batches of up to MAXSEG tensors per launch (see wsum_multi_kernel).
+template <int DT, int NP, int MAXSEG>
+hipError_t launch_multi(const int* tensors, int count, const void* const* peer_ptrs, void* const* outs,
+                        const int64_t* numels, const double* weights, int n, hipStream_t s) {
+  using W = typename Ops<DT>::w_t;
+  SegTable<W, NP, MAXSEG> tab;
+  std::memset(&tab, 0, sizeof(tab));
+  for (int k = 0; k < n; ++k) tab.w[k] = static_cast<W>(weights[k]);
+  int64_t cum = 0;
+  for (int i = 0; i < count; ++i) {
+    const int t = tensors[i];
+    for (int k = 0; k < n; ++k) tab.p[i][k] = peer_ptrs[static_cast<int64_t>(t) * n + k];
+    tab.out[i] = outs[t];
+    tab.n_elems[i] = numels[t];
+    const int64_t chunks = numels[t] / Ops<DT>::E;
+    const int64_t tiles = chunks ? (chunks + kBlock - 1) / kBlock : 1;
+    cum += tiles;
+    tab.tile_end[i] = cum;
+  }
+  hipLaunchKernelGGL((wsum_multi_kernel<DT, NP, MAXSEG, 2>), dim3(static_cast<unsigned>(cum)), dim3(kBlock), 0, s,
+                     tab, count, n);
+  return hipGetLastError();
+}
+
+template <int DT, int NP, int MAXSEG>
+hipError_t run_multi(const std::vector<int>& packed, const void* const* peer_ptrs, void* const* outs,
+                     const int64_t* numels, const double* weights, int n, hipStream_t s) {
+  for (size_t i = 0; i < packed.size(); i += MAXSEG) {
+    const int count = static_cast<int>(packed.size() - i < MAXSEG ? packed.size() - i : MAXSEG);
+    hipError_t e = launch_multi<DT, NP, MAXSEG>(packed.data() + i, count, peer_ptrs, outs, numels, weights, n, s);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+template <int DT>
+hipError_t run_multi_dt(const std::vector<int>& packed, const void* const* peer_ptrs, void* const* outs,
+                        const int64_t* numels, const double* weights, int n, hipStream_t s) {
+  if (n <= 8) return run_multi<DT, 8, 32>(packed, peer_ptrs, outs, numels, weights, n, s);
+  return run_multi<DT, 32, 8>(packed, peer_ptrs, outs, numels, weights, n, s);
+}
+
 int elem_size(int dtype) {
   switch (dtype) {
     case DLA_F32: return 4;
@@ -546,11 +626,40 @@ int dla_wsum_multi(int dtype, int n_tensors, const void* const* peer_ptrs, void*
   g_last_error.clear();
   if (n_tensors < 0 || (n_tensors > 0 && (!peer_ptrs || !outs || !numels)))
     return fail(DLA_E_INVALID, "dla_wsum_multi: bad tensor table");
+  const int es = elem_size(dtype);
+  if (es == 0) return fail(DLA_E_INVALID, "dla_wsum_multi: unknown dtype " + std::to_string(dtype));
+  if (n_peers < 1 || !weights) return fail(DLA_E_INVALID, "dla_wsum_multi: n_peers must be >= 1");
+  // Small, 16-byte aligned tensors share launches (<= 32 peers); large or unaligned
+  // tensors, and passes of more peers, take the single-tensor path.
+  constexpr int64_t kOwnLaunchBytes = 32ll << 20;
+  std::vector<int> packed;
   for (int t = 0; t < n_tensors; ++t) {
-    const int rc = wsum_impl(dtype, peer_ptrs + static_cast<int64_t>(t) * n_peers, weights, n_peers,
-                             numels[t], outs[t], stream, nullptr);
+    if (numels[t] < 0) return fail(DLA_E_INVALID, "dla_wsum_multi: negative numel");
+    if (numels[t] == 0) continue;
+    bool ok = n_peers <= 32 && numels[t] * es < kOwnLaunchBytes && outs[t] &&
+              (reinterpret_cast<uintptr_t>(outs[t]) & 15u) == 0;
+    for (int k = 0; ok && k < n_peers; ++k) {
+      const void* q = peer_ptrs[static_cast<int64_t>(t) * n_peers + k];
+      ok = q && (reinterpret_cast<uintptr_t>(q) & 15u) == 0;
+    }
+    if (ok) {
+      packed.push_back(t);
+      continue;
+    }
+    const int rc = wsum_impl(dtype, peer_ptrs + static_cast<int64_t>(t) * n_peers, weights, n_peers, numels[t],
+                             outs[t], stream, nullptr);
     if (rc != DLA_OK) return rc;
   }
+  if (packed.empty()) return DLA_OK;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  hipError_t e;
+  switch (dtype) {
+    case DLA_F32: e = run_multi_dt<DLA_F32>(packed, peer_ptrs, outs, numels, weights, n_peers, s); break;
+    case DLA_BF16: e = run_multi_dt<DLA_BF16>(packed, peer_ptrs, outs, numels, weights, n_peers, s); break;
+    case DLA_F16: e = run_multi_dt<DLA_F16>(packed, peer_ptrs, outs, numels, weights, n_peers, s); break;
+    default: e = run_multi_dt<DLA_F64>(packed, peer_ptrs, outs, numels, weights, n_peers, s); break;
+  }
+  if (e != hipSuccess) return fail(static_cast<int>(e), std::string("dla_wsum_multi: ") + hipGetErrorString(e));
   return DLA_OK;
 }
 

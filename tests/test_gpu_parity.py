@@ -223,3 +223,44 @@ def test_google_speech_full_size_bf16_sampled():
     sample = slab[:, :numel].index_select(1, idx).cpu()
     want = c_wsum([_bits(sample[k].contiguous(), "bf16") for k in range(n)], w, "bf16")
     assert same_bits(_bits(out[idx], "bf16"), want, "bf16")
+
+
+@pytest.mark.parametrize("n", [1, 8, 20, 40])
+def test_multi_tensor_batches(n):
+    """dla_wsum_multi: >32 tensors (several fused launches), ragged sizes, an empty
+    tensor, an unaligned view and one tensor above the own-launch size, per peer count."""
+    from accdfl_amd.core import wsum
+
+    rng = np.random.default_rng(n)
+    sizes = [int(x) for x in rng.integers(1, 5000, size=37)] + [0, 3, 9_000_001]
+    g = torch.Generator().manual_seed(n)
+    peers_cpu = [[(torch.randn(sz, generator=g) * 0.05) for sz in sizes] for _ in range(n)]
+    dev = [[t.cuda() for t in pl] for pl in peers_cpu]
+    # one unaligned view (4-byte offset) in tensor 5 of every peer
+    for k in range(n):
+        pad = torch.zeros(sizes[5] + 1, device="cuda")
+        pad[1:] = dev[k][5]
+        dev[k][5] = pad[1:]
+    w = [float(x) for x in rng.dirichlet(np.ones(n))]
+    outs = [torch.empty(sz, device="cuda") for sz in sizes]
+    wsum.wsum_multi(dev, w, outs)
+    torch.cuda.synchronize()
+    for i, sz in enumerate(sizes):
+        want = fedavg_bits([peers_cpu[k][i].numpy() for k in range(n)], w, "f32")
+        assert same_bits(outs[i].cpu().numpy(), want, "f32"), "tensor %d (numel %d)" % (i, sz)
+
+
+def test_multi_tensor_bf16_gnlenet_shapes_one_launch():
+    """Device-resident GNLeNet (14 tensors, configs[1]) in bf16 through the fused path."""
+    from accdfl_amd.core import wsum
+
+    shapes = [(32, 3, 5, 5), (32,), (32,), (32,), (32, 32, 5, 5), (32,), (32,), (32,), (64, 32, 5, 5), (64,),
+              (64,), (64,), (10, 576), (10,)]
+    g = torch.Generator().manual_seed(3)
+    peers = [[(torch.randn(s, generator=g) * 0.05).to(torch.bfloat16) for s in shapes] for _ in range(8)]
+    w = [0.125] * 8
+    outs = [torch.empty(s, dtype=torch.bfloat16, device="cuda") for s in shapes]
+    wsum.wsum_multi([[t.cuda() for t in pl] for pl in peers], w, outs)
+    for i in range(len(shapes)):
+        want = fedavg_bits([_bits(peers[k][i].reshape(-1), "bf16") for k in range(8)], w, "bf16")
+        assert same_bits(_bits(outs[i].reshape(-1), "bf16"), want, "bf16"), i
