@@ -196,14 +196,18 @@ def host_inclusive(n, p, reps=5):
 
 
 def small_configs(device, steps=200):
-    from accdfl_amd.core import wsum
+    """Device-resident reduces at the BASELINE configs' own model sizes, launched through a
+    prepared dla_plan (what a PeerSlab round pays)."""
+    from accdfl_amd import _lib
 
     res = {}
     for name, (n, p) in SMALL.items():
         slab = make_slab(n, (p + 63) // 64 * 64, torch.float32, device, 1000)
         w = [float(1.0 / n)] * n
         out = torch.empty(p, dtype=torch.float32, device=device)
-        wall, ev = time_kernel(lambda: wsum.wsum_rows(slab, w, p, out=out), steps, 20, 1)
+        plan = _lib.Plan(_lib.DLA_F32, [slab[k].data_ptr() for k in range(n)], w, p, out.data_ptr())
+        sp = torch.cuda.current_stream().cuda_stream
+        wall, ev = time_kernel(lambda: plan.launch(sp), steps, 20, 1)
         res[name] = {"GB/s": round((n + 1) * p * 4 / (ev / steps) / 1e9, 1), "us_per_reduce": round(ev / steps * 1e6, 2),
                      "bytes": (n + 1) * p * 4, "note": "fits the 256 MiB Infinity Cache; launch/latency-bound"}
         del slab

@@ -41,6 +41,10 @@ EXPORTED = (
     "dla_wsum_ex",
     "dla_wsum_slab",
     "dla_wsum_multi",
+    "dla_plan_create",
+    "dla_plan_set_weights",
+    "dla_plan_launch",
+    "dla_plan_destroy",
 )
 
 
@@ -104,6 +108,16 @@ class _Lib:
                                       ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_double), ctypes.c_int,
                                       vp]
         so.dla_wsum_multi.restype = ctypes.c_int
+        so.dla_plan_create.argtypes = [ctypes.POINTER(vp), ctypes.c_int, ctypes.POINTER(vp),
+                                       ctypes.POINTER(ctypes.c_double), ctypes.c_int, ctypes.c_int64, vp,
+                                       ctypes.POINTER(LaunchCfg)]
+        so.dla_plan_create.restype = ctypes.c_int
+        so.dla_plan_set_weights.argtypes = [vp, ctypes.POINTER(ctypes.c_double)]
+        so.dla_plan_set_weights.restype = ctypes.c_int
+        so.dla_plan_launch.argtypes = [vp, vp]
+        so.dla_plan_launch.restype = ctypes.c_int
+        so.dla_plan_destroy.argtypes = [vp]
+        so.dla_plan_destroy.restype = None
         v = so.dla_version()
         if v != ABI_VERSION:
             raise RuntimeError("libdlagg ABI version %d, expected %d" % (v, ABI_VERSION))
@@ -185,3 +199,35 @@ def wsum_multi_ptrs(dtype_code: int, peer_ptrs: Sequence[int], out_ptrs: Sequenc
     rc = L.so.dla_wsum_multi(dtype_code, t, _ptr_array(peer_ptrs), _ptr_array(out_ptrs), num, _dbl_array(weights),
                              n, stream_ptr)
     L.check(rc, "dla_wsum_multi")
+
+
+class Plan:
+    """dla_plan_t: a prepared reduce over fixed device buffers (launch-only per call)."""
+
+    def __init__(self, dtype_code: int, peer_ptrs: Sequence[int], weights: Sequence[float], n_elems: int,
+                 out_ptr: int, cfg: Optional[LaunchCfg] = None):
+        L = lib()
+        self._so = L.so
+        self._check = L.check
+        self.n_peers = len(peer_ptrs)
+        h = ctypes.c_void_p()
+        rc = L.so.dla_plan_create(ctypes.byref(h), dtype_code, _ptr_array(peer_ptrs), _dbl_array(weights),
+                                  self.n_peers, n_elems, out_ptr, ctypes.byref(cfg) if cfg is not None else None)
+        L.check(rc, "dla_plan_create")
+        self._h = h
+
+    def set_weights(self, weights: Sequence[float]) -> None:
+        if len(weights) != self.n_peers:
+            raise AssertionError("len(weights) != n_peers")
+        self._check(self._so.dla_plan_set_weights(self._h, _dbl_array(weights)), "dla_plan_set_weights")
+
+    def launch(self, stream_ptr: int) -> None:
+        rc = self._so.dla_plan_launch(self._h, stream_ptr)
+        if rc != 0:
+            self._check(rc, "dla_plan_launch")
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            self._so.dla_plan_destroy(h)
+            self._h = None

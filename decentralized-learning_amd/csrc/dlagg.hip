@@ -32,6 +32,7 @@
 
 #include <cstdint>
 #include <cstring>
+#include <new>
 #include <string>
 #include <vector>
 
@@ -588,6 +589,16 @@ int wsum_impl(int dtype, const void* const* peers, const double* weights, int n_
 
 }  // namespace
 
+struct dla_plan {
+  int dtype;
+  std::vector<const void*> peers;
+  std::vector<double> weights;
+  int64_t n_elems;
+  void* out;
+  dla_launch_cfg_t cfg;
+  bool has_cfg;
+};
+
 extern "C" {
 
 int dla_version(void) { return DLA_ABI_VERSION; }
@@ -662,5 +673,43 @@ int dla_wsum_multi(int dtype, int n_tensors, const void* const* peer_ptrs, void*
   if (e != hipSuccess) return fail(static_cast<int>(e), std::string("dla_wsum_multi: ") + hipGetErrorString(e));
   return DLA_OK;
 }
+
+int dla_plan_create(dla_plan_t** plan, int dtype, const void* const* peers, const double* weights, int n_peers,
+                    int64_t n_elems, void* out, const dla_launch_cfg_t* cfg) {
+  g_last_error.clear();
+  if (!plan) return fail(DLA_E_INVALID, "dla_plan_create: null plan");
+  *plan = nullptr;
+  if (elem_size(dtype) == 0) return fail(DLA_E_INVALID, "dla_plan_create: unknown dtype");
+  if (n_peers < 1 || !peers || !weights || n_elems < 0 || (n_elems > 0 && !out))
+    return fail(DLA_E_INVALID, "dla_plan_create: bad arguments");
+  for (int k = 0; k < n_peers; ++k)
+    if (!peers[k]) return fail(DLA_E_INVALID, "dla_plan_create: null peer pointer");
+  dla_plan* p = new (std::nothrow) dla_plan;
+  if (!p) return fail(DLA_E_INVALID, "dla_plan_create: out of host memory");
+  p->dtype = dtype;
+  p->peers.assign(peers, peers + n_peers);
+  p->weights.assign(weights, weights + n_peers);
+  p->n_elems = n_elems;
+  p->out = out;
+  p->has_cfg = cfg != nullptr;
+  if (cfg) p->cfg = *cfg;
+  *plan = p;
+  return DLA_OK;
+}
+
+int dla_plan_set_weights(dla_plan_t* plan, const double* weights) {
+  g_last_error.clear();
+  if (!plan || !weights) return fail(DLA_E_INVALID, "dla_plan_set_weights: null argument");
+  std::memcpy(plan->weights.data(), weights, sizeof(double) * plan->weights.size());
+  return DLA_OK;
+}
+
+int dla_plan_launch(const dla_plan_t* plan, void* stream) {
+  if (!plan) return fail(DLA_E_INVALID, "dla_plan_launch: null plan");
+  return wsum_impl(plan->dtype, plan->peers.data(), plan->weights.data(), static_cast<int>(plan->peers.size()),
+                   plan->n_elems, plan->out, stream, plan->has_cfg ? &plan->cfg : nullptr);
+}
+
+void dla_plan_destroy(dla_plan_t* plan) { delete plan; }
 
 }  // extern "C"

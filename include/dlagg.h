@@ -103,6 +103,17 @@ int dla_wsum_multi(int dtype, int n_tensors, const void* const* peer_ptrs, void*
 /* Largest peer count one kernel pass takes (kernel-argument pointer table). */
 int dla_max_peers_per_pass(void);
 
+/* Prepared reduce: validates and stores the peer/out pointers once, so a round
+ * that reduces the same device buffers again (a PeerSlab every round, a benchmark
+ * loop) pays only the launch.  Same semantics as dla_wsum. */
+typedef struct dla_plan dla_plan_t;
+int dla_plan_create(dla_plan_t** plan, int dtype, const void* const* peers, const double* weights,
+                    int n_peers, int64_t n_elems, void* out, const dla_launch_cfg_t* cfg);
+/* Replace the weights (e.g. new GL ages, fedavg.py:14-17 defaulting done by the caller). */
+int dla_plan_set_weights(dla_plan_t* plan, const double* weights);
+int dla_plan_launch(const dla_plan_t* plan, void* stream);
+void dla_plan_destroy(dla_plan_t* plan);
+
 #ifdef __cplusplus
 }
 #endif

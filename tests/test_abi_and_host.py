@@ -14,7 +14,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def _declared_symbols():
     text = open(os.path.join(ROOT, "include", "dlagg.h")).read()
-    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(dla_\w+)\s*\(", text, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|void|const char\*)\s+(dla_\w+)\s*\(", text, re.M)))
 
 
 @pytest.fixture(scope="module")

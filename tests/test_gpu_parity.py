@@ -264,3 +264,24 @@ def test_multi_tensor_bf16_gnlenet_shapes_one_launch():
     for i in range(len(shapes)):
         want = fedavg_bits([_bits(peers[k][i].reshape(-1), "bf16") for k in range(8)], w, "bf16")
         assert same_bits(_bits(outs[i].reshape(-1), "bf16"), want, "bf16"), i
+
+
+def test_plan_launch_and_set_weights():
+    from accdfl_amd import _lib
+    from accdfl_amd.core import wsum
+
+    peers = _random_peers(6, 123_457, "f32", seed=21)
+    dev = [p.cuda() for p in peers]
+    out = torch.empty(123_457, device="cuda")
+    w1 = [0.1, 0.2, 0.3, 0.1, 0.2, 0.1]
+    w2 = [1.0, 0.0, -0.5, 0.25, 0.125, 2.0]
+    plan = _lib.Plan(_lib.DLA_F32, [d.data_ptr() for d in dev], w1, out.numel(), out.data_ptr())
+    sp = torch.cuda.current_stream().cuda_stream
+    plan.launch(sp)
+    torch.cuda.synchronize()
+    assert same_bits(_bits(out, "f32"), fedavg_bits([p.numpy() for p in peers], w1, "f32"), "f32")
+    plan.set_weights(w2)
+    plan.launch(sp)
+    torch.cuda.synchronize()
+    assert same_bits(_bits(out, "f32"), fedavg_bits([p.numpy() for p in peers], w2, "f32"), "f32")
+    assert same_bits(_bits(wsum.wsum(dev, w2), "f32"), _bits(out, "f32"), "f32")
