@@ -69,6 +69,7 @@ def parse():
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) for real runs; gloo only to rehearse "
                                                              "several ranks on one GPU")
     ap.add_argument("--sweep", action="store_true", help="interleaved A/B of launch variants, then exit")
+    ap.add_argument("--host-breakdown", action="store_true", help="time the host-inclusive phases, then exit")
     ap.add_argument("--sweep-cfgs", default="", help="variant,chunks,grid;... (default: built-in list)")
     ap.add_argument("--no-ceilings", action="store_true", help="skip the probe ceilings in --sweep")
     return ap.parse_args()
@@ -192,7 +193,49 @@ def host_inclusive(n, p, reps=5):
         times.append(time.perf_counter() - t0)
     med = statistics.median(times)
     return {"value": round((n + 1) * p * 4 / med / 1e9, 3), "unit": "GB/s", "ms": round(med * 1e3, 2),
-            "path": "FedAvg.aggregate(CPU nn.Modules): deepcopy + pinned pack + H2D + reduce + D2H + unpack"}
+            "path": "FedAvg.aggregate(CPU nn.Modules): deepcopy (params uninitialised, pinned) + pinned pack + H2D + reduce + D2H into the result"}
+
+
+def host_breakdown(n, p, device):
+    """Phases of FedAvg.aggregate on CPU modules (the host-inclusive path), timed apart."""
+    import copy
+
+    from torch import nn
+
+    gen = torch.Generator().manual_seed(2000)
+    models = []
+    for _ in range(n):
+        m = nn.Module()
+        m.w = nn.Parameter(torch.randn(p, generator=gen) * 0.05)
+        models.append(m)
+    pinned = torch.empty((n, p), pin_memory=True)
+    dev = torch.empty((n, p), device=device)
+    out = torch.empty(p, device=device)
+    h_out = torch.empty(p, pin_memory=True)
+    res = {}
+
+    def t(name, fn, reps=3):
+        fn()
+        torch.cuda.synchronize()
+        ts = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            fn()
+            torch.cuda.synchronize()
+            ts.append(time.perf_counter() - t0)
+        res[name] = round(min(ts) * 1e3, 2)
+
+    t("deepcopy_model0_ms", lambda: copy.deepcopy(models[0]))
+    t("pack_pinned_ms", lambda: [pinned[k].copy_(models[k].w.detach()) for k in range(n)])
+    t("h2d_pinned_ms", lambda: dev.copy_(pinned, non_blocking=True))
+    t("h2d_pageable_ms", lambda: [dev[k].copy_(models[k].w.detach(), non_blocking=False) for k in range(n)])
+    from accdfl_amd.core import wsum
+    t("reduce_ms", lambda: wsum.wsum_rows(dev, [1.0 / n] * n, p, out=out))
+    t("d2h_pinned_ms", lambda: h_out.copy_(out, non_blocking=True))
+    c = copy.deepcopy(models[0])
+    t("unpack_ms", lambda: c.w.data.copy_(h_out))
+    res["threads"] = torch.get_num_threads()
+    return res
 
 
 def small_configs(device, steps=200):
@@ -291,10 +334,11 @@ def measured_ceilings(device, nbytes=1 << 30):
     so.dlp_mread8.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
                               ctypes.c_int, ctypes.c_void_p]
     for ch in (1, 2, 4):
-        for wr in (0, 1):
+        for wr in (0, 1, 2):
             _, ev = time_kernel(lambda: so.dlp_mread8(arr, each, dst.data_ptr(), sink.data_ptr(), ch, wr, sp()),
                                 30, 3, 1)
-            res["mread8_ch%d_write%d" % (ch, wr)] = round((8 + wr) * each / (ev / 30) / 1e9, 1)
+            res["mread8_ch%d_write%s" % (ch, ("0", "1", "1_sc1")[wr])] = round((8 + min(wr, 1)) * each /
+                                                                                (ev / 30) / 1e9, 1)
         _, ev = time_kernel(lambda: so.dlp_mread8(arr, each, srcs[0].data_ptr(), sink.data_ptr(), ch, 1, sp()),
                             30, 3, 1)
         res["mread8_ch%d_write_inplace" % ch] = round(9 * each / (ev / 30) / 1e9, 1)
@@ -310,6 +354,9 @@ def main():
     _lib.lib()  # fail loudly here if the HIP library is missing
     if args.sweep:
         sweep(args, device)
+        return
+    if args.host_breakdown:
+        print(json.dumps(host_breakdown(args.peers, args.params, device)))
         return
     dt = {"f32": torch.float32, "bf16": torch.bfloat16, "f16": torch.float16}[args.dtype]
     es = 4 if args.dtype == "f32" else 2

@@ -12,14 +12,13 @@ summation order = arrival order.
 """
 from __future__ import annotations
 
-import copy
 from typing import Dict, List, Optional
 
 import torch
 import torch.nn as nn
 
 from accdfl_amd.core.gradient_aggregation import GradientAggregationMethod
-from accdfl_amd.core.gradient_aggregation.fedavg import FedAvg
+from accdfl_amd.core.gradient_aggregation.fedavg import FedAvg, _center_copy
 
 
 class ModelManager:
@@ -66,15 +65,18 @@ class DeviceModelManager(ModelManager):
         self._capacity = capacity
         self._device = device
         self.slab: Optional["PeerSlab"] = None
-        self._first_model: Optional[nn.Module] = None
 
     def process_incoming_trained_model(self, peer_pk: bytes, incoming_model: nn.Module):
         if peer_pk in self.incoming_trained_models:
             return
-        if self.slab is None:
-            self.slab = self._slab_cls.for_model(incoming_model, capacity=self._capacity, device=self._device)
-        self.slab.stage(incoming_model)
         self.incoming_trained_models[peer_pk] = incoming_model
+        try:
+            if self.slab is None:
+                self.slab = self._slab_cls.for_model(incoming_model, capacity=self._capacity, device=self._device)
+            if self.slab.matches(list(incoming_model.parameters())):
+                self.slab.stage(incoming_model)
+        except TypeError:
+            pass  # mixed-dtype model: the round falls back to FedAvg.aggregate (uniform_with is False)
 
     def reset_incoming_trained_models(self):
         super().reset_incoming_trained_models()
@@ -91,6 +93,6 @@ class DeviceModelManager(ModelManager):
         else:
             assert len(weights) == n
         with torch.no_grad():
-            center = copy.deepcopy(models[0])
+            center = _center_copy(models[0])  # deepcopy(models[0]) minus the parameter values
             self.slab.reduce_into(list(center.parameters()), weights)
         return center

@@ -187,6 +187,11 @@ class PeerSlab:
             for p, v in zip(params, self.unflatten(flat)):
                 p.copy_(v)
             return
+        if all(p.is_pinned() and p.is_contiguous() for p in params):
+            for p, v in zip(params, torch.split(flat, self.numels)):
+                p.view(-1).copy_(v, non_blocking=True)  # D2H straight into the result
+            torch.cuda.current_stream(self.device).synchronize()
+            return
         if self._h_out is None or self._h_out.numel() < self.total:
             self._h_out = torch.empty(self.pitch, dtype=self.dtype, pin_memory=True)
         h = self._h_out[: self.total]

@@ -58,7 +58,8 @@ __global__ __launch_bounds__(256) void mread_kernel(const u32x4* const* __restri
                                                      const u32x4* s0, const u32x4* s1, const u32x4* s2,
                                                      const u32x4* s3, const u32x4* s4, const u32x4* s5,
                                                      const u32x4* s6, const u32x4* s7, int64_t n_chunks,
-                                                     u32x4* __restrict__ dst, uint32_t* __restrict__ sink) {
+                                                     u32x4* __restrict__ dst, uint32_t* __restrict__ sink,
+                                                     int sc1) {
   const u32x4* src[8] = {s0, s1, s2, s3, s4, s5, s6, s7};
   const int64_t base = static_cast<int64_t>(blockIdx.x) * 256 * CH + threadIdx.x;
   int64_t idx[CH];
@@ -78,7 +79,12 @@ __global__ __launch_bounds__(256) void mread_kernel(const u32x4* const* __restri
 #pragma unroll
     for (int k = 1; k < N_SRC; ++k) acc ^= v[k][c];
     if constexpr (WRITE) {
-      if (base + c * 256 < n_chunks) dst[idx[c]] = acc;
+      if (base + c * 256 < n_chunks) {
+        if (sc1)
+          asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(dst + idx[c]), "v"(acc) : "memory");
+        else
+          dst[idx[c]] = acc;
+      }
     } else {
       const uint32_t f = acc.x ^ acc.y ^ acc.z ^ acc.w;
       if (f == 0x9e3779b9u) sink[blockIdx.x & 1023] = f;
@@ -130,7 +136,7 @@ int dlp_copy(const void* src, void* dst, int64_t bytes, int nt, void* stream) {
   return static_cast<int>(hipGetLastError());
 }
 
-// 8-stream read (write = 0) or read + write (write = 1) of `bytes_each` per stream.
+// 8-stream read (write = 0), read + write (write = 1) or read + sc1 write (write = 2).
 int dlp_mread8(const void* const* srcs, int64_t bytes_each, void* dst, void* sink, int chunks, int write,
                void* stream) {
   if (!srcs || bytes_each < 16) return -1;
@@ -141,7 +147,7 @@ int dlp_mread8(const void* const* srcs, int64_t bytes_each, void* dst, void* sin
 #define DLP_L(CHV, W)                                                                                       \
   hipLaunchKernelGGL((mread_kernel<8, CHV, W>), dim3((n + 256 * CHV - 1) / (256 * CHV)), dim3(256), 0, s,   \
                      nullptr, p[0], p[1], p[2], p[3], p[4], p[5], p[6], p[7], n, static_cast<u32x4*>(dst), \
-                     static_cast<uint32_t*>(sink))
+                     static_cast<uint32_t*>(sink), write == 2)
   if (chunks == 1) { if (write) DLP_L(1, true); else DLP_L(1, false); }
   else if (chunks == 2) { if (write) DLP_L(2, true); else DLP_L(2, false); }
   else if (chunks == 4) { if (write) DLP_L(4, true); else DLP_L(4, false); }

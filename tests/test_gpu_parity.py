@@ -285,3 +285,26 @@ def test_plan_launch_and_set_weights():
     torch.cuda.synchronize()
     assert same_bits(_bits(out, "f32"), fedavg_bits([p.numpy() for p in peers], w2, "f32"), "f32")
     assert same_bits(_bits(wsum.wsum(dev, w2), "f32"), _bits(out, "f32"), "f32")
+
+
+def test_device_model_manager_falls_back_on_mixed_layouts():
+    """A round whose models do not share one layout is still aggregated exactly
+    (through FedAvg.aggregate), with the registry order kept."""
+    from types import SimpleNamespace
+
+    from torch import nn
+
+    from accdfl_amd.core.gradient_aggregation import GradientAggregationMethod
+    from accdfl_amd.core.model_manager import DeviceModelManager
+    from oracle.fedavg_oracle import fedavg_param_lists
+
+    torch.manual_seed(4)
+    a, b, c = nn.Linear(5, 3), nn.Linear(5, 3), nn.Linear(5, 3, bias=False)
+    mm = DeviceModelManager(None, SimpleNamespace(gradient_aggregation=GradientAggregationMethod.FEDAVG))
+    for pk, m in ((b"a", a), (b"c", c), (b"b", b)):
+        mm.process_incoming_trained_model(pk, m)
+    w = [0.5, 0.25, 0.25]
+    out = mm.aggregate_trained_models(w)
+    want = fedavg_param_lists([[p.detach().numpy() for p in m.parameters()] for m in (a, c, b)], w, "f32")
+    for p, q in zip(out.parameters(), want):
+        assert same_bits(p.detach().numpy(), q, "f32")
