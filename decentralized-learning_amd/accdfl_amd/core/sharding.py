@@ -15,8 +15,11 @@ Exchange steps exist only where data really has to move:
   the host path instead copies each bucket D2H straight into the result.
 * ``transpose_peer_sharded``: when peers arrive whole on different ranks (rank r
   received peers [r*m, (r+1)*m)), one RCCL all-to-all turns "peer-sharded" into
-  "bucket-sharded" so the reduce stays in list order and bit-exact (a local partial
-  sum + reduce-scatter would change the summation order).
+  "bucket-sharded" so the reduce stays in list order and bit-exact.
+* ``aggregate_peer_sharded(exact=False)``: the north star's reduce-scatter form — local
+  partial fold of each rank's peers, RCCL reduce-scatter(sum), all-gather.  m x less
+  traffic than the all-to-all, but the cross-rank sum is re-associated, so it is a
+  stated-tolerance mode, never the default.
 
 Every collective goes through ``torch.distributed`` (backend "nccl" = RCCL on ROCm;
 "gloo" in the CPU tests).  The per-bucket reduce is the libdlagg kernel by default;
@@ -116,8 +119,36 @@ class BucketShardedFedAvg:
         return recv.view(self.world * m, self.bucket_len)
 
     def aggregate_peer_sharded(self, local_peers: torch.Tensor, weights: Optional[Sequence[float]] = None,
-                               gather: bool = True) -> torch.Tensor:
-        """Peers split across ranks -> all-to-all -> bucket reduce -> (all-gather)."""
-        rows = self.transpose_peer_sharded(local_peers)
-        out = self.reduce_bucket(list(rows), weights)
+                               gather: bool = True, exact: bool = True) -> torch.Tensor:
+        """Peers split across ranks (rank r holds peers r*m .. r*m+m-1).
+
+        exact=True (default): all-to-all -> bucket reduce -> (all-gather); bit-identical
+        to the reference.  exact=False: each rank folds its own m peers (list order,
+        libdlagg), then one RCCL reduce-scatter(sum) of the partial models and the
+        all-gather.  That moves m x fewer bytes than the all-to-all, but it re-associates
+        the sum across ranks, so it is NOT bit-exact.  Both orders are within
+        (N-1)*u*sum|w_k p_k| of the exact sum (u = 2^-24), so per element
+        |this - reference| <= N * 2^-23 * sum_k |w_k p_k| (fp32; the tolerance the tests state)."""
+        if exact:
+            rows = self.transpose_peer_sharded(local_peers)
+            out = self.reduce_bucket(list(rows), weights)
+            return self.all_gather(out) if gather else out
+        m = local_peers.shape[0]
+        n = m * self.world
+        if not weights:
+            weights = [float(1. / n) for _ in range(n)]
+        else:
+            assert len(weights) == n
+        mine = list(weights[self.rank * m:(self.rank + 1) * m])
+        partial = torch.zeros(self.world * self.bucket_len, dtype=self.dtype, device=local_peers.device)
+        if self.n_elems:
+            self.reducer([local_peers[k] for k in range(m)], mine, partial[: self.n_elems])
+        out = torch.empty(self.bucket_len, dtype=self.dtype, device=local_peers.device)
+        if self.world == 1:
+            out.copy_(partial)
+        elif dist.get_backend(self.group) == "gloo":  # gloo has no reduce-scatter: all-reduce + slice
+            dist.all_reduce(partial, group=self.group)
+            out.copy_(partial[self.rank * self.bucket_len:(self.rank + 1) * self.bucket_len])
+        else:
+            dist.reduce_scatter_tensor(out, partial, group=self.group)
         return self.all_gather(out) if gather else out

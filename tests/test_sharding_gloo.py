@@ -56,7 +56,8 @@ def _worker(rank, world, port, n_peers, n_elems, root, q):
         m = n_peers // world
         local = torch.from_numpy(peers[rank * m:(rank + 1) * m].copy())
         full2 = sh.aggregate_peer_sharded(local, weights)
-        q.put((rank, full.numpy().view(np.uint32).copy(), full2.numpy().view(np.uint32).copy()))
+        full3 = sh.aggregate_peer_sharded(local, weights, exact=False)
+        q.put((rank, full.numpy().view(np.uint32).copy(), full2.numpy().view(np.uint32).copy(), full3.numpy().copy()))
     finally:
         dist.destroy_process_group()
 
@@ -78,6 +79,10 @@ def test_sharded_fedavg_is_bit_exact(world, n_peers, n_elems):
         assert p.exitcode == 0
     peers, weights = _inputs(n_peers, n_elems)
     want = fedavg_bits(list(peers), weights, "f32").view(np.uint32)
-    for rank, full, full2 in results:
+    # tolerance of the reduce-scatter (re-associating) mode: N * 2^-23 * sum_k |w_k p_k|
+    bound = n_peers * 2.0 ** -23 * np.sum(np.abs(np.asarray(weights)[:, None] * peers.astype(np.float64)), axis=0)
+    for rank, full, full2, full3 in results:
         assert np.array_equal(full, want), "bucket-sharded rank %d" % rank
         assert np.array_equal(full2, want), "peer-sharded rank %d" % rank
+        err = np.abs(full3.astype(np.float64) - want.view(np.float32).astype(np.float64))
+        assert np.all(err <= bound + 1e-45), "reduce-scatter mode rank %d: max err %g" % (rank, err.max())
