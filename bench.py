@@ -61,6 +61,7 @@ def parse():
     ap.add_argument("--variant", type=int, default=0)
     ap.add_argument("--chunks", type=int, default=0)
     ap.add_argument("--grid", type=int, default=0)
+    ap.add_argument("--block", type=int, default=0)
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-inclusive", action="store_true")
@@ -72,6 +73,7 @@ def parse():
     ap.add_argument("--host-breakdown", action="store_true", help="time the host-inclusive phases, then exit")
     ap.add_argument("--sweep-cfgs", default="", help="variant,chunks,grid;... (default: built-in list)")
     ap.add_argument("--no-ceilings", action="store_true", help="skip the probe ceilings in --sweep")
+    ap.add_argument("--libs", default="", help="comma list of libdlagg builds to A/B in --sweep (same process)")
     return ap.parse_args()
 
 
@@ -272,7 +274,31 @@ def sweep(args, device):
     if args.sweep_cfgs:
         cfgs = [tuple(int(x) for x in item.split(",")) for item in args.sweep_cfgs.split(";") if item]
     else:
-        cfgs = [(v, c, g) for v in (1, 2, 3, 4, 5) for c in (1, 2, 4) for g in (0, 4096)]
+        cfgs = [(v, c, 0, b) for v in (1, 2, 4) for c in (1, 2, 4) for b in (64, 256)]
+    if args.libs:
+        import ctypes
+
+        libs = []
+        for path in args.libs.split(","):
+            so = ctypes.CDLL(os.path.abspath(path))
+            so.dla_wsum_ex.argtypes = _lib.lib().so.dla_wsum_ex.argtypes
+            libs.append((os.path.basename(path), so))
+        pa = _lib._ptr_array(ptrs)
+        wa = _lib._dbl_array(w)
+        res = {(name,) + c: [] for name, _ in libs for c in cfgs}
+        for rnd in range(7):
+            for name, so in libs:
+                for c in cfgs:
+                    cfg = _lib.LaunchCfg(*c)
+                    fn = lambda: so.dla_wsum_ex(code, pa, wa, len(ptrs), args.params, out.data_ptr(), sp,  # noqa
+                                                ctypes.byref(cfg))
+                    _, ev = time_kernel(fn, 50, 5, 1)
+                    res[(name,) + c].append(ev / 50)
+        byts = (args.peers + 1) * args.params * es
+        for t, k in sorted((statistics.median(v), k) for k, v in res.items()):
+            print(json.dumps({"lib": k[0], "cfg": k[1:], "us": round(t * 1e6, 2),
+                              "GB/s": round(byts / t / 1e9, 1), "min_us": round(min(res[k]) * 1e6, 2)}))
+        return
     res = {c: [] for c in cfgs}
     for rnd in range(5):
         for c in cfgs:
@@ -282,9 +308,9 @@ def sweep(args, device):
             res[c].append(ev / 50)
     byts = (args.peers + 1) * args.params * es
     # in place: the average overwrites peer 0's row (allowed by the ABI: out may alias peers[0])
-    for c in ([] if args.sweep_cfgs else [(2, 4, 0), (4, 4, 4096)]):
+    for c in ([] if args.sweep_cfgs else [(4, 1, 0, 64)]):
         cfg = _lib.LaunchCfg(*c)
-        key = (c[0], c[1], -1)
+        key = (c[0], c[1], -1, c[3])
         res[key] = []
         for rnd in range(5):
             fn = lambda: _lib.wsum_ptrs(code, ptrs, w, args.params, ptrs[0], sp, cfg)  # noqa: E731
@@ -292,7 +318,8 @@ def sweep(args, device):
             res[key].append(ev / 50)
     rows = sorted(((statistics.median(v), c) for c, v in res.items()))
     for t, c in rows:
-        print(json.dumps({"variant": c[0], "chunks": c[1], "grid": c[2], "us": round(t * 1e6, 2),
+        print(json.dumps({"variant": c[0], "chunks": c[1], "grid": c[2], "block": c[3] if len(c) > 3 else 0,
+                          "us": round(t * 1e6, 2),
                           "GB/s": round(byts / t / 1e9, 1), "min_us": round(min(res[c]) * 1e6, 2)}))
     del slab
     if not args.no_ceilings:
@@ -367,8 +394,8 @@ def main():
     out = torch.empty(p, dtype=dt, device=device)
     w = [float(x) for x in np.random.default_rng(0).dirichlet(np.ones(n))]
     cfg = None
-    if args.variant or args.chunks or args.grid:
-        cfg = _lib.LaunchCfg(args.variant, args.chunks, args.grid)
+    if args.variant or args.chunks or args.grid or args.block:
+        cfg = _lib.LaunchCfg(args.variant, args.chunks, args.grid, args.block)
     ptrs = [slab[k].data_ptr() for k in range(n)]
     code = wsum.dtype_code(dt)
 

@@ -21,7 +21,7 @@ LIB_PATH = os.environ.get("DLAGG_LIB", os.path.join(PKG_ROOT, "lib", "libdlagg.s
 
 # dtype codes (include/dlagg.h)
 DLA_F32, DLA_BF16, DLA_F16, DLA_F64 = 0, 1, 2, 3
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 HIPCC_FLAGS = [
     "--offload-arch=gfx950",
@@ -131,7 +131,8 @@ class _Lib:
 
 class LaunchCfg(ctypes.Structure):
     """dla_launch_cfg_t (include/dlagg.h)."""
-    _fields_ = [("variant", ctypes.c_int), ("chunks", ctypes.c_int), ("grid_blocks", ctypes.c_int)]
+    _fields_ = [("variant", ctypes.c_int), ("chunks", ctypes.c_int), ("grid_blocks", ctypes.c_int),
+                ("block", ctypes.c_int)]
 
 
 _lib: Optional[_Lib] = None

@@ -40,7 +40,7 @@
 
 namespace {
 
-constexpr int kBlock = 256;           // 4 waves of 64 lanes
+constexpr int kBlock = 256;           // multi-tensor / scalar kernels: 4 waves of 64 lanes
 constexpr int kGroup = 8;             // peers loaded together before folding
 constexpr int kMaxPeersPerPass = 128; // pointer table in the kernel-argument block
 
@@ -220,12 +220,12 @@ __device__ inline void store16(uint4* p, const uint4& v) {
 
 // ------------------------------------------------------------ tile bodies
 //
-// fold_tile: one tile = kBlock * CH chunks; lane l of the block owns chunks
-// base0 + c*kBlock + l.  Peers are folded in list order, loaded in groups of
+// fold_tile: one tile = BS * CH chunks; lane l of the block owns chunks
+// base0 + c*BS + l.  Peers are folded in list order, loaded in groups of
 // kGroup so a group's kGroup*CH loads all issue before the first wait.
 // ACC_IN: the running sum starts from `out` (second and later passes of a reduce
 // with more than KMAX peers) instead of p0 * 0.
-template <int DT, int CH, bool NT, int SP, bool ACC_IN>
+template <int DT, int BS, int CH, bool NT, int SP, bool ACC_IN>
 __device__ __attribute__((always_inline)) inline void fold_tile(
     const void* const* __restrict__ p, const typename Ops<DT>::w_t* __restrict__ w, int n_peers,
     int64_t base0, int64_t n_chunks, uint4* __restrict__ out) {
@@ -239,8 +239,8 @@ __device__ __attribute__((always_inline)) inline void fold_tile(
   int64_t idx[CH];
 #pragma unroll
   for (int c = 0; c < CH; ++c) {
-    live[c] = base + c * kBlock < n_chunks;
-    idx[c] = live[c] ? base + c * kBlock : n_chunks - 1;
+    live[c] = base + c * BS < n_chunks;
+    idx[c] = live[c] ? base + c * BS : n_chunks - 1;
   }
   acc_t acc[CH][E];
   int k0 = 0;
@@ -316,15 +316,15 @@ __device__ __attribute__((always_inline)) inline void fold_tail(
 // ------------------------------------------------ register-stream kernel
 // One flat buffer per peer; tiles dealt to workgroups (grid-stride when the grid
 // is smaller than the tile count); block 0 also folds the ragged tail.
-template <int DT, int KMAX, int CH, bool NT, int SP, bool ACC_IN>
-__global__ __launch_bounds__(kBlock) void wsum_stream_kernel(
+template <int DT, int KMAX, int BS, int CH, bool NT, int SP, bool ACC_IN>
+__global__ __launch_bounds__(BS) void wsum_stream_kernel(
     const PeerTable<typename Ops<DT>::w_t, KMAX> tab, int n_peers, int64_t n_chunks,
     int64_t n_elems, void* __restrict__ out_v) {
-  const int64_t tile_chunks = static_cast<int64_t>(kBlock) * CH;
+  const int64_t tile_chunks = static_cast<int64_t>(BS) * CH;
   const int64_t n_tiles = (n_chunks + tile_chunks - 1) / tile_chunks;
   for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x)
-    fold_tile<DT, CH, NT, SP, ACC_IN>(tab.p, tab.w, n_peers, tile * tile_chunks, n_chunks,
-                                      static_cast<uint4*>(out_v));
+    fold_tile<DT, BS, CH, NT, SP, ACC_IN>(tab.p, tab.w, n_peers, tile * tile_chunks, n_chunks,
+                                          static_cast<uint4*>(out_v));
   if (blockIdx.x == 0) fold_tail<DT, ACC_IN>(tab.p, tab.w, n_peers, n_chunks, n_elems, out_v);
 }
 
@@ -352,7 +352,7 @@ __global__ __launch_bounds__(kBlock) void wsum_multi_kernel(
   const int64_t n_elems = tab.n_elems[s];
   const int64_t n_chunks = n_elems / Ops<DT>::E;
   if (tile * kBlock < n_chunks)
-    fold_tile<DT, 1, true, SP, false>(tab.p[s], tab.w, n_peers, tile * kBlock, n_chunks,
+    fold_tile<DT, kBlock, 1, true, SP, false>(tab.p[s], tab.w, n_peers, tile * kBlock, n_chunks,
                                       static_cast<uint4*>(tab.out[s]));
   if (tile == 0) fold_tail<DT, false>(tab.p[s], tab.w, n_peers, n_chunks, n_elems, tab.out[s]);
 }
@@ -383,51 +383,77 @@ __global__ __launch_bounds__(kBlock) void wsum_scalar_kernel(
 // ------------------------------------------------------------------ launching
 
 struct Launch {
-  int variant;
-  int chunks;  // 0 = pick by size (chunks_for)
-  int grid_blocks;
+  int variant;      // 1 plain/plain, 2 nt/plain, 4 nt/sc1 (load/store cache policy)
+  int block;        // 64 or 256 threads; 0 = pick (shape_for)
+  int chunks;       // 1, 2, 4; 0 = pick (shape_for)
+  int grid_blocks;  // 0 = one workgroup per tile
 };
 
-// Chunks per lane: 4 (most bytes in flight per wave) while that still leaves >= 2048
-// tiles (8 per CU) to spread over the 256 CUs; fewer for small reduces, where
-// CH=4 would leave CUs idle (measured: 128 x 2 M bf16, CH=1 6.49 vs CH=4 5.65 TB/s).
-// Passes of more than 32 peers take CH=1: the per-peer loop already keeps a wave
-// busy, and CH=4's 189 VGPRs halve the waves per SIMD (128 x 21.3 M bf16, the
-// google_speech config: CH=1 6.53 vs CH=4 6.28 TB/s; 32 peers: equal).
-int chunks_for(int64_t n_chunks, int n_peers) {
+// Workgroup shape by dtype, peer count and size (interleaved A/B on MI355X, r01 sweeps):
+//  * default: 64-thread workgroups, 1 chunk per lane — the most, smallest workgroups.
+//    8 x 25 M fp32: 6.50 vs 6.39 TB/s for 256 x 4; 16 x 21.3 M fp32 6.44 vs 6.24;
+//    128 x 21.3 M bf16 (google_speech) 6.48 vs 6.27.
+//  * 16-bit dtypes with <= 16 peers: 256 x 4 (each chunk carries 8 elements of VALU work;
+//    more chunks per lane keep more bytes in flight): 8 x 50 M bf16 6.65 vs 6.38 TB/s —
+//    while that still leaves >= 2048 tiles (8 per CU).
+void shape_for(int64_t n_chunks, int n_peers, int elems_per_chunk, int* block, int* chunks) {
   constexpr int64_t kMinTiles = 2048;
-  if (n_peers > 32) return 1;
-  if (n_chunks >= kMinTiles * kBlock * 4) return 4;
-  if (n_chunks >= kMinTiles * kBlock * 2) return 2;
-  return 1;
+  if (elems_per_chunk == 8 && n_peers <= 16 && n_chunks >= kMinTiles * 256 * 4) {
+    *block = 256;
+    *chunks = 4;
+    return;
+  }
+  *block = 64;
+  *chunks = 1;
 }
 
 Launch resolve(const dla_launch_cfg_t* cfg) {
-  // default (measured on MI355X, profiles/r01_*): nt loads + sc1 stores, 4 chunks per lane,
-  // one workgroup per tile: 6.43-6.58 TB/s on 8 x 25 M fp32 vs 6.21-6.43 for plain stores.
-  Launch l{4, 0, 0};
+  // default: nt loads + sc1 stores (+3.5 % over plain stores on every box measured)
+  Launch l{4, 0, 0, 0};
   if (cfg) {
     if (cfg->variant) l.variant = cfg->variant;
-    if (cfg->chunks) l.chunks = cfg->chunks;
+    l.block = cfg->block;
+    l.chunks = cfg->chunks;
     l.grid_blocks = cfg->grid_blocks;
   }
   return l;
 }
 
-template <int DT, int KMAX, int CH, bool NT, int SP, bool ACC_IN>
+template <int DT, int KMAX, int BS, int CH, bool NT, int SP, bool ACC_IN>
 hipError_t launch_stream(const PeerTable<typename Ops<DT>::w_t, KMAX>& tab, int n, int64_t n_elems,
                          void* out, hipStream_t s, int grid_blocks) {
   constexpr int E = Ops<DT>::E;
   const int64_t n_chunks = n_elems / E;
-  const int64_t tile_chunks = static_cast<int64_t>(kBlock) * CH;
+  const int64_t tile_chunks = static_cast<int64_t>(BS) * CH;
   int64_t tiles = (n_chunks + tile_chunks - 1) / tile_chunks;
   if (tiles < 1) tiles = 1;  // block 0 still handles the ragged tail
   int64_t grid = grid_blocks > 0 ? grid_blocks : tiles;
   if (grid > tiles) grid = tiles;
   if (grid > 0x7fffffff) grid = 0x7fffffff;
-  hipLaunchKernelGGL((wsum_stream_kernel<DT, KMAX, CH, NT, SP, ACC_IN>), dim3(static_cast<unsigned>(grid)),
-                     dim3(kBlock), 0, s, tab, n, n_chunks, n_elems, out);
+  hipLaunchKernelGGL((wsum_stream_kernel<DT, KMAX, BS, CH, NT, SP, ACC_IN>), dim3(static_cast<unsigned>(grid)),
+                     dim3(BS), 0, s, tab, n, n_chunks, n_elems, out);
   return hipGetLastError();
+}
+
+template <int DT, int KMAX, int BS, int CH, bool ACC_IN>
+hipError_t launch_variant(const PeerTable<typename Ops<DT>::w_t, KMAX>& tab, int n, int64_t n_elems, void* out,
+                          hipStream_t s, const Launch& l) {
+  switch (l.variant) {
+    case 1: return launch_stream<DT, KMAX, BS, CH, false, 0, ACC_IN>(tab, n, n_elems, out, s, l.grid_blocks);
+    case 2: return launch_stream<DT, KMAX, BS, CH, true, 0, ACC_IN>(tab, n, n_elems, out, s, l.grid_blocks);
+    default: return launch_stream<DT, KMAX, BS, CH, true, 2, ACC_IN>(tab, n, n_elems, out, s, l.grid_blocks);
+  }
+}
+
+template <int DT, int KMAX, int BS, bool ACC_IN>
+hipError_t launch_chunks(const PeerTable<typename Ops<DT>::w_t, KMAX>& tab, int n, int64_t n_elems, void* out,
+                         hipStream_t s, const Launch& l, int chunks) {
+  switch (chunks) {
+    case 1: return launch_variant<DT, KMAX, BS, 1, ACC_IN>(tab, n, n_elems, out, s, l);
+    case 2: return launch_variant<DT, KMAX, BS, 2, ACC_IN>(tab, n, n_elems, out, s, l);
+    case 4: return launch_variant<DT, KMAX, BS, 4, ACC_IN>(tab, n, n_elems, out, s, l);
+    default: return hipErrorInvalidValue;
+  }
 }
 
 template <int DT, int KMAX, bool ACC_IN>
@@ -441,26 +467,15 @@ hipError_t launch_pass(const PeerTable<typename Ops<DT>::w_t, KMAX>& tab, int n,
                        dim3(kBlock), 0, s, tab, n, n_elems, out);
     return hipGetLastError();
   }
-  // variant 1: plain loads/stores; 2: nt loads; 3: nt loads + nt stores;
-  //         4: nt loads + sc1 stores; 5: nt loads + sc0 sc1 stores
-#define DLA_CH_CASE(CHV)                                                                              \
-  case CHV:                                                                                           \
-    switch (l.variant) {                                                                              \
-      case 1: return launch_stream<DT, KMAX, CHV, false, 0, ACC_IN>(tab, n, n_elems, out, s, l.grid_blocks); \
-      case 2: return launch_stream<DT, KMAX, CHV, true, 0, ACC_IN>(tab, n, n_elems, out, s, l.grid_blocks);  \
-      case 3: return launch_stream<DT, KMAX, CHV, true, 1, ACC_IN>(tab, n, n_elems, out, s, l.grid_blocks);  \
-      case 4: return launch_stream<DT, KMAX, CHV, true, 2, ACC_IN>(tab, n, n_elems, out, s, l.grid_blocks);  \
-      default: return launch_stream<DT, KMAX, CHV, true, 3, ACC_IN>(tab, n, n_elems, out, s, l.grid_blocks); \
-    }
-  const int chunks = l.chunks ? l.chunks : chunks_for(n_elems / Ops<DT>::E, n);
-  switch (chunks) {
-    DLA_CH_CASE(1)
-    DLA_CH_CASE(2)
-    DLA_CH_CASE(4)
-#undef DLA_CH_CASE
-    default:
-      return hipErrorInvalidValue;
+  int block = l.block, chunks = l.chunks;
+  if (!block || !chunks) {
+    int b, c;
+    shape_for(n_elems / Ops<DT>::E, n, Ops<DT>::E, &b, &c);
+    if (!block) block = b;
+    if (!chunks) chunks = c;
   }
+  if (block == 64) return launch_chunks<DT, KMAX, 64, ACC_IN>(tab, n, n_elems, out, s, l, chunks);
+  return launch_chunks<DT, KMAX, 256, ACC_IN>(tab, n, n_elems, out, s, l, chunks);
 }
 
 template <int DT, int KMAX>
@@ -570,10 +585,12 @@ int wsum_impl(int dtype, const void* const* peers, const double* weights, int n_
                                      std::to_string(kMaxPeersPerPass));
   }
   const Launch l = resolve(cfg);
-  if (l.variant < 1 || l.variant > 5)
-    return fail(DLA_E_CONFIG, "dla_wsum: unsupported variant " + std::to_string(l.variant));
+  if (l.variant != 1 && l.variant != 2 && l.variant != 4)
+    return fail(DLA_E_CONFIG, "dla_wsum: unsupported variant " + std::to_string(l.variant) + " (1, 2 or 4)");
   if (l.chunks != 0 && l.chunks != 1 && l.chunks != 2 && l.chunks != 4)
     return fail(DLA_E_CONFIG, "dla_wsum: chunks must be 0 (auto), 1, 2 or 4");
+  if (l.block != 0 && l.block != 64 && l.block != 256)
+    return fail(DLA_E_CONFIG, "dla_wsum: block must be 0 (auto), 64 or 256");
   if (l.grid_blocks < 0) return fail(DLA_E_CONFIG, "dla_wsum: grid_blocks < 0");
   hipStream_t s = static_cast<hipStream_t>(stream);
   hipError_t e;

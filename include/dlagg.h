@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define DLA_ABI_VERSION 1
+#define DLA_ABI_VERSION 2
 
 /* element dtypes of the peer buffers and of the output */
 #define DLA_F32 0
@@ -60,10 +60,10 @@ extern "C" {
 typedef struct dla_launch_cfg {
   int variant;      /* 0 = default (4); cache policy of the register stream:
                        1 = plain loads / plain stores   2 = nt loads / plain stores
-                       3 = nt loads / nt stores         4 = nt loads / sc1 stores
-                       5 = nt loads / sc0 sc1 stores                                      */
-  int chunks;       /* 16-byte chunks per lane per peer per tile: 1, 2, 4; 0 = by size   */
+                       4 = nt loads / sc1 stores (write-through, line not kept in L2)    */
+  int chunks;       /* 16-byte chunks per lane per peer per tile: 1, 2, 4; 0 = by shape  */
   int grid_blocks;  /* workgroups; 0 = one per work tile (no grid-stride loop)           */
+  int block;        /* threads per workgroup: 64 or 256; 0 = by shape                    */
 } dla_launch_cfg_t;
 
 /* ABI version (DLA_ABI_VERSION). */

@@ -44,7 +44,7 @@ def test_library_version_and_argument_errors(lib_path):
     from accdfl_amd import _lib
 
     L = _lib.lib()
-    assert L.so.dla_version() == 1
+    assert L.so.dla_version() == 2
     assert L.max_peers_per_pass == 128
     # n_peers = 0 -> DLA_E_INVALID with a message
     rc = L.so.dla_wsum(0, None, None, 0, 10, None, None)
@@ -60,6 +60,10 @@ def test_library_version_and_argument_errors(lib_path):
     ptrs = [4096 * (k + 1) for k in range(130)]
     with pytest.raises(_lib.DlaggError, match="alias"):
         _lib.wsum_ptrs(0, ptrs, [1.0] * 130, 64, ptrs[5], 0)
+    # launch knobs outside the built set are refused before any launch
+    for bad in (_lib.LaunchCfg(3, 0, 0, 0), _lib.LaunchCfg(4, 3, 0, 0), _lib.LaunchCfg(4, 1, 0, 128)):
+        with pytest.raises(_lib.DlaggError):
+            _lib.wsum_ptrs(0, [4096], [1.0], 64, 8192, 0, bad)
 
 
 def _tiny_models(n):

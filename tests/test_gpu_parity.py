@@ -119,8 +119,8 @@ def _bits(t, dtype):
     return gc.from_torch(t, dtype)
 
 
-LAUNCH_CFGS = [(1, 1, 0), (2, 1, 0), (3, 1, 0), (1, 2, 0), (2, 2, 0), (3, 2, 0), (1, 4, 0), (2, 4, 0), (3, 4, 0),
-               (4, 4, 0), (5, 2, 0), (5, 4, 0), (2, 1, 512), (1, 2, 300), (3, 4, 1000)]
+LAUNCH_CFGS = [(v, c, g, b) for v in (1, 2, 4) for c in (1, 2, 4) for b in (64, 256) for g in (0,)] + [
+    (4, 1, 512, 64), (2, 2, 300, 256), (4, 4, 1000, 256), (0, 0, 0, 0)]
 
 
 @pytest.mark.parametrize("dtype", ["f32", "bf16", "f16", "f64"])
@@ -133,11 +133,11 @@ def test_every_launch_variant_is_bit_exact(dtype):
     w = [float(x) for x in np.random.default_rng(1).dirichlet(np.ones(8))]
     want = c_wsum([_bits(p, dtype) for p in peers], w, dtype)
     dev = [p.cuda() for p in peers]
-    for variant, chunks, grid in LAUNCH_CFGS:
-        cfg = _lib.LaunchCfg(variant, chunks, grid)
+    for variant, chunks, grid, block in LAUNCH_CFGS:
+        cfg = _lib.LaunchCfg(variant, chunks, grid, block)
         out = wsum.wsum(dev, w, cfg=cfg)
         torch.cuda.synchronize()
-        assert same_bits(_bits(out, dtype), want, dtype), (dtype, variant, chunks, grid)
+        assert same_bits(_bits(out, dtype), want, dtype), (dtype, variant, chunks, grid, block)
 
 
 @pytest.mark.parametrize("n", [1, 2, 3, 7, 8, 9, 16, 31, 32, 33, 64, 127, 128, 129, 257])
