@@ -16,7 +16,8 @@ KERNEL = "wsum_stream_kernel"
 
 
 def find(pattern):
-    hits = sorted(glob.glob(os.path.join(out_dir, "**", pattern), recursive=True))
+    hits = sorted(h for h in glob.glob(os.path.join(out_dir, "**", pattern), recursive=True)
+                  if os.sep + "summary" + os.sep not in h)
     return hits[0] if hits else None
 
 
@@ -27,19 +28,34 @@ def rows(path):
 
 summary = {"round": rnd, "bench_args": args}
 stats = find("*kernel_stats.csv")
-kname = None
 if stats:
     shutil.copy(stats, os.path.join(HERE, "%s_kernel_stats.csv" % rnd))
-    # the dominant instantiation of the reduce kernel = the north-star launches
-    cands = [r for r in rows(stats) if KERNEL in r.get("Name", "")]
-    if cands:
-        r = max(cands, key=lambda r: float(r["TotalDurationNs"]))
-        kname = r["Name"]
+# Per-dispatch trace: the north-star launches are the (kernel, grid) group of the reduce
+# kernel with the largest total time (the same instantiation also serves the small
+# configs at other grid sizes, so the per-name stats file mixes them).
+kname, kgrid = None, None
+trace = find("*kernel_trace.csv")
+if trace:
+    groups = {}
+    for r in rows(trace):
+        if KERNEL not in r["Kernel_Name"]:
+            continue
+        key = (r["Kernel_Name"], r["Grid_Size_X"])
+        groups.setdefault(key, []).append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+    if groups:
+        (kname, kgrid), durs = max(groups.items(), key=lambda kv: sum(kv[1]))
+        durs.sort()
         summary["kernel"] = kname
-        summary["calls"] = int(r["Calls"])
-        summary["avg_ns"] = float(r["AverageNs"])
-        summary["min_ns"] = float(r["MinNs"])
-        summary["max_ns"] = float(r["MaxNs"])
+        summary["grid_threads"] = int(kgrid)
+        summary["calls"] = len(durs)
+        summary["avg_ns"] = sum(durs) / len(durs)
+        summary["median_ns"] = durs[len(durs) // 2]
+        summary["min_ns"] = durs[0]
+        summary["max_ns"] = durs[-1]
+        with open(os.path.join(HERE, "%s_ns_kernel_trace_stats.csv" % rnd), "w") as f:
+            f.write("Name,GridThreads,Calls,AverageNs,MedianNs,MinNs,MaxNs\n")
+            f.write('"%s",%s,%d,%.1f,%d,%d,%d\n' % (kname, kgrid, len(durs), summary["avg_ns"], summary["median_ns"],
+                                                   durs[0], durs[-1]))
 
 
 def pmc(sub, counter):
@@ -51,7 +67,7 @@ def pmc(sub, counter):
         return None
     vals = [float(r["Counter_Value"]) for r in rows(path)
             if (r.get("Kernel_Name", "") == kname if kname else KERNEL in r.get("Kernel_Name", ""))
-            and r.get("Counter_Name") == counter]
+            and (kgrid is None or r.get("Grid_Size") == kgrid) and r.get("Counter_Name") == counter]
     if not vals:
         return None
     vals.sort()
