@@ -12,12 +12,14 @@ summation order = arrival order.
 """
 from __future__ import annotations
 
+import copy
 from typing import Dict, List, Optional
 
 import torch
 import torch.nn as nn
 
 from accdfl_amd.core.gradient_aggregation import GradientAggregationMethod
+from accdfl_amd.core import wire
 from accdfl_amd.core.gradient_aggregation.fedavg import FedAvg, _center_copy
 
 
@@ -49,16 +51,34 @@ class ModelManager:
         return self.get_aggregation_method().aggregate(models, weights=weights)
 
 
+class WirePeer:
+    """A peer model received as ``serialize_model`` bytes and decoded by
+    ``wire.loads_state_dict``: its state dict, without the ``create_model`` +
+    ``load_state_dict`` the reference runs (accdfl/core/models/__init__.py:13-16)."""
+
+    def __init__(self, state_dict):
+        self.state_dict = state_dict
+
+    def materialize(self, template: nn.Module) -> nn.Module:
+        """The module the reference's ``unserialize_model`` would build."""
+        m = copy.deepcopy(template)
+        m.load_state_dict(self.state_dict)
+        return m
+
+
 class DeviceModelManager(ModelManager):
     """ModelManager whose received models are staged into HBM on arrival.
 
     ``capacity`` bounds the number of models one round holds (the DFL sample size, or
-    1 + in-degree in DL); the slab grows if it is exceeded.
+    1 + in-degree in DL); the slab grows if it is exceeded.  ``template`` is a module of
+    the session's architecture (default: ``model``); it is needed only for models that
+    arrive as wire bytes (``process_incoming_serialized``).
     """
 
     def __init__(self, model: Optional[nn.Module], settings, participant_index: int = 0, capacity: int = 8,
-                 device: Optional[torch.device] = None):
+                 device: Optional[torch.device] = None, template: Optional[nn.Module] = None):
         super().__init__(model, settings, participant_index)
+        self.template = template if template is not None else model
         from accdfl_amd.core.peer_slab import PeerSlab  # noqa: WPS433 (keeps import light for CPU-only users)
 
         self._slab_cls = PeerSlab
@@ -78,21 +98,66 @@ class DeviceModelManager(ModelManager):
         except TypeError:
             pass  # mixed-dtype model: the round falls back to FedAvg.aggregate (uniform_with is False)
 
+    def process_incoming_serialized(self, peer_pk: bytes, data: bytes):
+        """A model straight from the wire (``serialize_model`` bytes, e.g. EVA's
+        ``TransferResult.data``): decoded without executing the payload and staged into
+        HBM; no ``create_model`` / ``load_state_dict`` (§8 f1)."""
+        if peer_pk in self.incoming_trained_models:
+            return
+        if self.template is None:
+            raise ValueError("DeviceModelManager needs a template module to decode wire payloads")
+        sd = wire.loads_state_dict(data)
+        params = wire.parameter_tensors(sd, self.template)
+        self.incoming_trained_models[peer_pk] = WirePeer(sd)
+        if self.slab is None:
+            self.slab = self._slab_cls.for_model(self.template, capacity=self._capacity, device=self._device)
+        if self.slab.matches(params):
+            self.slab.stage(params)
+
     def reset_incoming_trained_models(self):
         super().reset_incoming_trained_models()
         if self.slab is not None:
             self.slab.reset()
 
+    def _modules(self) -> List[nn.Module]:
+        return [m.materialize(self.template) if isinstance(m, WirePeer) else m
+                for m in self.incoming_trained_models.values()]
+
+    def _uniform(self) -> bool:
+        entries = list(self.incoming_trained_models.values())
+        if self.slab is None or len(entries) != self.slab.n:
+            return False
+        for m in entries:
+            params = (wire.parameter_tensors(m.state_dict, self.template) if isinstance(m, WirePeer)
+                      else list(m.parameters()))
+            if not self.slab.matches(params):
+                return False
+        return True
+
     def aggregate_trained_models(self, weights: List[float] = None) -> Optional[nn.Module]:
-        models = [model for model in self.incoming_trained_models.values()]
-        if self.get_aggregation_method() is not FedAvg or self.slab is None or not self.slab.uniform_with(models):
-            return super().aggregate_trained_models(weights)
-        n = len(models)
+        if self.get_aggregation_method() is not FedAvg or not self._uniform():
+            return self.get_aggregation_method().aggregate(self._modules(), weights=weights)
+        entries = list(self.incoming_trained_models.values())
+        n = len(entries)
         if not weights:
             weights = [float(1. / n) for _ in range(n)]
         else:
             assert len(weights) == n
         with torch.no_grad():
-            center = _center_copy(models[0])  # deepcopy(models[0]) minus the parameter values
+            first = entries[0]
+            if isinstance(first, WirePeer):
+                # deepcopy(models[0]) of the module unserialize_model would have built:
+                # the template's structure with the first arrival's buffers.
+                center = _center_copy(self.template)
+                for name, buf in center.named_buffers():
+                    if name in first.state_dict:
+                        buf.copy_(first.state_dict[name])
+            else:
+                center = _center_copy(first)  # deepcopy(models[0]) minus the parameter values
             self.slab.reduce_into(list(center.parameters()), weights)
         return center
+
+    def aggregate_serialized(self, weights: List[float] = None) -> bytes:
+        """``serialize_model(aggregate_trained_models(weights))`` — the bytes a DFL
+        aggregator sends back to the participants (accdfl/dfl/community.py:556-567)."""
+        return wire.serialize_model(self.aggregate_trained_models(weights))

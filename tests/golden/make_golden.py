@@ -182,6 +182,27 @@ def main():
 
     for name, dt, models, weights in cases:
         save_case(name, dt, models, weights)
+    save_wire_case()
+
+
+def save_wire_case():
+    """Wire format (f1/f3): the reference's own serialize_model bytes of 4 spambase
+    models (configs[0]), the reference FedAvg result's bytes, and the weights."""
+    from accdfl.core.models import create_model, serialize_model
+
+    models = []
+    for k in range(4):
+        torch.manual_seed(9000 + k)
+        models.append(create_model("spambase"))
+    weights = dirichlet(4, 11)
+    out = FedAvg.aggregate(models, weights)
+    arrays = {"peer_%d" % k: np.frombuffer(serialize_model(m), dtype=np.uint8).copy() for k, m in enumerate(models)}
+    arrays["out"] = np.frombuffer(serialize_model(out), dtype=np.uint8).copy()
+    arrays["weights"] = np.array(weights, dtype=np.float64)
+    arrays["param_names"] = np.array(json.dumps([n for n, _ in models[0].named_parameters()]))
+    path = os.path.join(HERE, "wire_spambase_n4.npz")
+    np.savez_compressed(path, **arrays)
+    print("%-28s %7.1f KiB" % ("wire_spambase_n4", os.path.getsize(path) / 1024))
 
 
 if __name__ == "__main__":

@@ -27,7 +27,8 @@ class Case:
 
 
 def case_names() -> List[str]:
-    return sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN_DIR, "*.npz")))
+    return sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN_DIR, "*.npz"))
+                  if not os.path.basename(p).startswith("wire_"))
 
 
 def load(name: str) -> Case:

@@ -1,0 +1,101 @@
+"""Wire format (§8 f1/f3): decoding the reference's serialize_model bytes without
+executing the payload, and producing bytes in the same format."""
+import io
+import json
+import os
+import pickle
+
+import numpy as np
+import pytest
+import torch
+from torch import nn
+
+from oracle.fedavg_oracle import fedavg_bits, same_bits
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "wire_spambase_n4.npz")
+
+
+def _wire_case():
+    z = np.load(GOLDEN)
+    peers = [z["peer_%d" % k].tobytes() for k in range(4)]
+    return peers, z["out"].tobytes(), [float(x) for x in z["weights"]], json.loads(str(z["param_names"]))
+
+
+def test_decode_reference_payloads_and_pin_the_average():
+    from accdfl_amd.core import wire
+
+    peers, out, weights, names = _wire_case()
+    sds = [wire.loads_state_dict(b) for b in peers]
+    want = wire.loads_state_dict(out)
+    assert list(sds[0].keys()) == names == list(want.keys())
+    for name in names:
+        got = fedavg_bits([sd[name].numpy().reshape(-1) for sd in sds], weights, "f32")
+        assert same_bits(got, want[name].numpy().reshape(-1), "f32"), name
+
+
+class _Evil:
+    def __reduce__(self):
+        return (os.system, ("echo pwned > /tmp/accdfl_amd_pwned",))
+
+
+def test_refuses_foreign_globals():
+    from accdfl_amd.core import wire
+
+    payload = pickle.dumps({"w": _Evil()})
+    if os.path.exists("/tmp/accdfl_amd_pwned"):
+        os.remove("/tmp/accdfl_amd_pwned")
+    with pytest.raises(wire.UnsafePayloadError):
+        wire.loads_state_dict(payload)
+    assert not os.path.exists("/tmp/accdfl_amd_pwned")
+    with pytest.raises(wire.UnsafePayloadError):
+        wire.loads_state_dict(pickle.dumps([1, 2, 3]))  # not a state dict
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16, torch.float64])
+def test_round_trip_every_dtype_with_buffers(dtype):
+    from accdfl_amd.core import wire
+
+    m = nn.Sequential(nn.Linear(7, 5), nn.BatchNorm1d(5)).to(dtype)
+    b = wire.serialize_model(m)
+    sd = wire.loads_state_dict(b)
+    ref = m.state_dict()
+    assert list(sd.keys()) == list(ref.keys())
+    for k in ref:
+        assert sd[k].dtype == ref[k].dtype and torch.equal(sd[k], ref[k]), k
+    # the reference's own decoder (pickle.loads + load_state_dict) reads our bytes
+    m2 = nn.Sequential(nn.Linear(7, 5), nn.BatchNorm1d(5)).to(dtype)
+    m2.load_state_dict(pickle.loads(b))
+    assert all(torch.equal(p, q) for p, q in zip(m.parameters(), m2.parameters()))
+    assert [n for n, _ in m.named_parameters()] == [n for n, _ in m2.named_parameters()]
+    assert [t.data_ptr() for t in wire.parameter_tensors(sd, m)] == [sd[n].data_ptr() for n, _ in m.named_parameters()]
+
+
+@pytest.mark.gpu
+def test_device_model_manager_wire_round():
+    """A DFL-style aggregator round on wire bytes: decode -> HBM -> reduce -> bytes,
+    against the reference's own FedAvg result for the same payloads."""
+    from types import SimpleNamespace
+
+    from accdfl_amd.core import wire
+    from accdfl_amd.core.gradient_aggregation import GradientAggregationMethod
+    from accdfl_amd.core.model_manager import DeviceModelManager
+
+    class LinearModel(nn.Module):  # same parameter names as the reference's spambase model
+        def __init__(self):
+            super().__init__()
+            self.model = nn.Linear(57, 2)
+
+    peers, out, weights, names = _wire_case()
+    mm = DeviceModelManager(None, SimpleNamespace(gradient_aggregation=GradientAggregationMethod.FEDAVG),
+                            template=LinearModel(), capacity=2)
+    for k, b in enumerate(peers):
+        mm.process_incoming_serialized(b"peer%d" % k, b)
+    mm.process_incoming_serialized(b"peer1", peers[2])  # duplicate peer: ignored
+    assert mm.slab.n == 4
+    model = mm.aggregate_trained_models(weights)
+    want = wire.loads_state_dict(out)
+    for name, p in model.named_parameters():
+        assert same_bits(p.detach().numpy(), want[name].numpy(), "f32"), name
+    back = wire.loads_state_dict(mm.aggregate_serialized(weights))
+    for name in names:
+        assert same_bits(back[name].numpy(), want[name].numpy(), "f32"), name
