@@ -369,6 +369,16 @@ def measured_ceilings(device, nbytes=1 << 30):
         _, ev = time_kernel(lambda: so.dlp_mread8(arr, each, srcs[0].data_ptr(), sink.data_ptr(), ch, 1, sp()),
                             30, 3, 1)
         res["mread8_ch%d_write_inplace" % ch] = round(9 * each / (ev / 30) / 1e9, 1)
+    del srcs
+    # tile-interleaved peer layout ([tiles][8 (+1 out)][T]) — one contiguous region per workgroup
+    slab9 = torch.empty(9 * each // 4, dtype=torch.float32, device=device).normal_()
+    so.dlp_tiled8.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                              ctypes.c_void_p]
+    for ch in (1, 4, 16):
+        for slot in (0, 1):
+            _, ev = time_kernel(lambda: so.dlp_tiled8(slab9.data_ptr(), each, dst.data_ptr(), ch, slot, sp()),
+                                30, 3, 1)
+            res["tiled8_ch%d_outslot%d" % (ch, slot)] = round(9 * each / (ev / 30) / 1e9, 1)
     return res
 
 

@@ -30,6 +30,7 @@ device-resident path is stream-ordered like any torch op.
 from __future__ import annotations
 
 import copy
+import os
 import threading
 from typing import Dict, List, Tuple
 
@@ -55,7 +56,7 @@ class _HostStaging:
         self.dtype = dtype
         self.rows = 0
         self.pitch = 0
-        self.h_in = self.d_in = self.d_out = self.h_out = None
+        self.h_in = self.d_in = self.d_out = None
         self.copy_stream = torch.cuda.Stream(device)
 
     def ensure(self, rows: int, pitch: int):
@@ -66,7 +67,6 @@ class _HostStaging:
         self.h_in = torch.empty((rows, pitch), dtype=self.dtype, pin_memory=True)
         self.d_in = torch.empty((rows, pitch), dtype=self.dtype, device=self.device)
         self.d_out = torch.empty(pitch, dtype=self.dtype, device=self.device)
-        self.h_out = torch.empty(pitch, dtype=self.dtype, pin_memory=True)
         self.rows, self.pitch = rows, pitch
 
 
@@ -82,49 +82,124 @@ def _get_staging(device: torch.device, dtype: torch.dtype) -> _HostStaging:
     return st
 
 
+_staging_sharded: Dict[Tuple[torch.device, torch.dtype, int], _HostStaging] = {}
+
+
+def _get_staging_sharded(device: torch.device, dtype: torch.dtype, slot: int) -> _HostStaging:
+    """Staging for bucket ``slot`` of a sharded reduce (distinct even when two buckets share a
+    device, which the single-GPU tests use to exercise the sharded path)."""
+    key = (device, dtype, slot)
+    st = _staging_sharded.get(key)
+    if st is None:
+        st = _staging_sharded[key] = _HostStaging(device, dtype)
+    return st
+
+
 def release_staging() -> None:
     """Free the cached host/device staging slabs."""
     with _staging_lock:
         _staging.clear()
+        _staging_sharded.clear()
 
 
-def _reduce_host_staged(device, dtype, center: List[torch.Tensor], peers: List[List[torch.Tensor]], weights):
-    """One dtype group, every model contributing to every tensor: pack -> H2D -> reduce -> D2H."""
+# Devices the host-staged path may shard over (one process, several GPUs): the reference
+# hands CPU modules to the aggregator, so the path is PCIe-bound, and splitting the flat
+# parameter vector into buckets sends each GPU's share over its own PCIe link.  Buckets keep
+# every element's summation order: the result is bit-identical for any device count.
+_host_devices: List[torch.device] = []
+_MIN_SHARD_BYTES = 8 << 20  # per device; smaller models stay on one GPU
+
+
+def set_host_devices(devices) -> None:
+    """Use these HIP devices for CPU-resident models (default: the current device, or the
+    comma list in ACCDFL_AMD_DEVICES)."""
+    global _host_devices
+    _host_devices = [torch.device("cuda", d) if isinstance(d, int) else torch.device(d) for d in devices]
+
+
+def _devices_for(device: torch.device) -> List[torch.device]:
+    if _host_devices:
+        return list(_host_devices)
+    env = os.environ.get("ACCDFL_AMD_DEVICES", "")
+    if env:
+        return [torch.device("cuda", int(x)) for x in env.split(",") if x.strip()]
+    return [device]
+
+
+def _flat_slices(tensors: List[torch.Tensor], numels: List[int], start: int, end: int) -> List[torch.Tensor]:
+    """1-D views covering [start, end) of the virtual concatenation of ``tensors``."""
+    out, off = [], 0
+    for t, n in zip(tensors, numels):
+        s, e = max(start, off), min(end, off + n)
+        if s < e:
+            out.append(t.reshape(-1)[s - off:e - off])
+        off += n
+        if off >= end:
+            break
+    return out
+
+
+def _reduce_host_staged(devices: List[torch.device], dtype, center: List[torch.Tensor],
+                        peers: List[List[torch.Tensor]], weights):
+    """One dtype group, every model contributing to every tensor: pack -> H2D -> reduce -> D2H,
+    bucket-sharded over ``devices`` (each bucket over its own GPU's PCIe link)."""
+    from accdfl_amd.core.sharding import bucket_bounds
+
     numels = [c.numel() for c in center]
     total = sum(numels)
     if total == 0:
         return
     esize = torch.empty((), dtype=dtype).element_size()
-    pitch = _round_up(total, _ALIGN_BYTES // esize)
+    align = _ALIGN_BYTES // esize
+    g_max = max(1, min(len(devices), (total * esize) // _MIN_SHARD_BYTES))
+    devices = devices[:g_max]
+    bounds = bucket_bounds(total, len(devices), align)
     n = len(peers)
     with _staging_lock:
-        st = _get_staging(device, dtype)
-        st.ensure(n, pitch)
-        compute = torch.cuda.current_stream(device)
-        st.copy_stream.wait_stream(compute)  # previous users of d_in are done
+        stages = []
+        for dev, (s, e) in zip(devices, bounds):
+            st = _get_staging(dev, dtype) if len(devices) == 1 else _get_staging_sharded(dev, dtype, len(stages))
+            st.ensure(n, _round_up(max(e - s, 1), align))
+            st.copy_stream.wait_stream(torch.cuda.current_stream(dev))  # previous users of d_in are done
+            stages.append(st)
         for k in range(n):
             flat = [p.detach().reshape(-1) for p in peers[k]]
-            if all(t.device.type == "cpu" for t in flat):
-                row = st.h_in[k, :total]
-                torch.cat(flat, out=row)
-                with torch.cuda.stream(st.copy_stream):
-                    st.d_in[k, :total].copy_(row, non_blocking=True)
-            else:
-                with torch.cuda.stream(st.copy_stream):
-                    torch.cat([t.to(device, non_blocking=True) for t in flat], out=st.d_in[k, :total])
-        compute.wait_stream(st.copy_stream)
-        _wsum.wsum_rows(st.d_in, weights, total, out=st.d_out)
-        # D2H straight into the result's parameters when they are pinned and dense
-        # (see _center_copy); otherwise through the pinned staging buffer.
+            on_cpu = all(t.device.type == "cpu" for t in flat)
+            for st, dev, (s, e) in zip(stages, devices, bounds):
+                if s == e:
+                    continue
+                parts = _flat_slices(flat, numels, s, e)
+                if on_cpu:
+                    row = st.h_in[k, : e - s]
+                    if len(parts) == 1:
+                        row.copy_(parts[0])
+                    else:
+                        torch.cat(parts, out=row)
+                    with torch.cuda.stream(st.copy_stream):
+                        st.d_in[k, : e - s].copy_(row, non_blocking=True)
+                else:
+                    with torch.cuda.device(dev), torch.cuda.stream(st.copy_stream):
+                        torch.cat([t.to(dev, non_blocking=True) for t in parts], out=st.d_in[k, : e - s])
         direct = all(c.is_pinned() and c.is_contiguous() for c in center)
-        if direct:
-            for c, o in zip(center, torch.split(st.d_out[:total], numels)):
-                c.view(-1).copy_(o, non_blocking=True)
-            compute.synchronize()
-        else:
-            st.h_out[:total].copy_(st.d_out[:total], non_blocking=True)
-            compute.synchronize()
-            for c, o in zip(center, torch.split(st.h_out[:total], numels)):
+        h_out = None if direct else torch.empty(total, dtype=dtype, pin_memory=True)
+        for st, dev, (s, e) in zip(stages, devices, bounds):
+            if s == e:
+                continue
+            compute = torch.cuda.current_stream(dev)
+            compute.wait_stream(st.copy_stream)
+            with torch.cuda.device(dev):
+                _wsum.wsum_rows(st.d_in, weights, e - s, out=st.d_out)
+                # D2H straight into the result's parameters when they are pinned and dense
+                # (see _center_copy); otherwise through one pinned buffer.
+                dst = _flat_slices(center, numels, s, e) if direct else [h_out[s:e]]
+                off = 0
+                for d in dst:
+                    d.copy_(st.d_out[off:off + d.numel()], non_blocking=True)
+                    off += d.numel()
+        for dev in devices:
+            torch.cuda.current_stream(dev).synchronize()
+        if not direct:
+            for c, o in zip(center, torch.split(h_out, numels)):
                 c.copy_(o.view_as(c))
 
 
@@ -183,7 +258,7 @@ def reduce_parameters(center_params: List[torch.Tensor], peer_params: List[List[
         if resident:
             _reduce_device_resident(dtype, center, peers, weights)
         else:
-            _reduce_host_staged(device, dtype, center, peers, weights)
+            _reduce_host_staged(_devices_for(device), dtype, center, peers, weights)
     for i in partial:
         ks = [k for k in range(n) if len(peer_params[k]) > i]
         _reduce_param(device, center_params[i], [peer_params[k][i] for k in ks], [weights[k] for k in ks])

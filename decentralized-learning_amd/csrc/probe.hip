@@ -105,9 +105,54 @@ int launch_read(const void* src, int64_t bytes, void* sink, int nt, hipStream_t 
   return static_cast<int>(hipGetLastError());
 }
 
+// Tile-interleaved layout probe: peers stored as [tiles][NS][T chunks] (T = 64 * CH,
+// one wave per workgroup), so a workgroup reads one contiguous NS*T*16-byte region.
+// OUT_SLOT: the output goes to slot NS of a [tiles][NS+1][T] layout (same region) instead
+// of a separate flat buffer.
+template <int NS, int CH, bool OUT_SLOT>
+__global__ __launch_bounds__(64) void tiled_kernel(const u32x4* __restrict__ src, int64_t n_tiles,
+                                                    u32x4* __restrict__ dst) {
+  constexpr int T = 64 * CH;
+  const int64_t tile = blockIdx.x;
+  if (tile >= n_tiles) return;
+  constexpr int SLOTS = OUT_SLOT ? NS + 1 : NS;
+  const u32x4* base = src + tile * SLOTS * T;
+  u32x4 v[NS][CH];
+#pragma unroll
+  for (int k = 0; k < NS; ++k)
+#pragma unroll
+    for (int c = 0; c < CH; ++c) v[k][c] = __builtin_nontemporal_load(base + k * T + c * 64 + threadIdx.x);
+#pragma unroll
+  for (int c = 0; c < CH; ++c) {
+    u32x4 acc = v[0][c];
+#pragma unroll
+    for (int k = 1; k < NS; ++k) acc ^= v[k][c];
+    u32x4* o = OUT_SLOT ? const_cast<u32x4*>(base) + NS * T + c * 64 + threadIdx.x : dst + tile * T + c * 64 + threadIdx.x;
+    asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(o), "v"(acc) : "memory");
+  }
+}
+
 }  // namespace
 
 extern "C" {
+
+// bytes_each per peer (8 peers); layout [tiles][8 or 9][64*chunks*16 B]; out_slot 0/1.
+int dlp_tiled8(void* slab, int64_t bytes_each, void* dst, int chunks, int out_slot, void* stream) {
+  if (!slab || bytes_each < 16) return -1;
+  const int64_t T = 64 * chunks;
+  const int64_t n_tiles = bytes_each / 16 / T;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const u32x4* src = static_cast<const u32x4*>(slab);
+  u32x4* d = static_cast<u32x4*>(dst);
+#define DLP_T(CHV, OS) hipLaunchKernelGGL((tiled_kernel<8, CHV, OS>), dim3(n_tiles), dim3(64), 0, s, src, n_tiles, d)
+  if (chunks == 1) { if (out_slot) DLP_T(1, true); else DLP_T(1, false); }
+  else if (chunks == 4) { if (out_slot) DLP_T(4, true); else DLP_T(4, false); }
+  else if (chunks == 16) { if (out_slot) DLP_T(16, true); else DLP_T(16, false); }
+  else return -1;
+#undef DLP_T
+  return static_cast<int>(hipGetLastError());
+}
+
 
 // Read `bytes` (multiple of 16) from src; `chunks` in {1, 4, 8}; sink >= 4 KiB.
 int dlp_read(const void* src, int64_t bytes, void* sink, int chunks, int nt, void* stream) {

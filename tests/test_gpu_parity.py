@@ -308,3 +308,28 @@ def test_device_model_manager_falls_back_on_mixed_layouts():
     want = fedavg_param_lists([[p.detach().numpy() for p in m.parameters()] for m in (a, c, b)], w, "f32")
     for p, q in zip(out.parameters(), want):
         assert same_bits(p.detach().numpy(), q, "f32")
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+def test_host_path_sharded_over_devices(dtype):
+    """CPU models bucket-sharded over several devices (here three shards on cuda:0: the
+    same code path as three GPUs) — buckets cut through parameter tensors, result bit-exact."""
+    from torch import nn
+
+    from accdfl_amd.core.gradient_aggregation import fedavg as fa
+
+    shapes = [(1_000_003,), (3, 1_000_000), (2_500_001,), (17,), (500_000, 2)]
+    g = torch.Generator().manual_seed(31)
+    models = []
+    for _ in range(5):
+        m = nn.ParameterList([nn.Parameter((torch.randn(s, generator=g) * 0.05).to(TDT[dtype])) for s in shapes])
+        models.append(m)
+    w = [0.3, 0.1, 0.2, 0.25, 0.15]
+    fa.set_host_devices(["cuda:0", "cuda:0", "cuda:0"])
+    try:
+        out = fa.FedAvg.aggregate(models, w)
+    finally:
+        fa.set_host_devices([])
+    for i, p in enumerate(out.parameters()):
+        want = fedavg_bits([gc.as_float(_bits(m[i].detach().reshape(-1), dtype), dtype) for m in models], w, dtype)
+        assert same_bits(gc.as_float(_bits(p.detach().reshape(-1), dtype), dtype), want, dtype), i
