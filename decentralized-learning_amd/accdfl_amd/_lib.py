@@ -45,6 +45,7 @@ EXPORTED = (
     "dla_plan_set_weights",
     "dla_plan_launch",
     "dla_plan_destroy",
+    "dla_mean",
 )
 
 
@@ -116,6 +117,8 @@ class _Lib:
         so.dla_plan_set_weights.restype = ctypes.c_int
         so.dla_plan_launch.argtypes = [vp, vp]
         so.dla_plan_launch.restype = ctypes.c_int
+        so.dla_mean.argtypes = [ctypes.c_int, ctypes.POINTER(vp), ctypes.c_int, ctypes.c_int64, vp, vp]
+        so.dla_mean.restype = ctypes.c_int
         so.dla_plan_destroy.argtypes = [vp]
         so.dla_plan_destroy.restype = None
         v = so.dla_version()
@@ -179,6 +182,13 @@ def wsum_ptrs(dtype_code: int, peer_ptrs: Sequence[int], weights: Sequence[float
         rc = L.so.dla_wsum_ex(dtype_code, _ptr_array(peer_ptrs), _dbl_array(weights), n, n_elems, out_ptr,
                               stream_ptr, ctypes.byref(cfg))
     L.check(rc, "dla_wsum")
+
+
+def mean_ptrs(dtype_code: int, peer_ptrs: Sequence[int], n_elems: int, out_ptr: int, stream_ptr: int) -> None:
+    """dla_mean: sequential sum / N (teacher-logit aggregation)."""
+    L = lib()
+    rc = L.so.dla_mean(dtype_code, _ptr_array(peer_ptrs), len(peer_ptrs), n_elems, out_ptr, stream_ptr)
+    L.check(rc, "dla_mean")
 
 
 def wsum_slab_ptr(dtype_code: int, base_ptr: int, pitch_elems: int, weights: Sequence[float], n_peers: int,

@@ -357,6 +357,73 @@ __global__ __launch_bounds__(kBlock) void wsum_multi_kernel(
   if (tile == 0) fold_tail<DT, false>(tab.p[s], tab.w, n_peers, n_chunks, n_elems, tab.out[s]);
 }
 
+// ------------------------------------------------ teacher-logit mean (§8 f4)
+// scripts/distill.py:124-129: torch.mean(torch.stack(preds), dim=0) = sum / N.  Contract:
+// acc = +0; acc = acc + p_k in list order (op-math = storage type, F32/F64 only); the last
+// pass divides by N (correctly rounded).  torch's own CPU/GPU sum order is an
+// implementation detail (vectorised columns sequential, tail columns and N > 16 cascaded),
+// so parity with torch.mean is within a stated tolerance; with the sequential oracle it is
+// bit-exact.  One 16-byte chunk per lane, 64-thread workgroups.
+template <int DT, int KMAX, bool ACC_IN, bool ALIGNED>
+__global__ __launch_bounds__(64) void mean_kernel(const PeerTable<typename Ops<DT>::w_t, KMAX> tab, int n_peers,
+                                                  int64_t n_chunks, int64_t n_elems, void* __restrict__ out_v,
+                                                  typename Ops<DT>::acc_t divisor, int divide) {
+  using O = Ops<DT>;
+  using acc_t = typename O::acc_t;
+  using elem_t = typename O::elem_t;
+  constexpr int E = O::E;
+  static_assert(DT == DLA_F32 || DT == DLA_F64, "mean: f32/f64 only");
+  if constexpr (ALIGNED) {
+    const int64_t i = static_cast<int64_t>(blockIdx.x) * 64 + threadIdx.x;
+    if (i < n_chunks) {
+      uint4* out = static_cast<uint4*>(out_v);
+      acc_t acc[E];
+      if constexpr (ACC_IN) {
+        O::unpack(out[i], acc);
+      } else {
+#pragma unroll
+        for (int e = 0; e < E; ++e) acc[e] = acc_t(0);
+      }
+      int k = 0;
+      for (; k + kGroup <= n_peers; k += kGroup) {
+        uint4 v[kGroup];
+#pragma unroll
+        for (int g = 0; g < kGroup; ++g) v[g] = load16<true>(static_cast<const uint4*>(tab.p[k + g]) + i);
+#pragma unroll
+        for (int g = 0; g < kGroup; ++g) {
+          acc_t x[E];
+          O::unpack(v[g], x);
+#pragma unroll
+          for (int e = 0; e < E; ++e) acc[e] = acc[e] + x[e];
+        }
+      }
+      for (; k < n_peers; ++k) {
+        acc_t x[E];
+        O::unpack(load16<true>(static_cast<const uint4*>(tab.p[k]) + i), x);
+#pragma unroll
+        for (int e = 0; e < E; ++e) acc[e] = acc[e] + x[e];
+      }
+      if (divide) {
+#pragma unroll
+        for (int e = 0; e < E; ++e) acc[e] = acc[e] / divisor;
+      }
+      store16<2>(out + i, O::pack(acc));
+    }
+  }
+  // ragged tail (aligned) or everything (unaligned): one element per lane
+  const int64_t j0 = ALIGNED ? n_chunks * E : 0;
+  const int64_t stride = ALIGNED ? 64 : static_cast<int64_t>(gridDim.x) * 64;
+  const int64_t start = ALIGNED ? (blockIdx.x == 0 ? j0 + threadIdx.x : n_elems)
+                                : static_cast<int64_t>(blockIdx.x) * 64 + threadIdx.x;
+  for (int64_t j = start; j < n_elems; j += stride) {
+    elem_t* o = static_cast<elem_t*>(out_v);
+    acc_t acc = ACC_IN ? O::to_acc(o[j]) : acc_t(0);
+    for (int k = 0; k < n_peers; ++k) acc = acc + O::to_acc(static_cast<const elem_t*>(tab.p[k])[j]);
+    if (divide) acc = acc / divisor;
+    o[j] = O::from_acc(acc);
+  }
+}
+
 // ---------------------------------------------------- scalar kernel (unaligned)
 // Any alignment; one element per lane, grid-stride.  Used only when a buffer is
 // not 16-byte aligned (e.g. an odd-offset view).
@@ -555,6 +622,49 @@ hipError_t run_multi_dt(const std::vector<int>& packed, const void* const* peer_
   return run_multi<DT, 32, 8>(packed, peer_ptrs, outs, numels, weights, n, s);
 }
 
+template <int DT, int KMAX>
+hipError_t mean_pass(const void* const* peers, int n, int n_total, int64_t n_elems, void* out, hipStream_t s,
+                     bool acc_in, bool divide) {
+  using W = typename Ops<DT>::w_t;
+  PeerTable<W, KMAX> tab;
+  std::memset(&tab, 0, sizeof(tab));
+  bool aligned = (reinterpret_cast<uintptr_t>(out) & 15u) == 0;
+  for (int k = 0; k < n; ++k) {
+    tab.p[k] = peers[k];
+    tab.w[k] = W(1);
+    aligned = aligned && (reinterpret_cast<uintptr_t>(peers[k]) & 15u) == 0;
+  }
+  constexpr int E = Ops<DT>::E;
+  const int64_t n_chunks = aligned ? n_elems / E : 0;
+  int64_t grid = aligned ? (n_chunks + 63) / 64 : (n_elems + 63) / 64;
+  if (!aligned && grid > 8192) grid = 8192;
+  if (grid < 1) grid = 1;
+  const typename Ops<DT>::acc_t d = static_cast<typename Ops<DT>::acc_t>(n_total);
+#define DLA_MEAN_L(AI, AL)                                                                                  \
+  hipLaunchKernelGGL((mean_kernel<DT, KMAX, AI, AL>), dim3(static_cast<unsigned>(grid)), dim3(64), 0, s, tab, n, \
+                     n_chunks, n_elems, out, d, divide ? 1 : 0)
+  if (acc_in) {
+    if (aligned) DLA_MEAN_L(true, true); else DLA_MEAN_L(true, false);
+  } else {
+    if (aligned) DLA_MEAN_L(false, true); else DLA_MEAN_L(false, false);
+  }
+#undef DLA_MEAN_L
+  return hipGetLastError();
+}
+
+template <int DT>
+hipError_t run_mean(const void* const* peers, int n, int64_t n_elems, void* out, hipStream_t s) {
+  for (int k0 = 0; k0 < n; k0 += kMaxPeersPerPass) {
+    const int m = n - k0 < kMaxPeersPerPass ? n - k0 : kMaxPeersPerPass;
+    const bool last = k0 + m >= n;
+    hipError_t e = m <= 8 ? mean_pass<DT, 8>(peers + k0, m, n, n_elems, out, s, k0 > 0, last)
+                 : m <= 32 ? mean_pass<DT, 32>(peers + k0, m, n, n_elems, out, s, k0 > 0, last)
+                           : mean_pass<DT, kMaxPeersPerPass>(peers + k0, m, n, n_elems, out, s, k0 > 0, last);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
 int elem_size(int dtype) {
   switch (dtype) {
     case DLA_F32: return 4;
@@ -728,5 +838,24 @@ int dla_plan_launch(const dla_plan_t* plan, void* stream) {
 }
 
 void dla_plan_destroy(dla_plan_t* plan) { delete plan; }
+
+int dla_mean(int dtype, const void* const* peers, int n_peers, int64_t n_elems, void* out, void* stream) {
+  g_last_error.clear();
+  if (dtype != DLA_F32 && dtype != DLA_F64) return fail(DLA_E_INVALID, "dla_mean: F32 or F64 only");
+  if (n_peers < 1 || !peers) return fail(DLA_E_INVALID, "dla_mean: n_peers must be >= 1");
+  if (n_elems < 0) return fail(DLA_E_INVALID, "dla_mean: n_elems < 0");
+  if (n_elems == 0) return DLA_OK;
+  if (!out) return fail(DLA_E_INVALID, "dla_mean: null out");
+  for (int k = 0; k < n_peers; ++k) {
+    if (!peers[k]) return fail(DLA_E_INVALID, "dla_mean: null peer pointer");
+    if (n_peers > kMaxPeersPerPass && k > 0 && peers[k] == out)
+      return fail(DLA_E_ALIAS, "dla_mean: out aliases a peer other than peers[0] in a multi-pass mean");
+  }
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const hipError_t e = dtype == DLA_F32 ? run_mean<DLA_F32>(peers, n_peers, n_elems, out, s)
+                                        : run_mean<DLA_F64>(peers, n_peers, n_elems, out, s);
+  if (e != hipSuccess) return fail(static_cast<int>(e), std::string("dla_mean: ") + hipGetErrorString(e));
+  return DLA_OK;
+}
 
 }  // extern "C"

@@ -100,6 +100,15 @@ int dla_wsum_slab(int dtype, const void* base, int64_t pitch_elems, const double
 int dla_wsum_multi(int dtype, int n_tensors, const void* const* peer_ptrs, void* const* outs,
                    const int64_t* numels, const double* weights, int n_peers, void* stream);
 
+/* Replaces scripts/distill.py:124-129 (teacher-logit aggregation,
+ * torch.mean(torch.stack(preds), dim=0)) for a whole batch of logits at once:
+ *     out = (((+0 + p_0) + p_1) + ... + p_{N-1}) / N      element-wise, F32 or F64.
+ * The sum is sequential in list order, op-math = storage type, and the division is
+ * correctly rounded; torch's own reduction order is implementation-defined, so parity
+ * with torch.mean is within |err| <= N * 2^-23 * sum_k |p_k| / N (f32).  out may alias
+ * peers[0] (also when n_peers > DLA_MAX_PEERS_PER_PASS). */
+int dla_mean(int dtype, const void* const* peers, int n_peers, int64_t n_elems, void* out, void* stream);
+
 /* Largest peer count one kernel pass takes (kernel-argument pointer table). */
 int dla_max_peers_per_pass(void);
 

@@ -333,3 +333,56 @@ def test_host_path_sharded_over_devices(dtype):
     for i, p in enumerate(out.parameters()):
         want = fedavg_bits([gc.as_float(_bits(m[i].detach().reshape(-1), dtype), dtype) for m in models], w, dtype)
         assert same_bits(gc.as_float(_bits(p.detach().reshape(-1), dtype), dtype), want, dtype), i
+
+
+def _seq_mean(arrs, dtype):
+    acc = np.zeros_like(arrs[0])
+    for a in arrs:
+        acc = (acc + a).astype(arrs[0].dtype)
+    return (acc / arrs[0].dtype.type(len(arrs))).astype(arrs[0].dtype)
+
+
+@pytest.mark.parametrize("n", [1, 2, 5, 8, 17, 130])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
+def test_teacher_logit_mean(n, dtype):
+    """§8 f4 (scripts/distill.py:124-129): bit-exact vs the sequential-sum/N oracle,
+    within N*2^-23*sum|p|/N of torch.mean(torch.stack(...), 0)."""
+    from accdfl_amd.core.distill import aggregate_predictions, mean_logits
+
+    g = torch.Generator().manual_seed(n)
+    S, C = 257, 100
+    teachers = [(torch.randn(S, C, generator=g) * 3).to(dtype) for _ in range(n)]
+    out = mean_logits([t.cuda() for t in teachers])
+    want = _seq_mean([t.numpy() for t in teachers], dtype)
+    assert np.array_equal(out.cpu().numpy(), want)
+    ref = torch.mean(torch.stack(teachers), dim=0).numpy()
+    eps = 2.0 ** -23 if dtype == torch.float32 else 2.0 ** -52
+    bound = eps * np.sum(np.abs(np.stack([t.numpy() for t in teachers])), axis=0)  # N * eps * sum|p| / N
+    assert np.all(np.abs(out.cpu().numpy().astype(np.float64) - ref) <= bound + 1e-30)
+    # the reference's list-of-samples form
+    per_sample = aggregate_predictions([[t[s] for s in range(S)] for t in teachers])
+    assert len(per_sample) == S and np.array_equal(torch.stack(per_sample).cpu().numpy(), want)
+
+
+def test_teacher_logit_mean_specials_unaligned_alias():
+    from accdfl_amd import _lib
+
+    n, numel = 4, 1003
+    base = torch.randn(n, numel + 1)
+    base[0, 1] = -0.0
+    base[:, 2] = -0.0            # all -0: torch's +0 start gives +0
+    base[1, 3] = float("inf")    # inf stays inf (no p0*0 init in mean)
+    base[2, 4] = float("nan")
+    dev = base.cuda()
+    views = [dev[k, 1:] for k in range(n)]  # 4-byte offset: scalar path
+    out = torch.empty(numel, device="cuda")
+    _lib.mean_ptrs(_lib.DLA_F32, [v.data_ptr() for v in views], numel, out.data_ptr(),
+                   torch.cuda.current_stream().cuda_stream)
+    want = _seq_mean([base[k, 1:].numpy() for k in range(n)], torch.float32)
+    assert same_bits(out.cpu().numpy(), want, "f32")
+    assert out[1].item() == 0.0 and not np.signbit(out[1].item())
+    rows = [dev[k, :numel].contiguous() for k in range(n)]
+    aliased = rows[0]
+    _lib.mean_ptrs(_lib.DLA_F32, [r.data_ptr() for r in rows], numel, aliased.data_ptr(),
+                   torch.cuda.current_stream().cuda_stream)
+    assert same_bits(aliased.cpu().numpy(), _seq_mean([base[k, :numel].numpy() for k in range(n)], None), "f32")
