@@ -10,7 +10,6 @@ import random
 from math import floor
 from types import SimpleNamespace
 
-import numpy as np
 import pytest
 import torch
 from torch import nn
@@ -18,8 +17,6 @@ from torch import nn
 from oracle.fedavg_oracle import fedavg_param_lists, same_bits
 
 pytestmark = pytest.mark.gpu
-
-SETTINGS = None
 
 
 def _settings():
