@@ -236,6 +236,25 @@ def host_breakdown(n, p, device):
     t("d2h_pinned_ms", lambda: h_out.copy_(out, non_blocking=True))
     c = copy.deepcopy(models[0])
     t("unpack_ms", lambda: c.w.data.copy_(h_out))
+    # f1 wire ingress of one peer (serialize_model bytes of a 25 M fp32 model)
+    import pickle
+
+    from accdfl_amd.core import wire
+    from accdfl_amd.core.peer_slab import PeerSlab
+
+    data = wire.serialize_model(models[0])
+    res["wire_payload_MB"] = round(len(data) / 1e6, 1)
+    t("wire_safe_decode_ms", lambda: wire.loads_state_dict(data))
+    t("reference_decode_pickle_loads_ms", lambda: pickle.loads(data))  # our own bytes
+    sd = wire.loads_state_dict(data)
+    t("reference_load_state_dict_ms", lambda: c.load_state_dict(sd))
+    slab = PeerSlab([(p,)], torch.float32, capacity=1, device=device)
+
+    def stage():
+        slab.reset()
+        slab.stage([sd["w"]])
+        slab.copy_stream.synchronize()
+    t("wire_stage_h2d_ms", stage)
     res["threads"] = torch.get_num_threads()
     return res
 

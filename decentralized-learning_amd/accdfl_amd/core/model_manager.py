@@ -106,7 +106,7 @@ class DeviceModelManager(ModelManager):
             return
         if self.template is None:
             raise ValueError("DeviceModelManager needs a template module to decode wire payloads")
-        sd = wire.loads_state_dict(data)
+        sd = wire.loads_state_dict(data, copy=False)  # read-only views of `data`; staged, never written
         params = wire.parameter_tensors(sd, self.template)
         self.incoming_trained_models[peer_pk] = WirePeer(sd)
         if self.slab is None:

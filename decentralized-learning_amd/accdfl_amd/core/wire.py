@@ -31,8 +31,72 @@ class UnsafePayloadError(pickle.UnpicklingError):
     """The payload references something a state_dict pickle never contains."""
 
 
+_LEGACY_MAGIC = 0x1950A86A20F9469CFC6C
+_LEGACY_PROTOCOL = 1001
+_STORAGE_DTYPES = {
+    "FloatStorage": torch.float32, "DoubleStorage": torch.float64, "HalfStorage": torch.float16,
+    "BFloat16Storage": torch.bfloat16, "LongStorage": torch.int64, "IntStorage": torch.int32,
+    "ShortStorage": torch.int16, "CharStorage": torch.int8, "ByteStorage": torch.uint8,
+    "BoolStorage": torch.bool,
+}
+
+
+class _BlobUnpickler(pickle.Unpickler):
+    """The pickles inside one legacy ``torch.save`` storage blob: ints, a sys-info dict,
+    the storage's persistent id (naming a ``torch.<X>Storage`` class) and the key list."""
+
+    def find_class(self, module: str, name: str):
+        if module == "torch" and name in _STORAGE_DTYPES:
+            return ("storage_class", name)
+        raise UnsafePayloadError("accdfl_amd: refusing global %s.%s in a storage blob" % (module, name))
+
+    def persistent_load(self, pid):
+        if (not isinstance(pid, tuple) or len(pid) != 6 or pid[0] != "storage" or not isinstance(pid[1], tuple)
+                or pid[5] is not None):
+            raise UnsafePayloadError("accdfl_amd: unexpected persistent id in a storage blob")
+        return ("storage", _STORAGE_DTYPES[pid[1][1]], str(pid[2]), int(pid[4]))
+
+
+def _parse_storage_blob(blob: bytes) -> torch.TypedStorage:
+    """Zero-copy decode of ``TypedStorage.__reduce__``'s blob (legacy torch.save of one
+    storage; torch/serialization.py _legacy_save): the element data is viewed in place."""
+    f = io.BytesIO(blob)
+    u = _BlobUnpickler(f)
+    if u.load() != _LEGACY_MAGIC or u.load() != _LEGACY_PROTOCOL:
+        raise UnsafePayloadError("not a legacy storage blob")
+    info = u.load()
+    if not isinstance(info, dict) or not info.get("little_endian", False):
+        raise UnsafePayloadError("unsupported storage blob byte order")
+    u = _BlobUnpickler(f)
+    obj = u.load()
+    keys = _BlobUnpickler(f).load()
+    if not (isinstance(obj, tuple) and obj[0] == "storage" and keys == [obj[2]]):
+        raise UnsafePayloadError("storage blob does not hold exactly one storage")
+    _, dtype, _, numel = obj
+    pos = f.tell()
+    esize = torch.empty((), dtype=dtype).element_size()
+    n_saved = int.from_bytes(blob[pos:pos + 8], "little")
+    start, nbytes = pos + 8, numel * esize
+    if n_saved != numel or start + nbytes != len(blob):
+        raise UnsafePayloadError("storage blob size mismatch")
+    if numel == 0:
+        data = torch.empty(0, dtype=dtype)
+    else:
+        import warnings
+
+        with warnings.catch_warnings():  # read-only bytes: the tensor is never written in place
+            warnings.simplefilter("ignore", UserWarning)
+            data = torch.frombuffer(memoryview(blob)[start:start + nbytes], dtype=dtype)
+    return torch.TypedStorage(wrap_storage=data.untyped_storage(), dtype=dtype, _internal=True)
+
+
 def _load_storage_blob(blob: bytes):
-    return torch.load(io.BytesIO(blob), weights_only=True)
+    try:
+        return _parse_storage_blob(blob)
+    except UnsafePayloadError:
+        raise
+    except Exception:  # any other layout: torch's own safe loader
+        return torch.load(io.BytesIO(blob), weights_only=True)
 
 
 _ALLOWED = {
@@ -50,11 +114,20 @@ class _StateDictUnpickler(pickle.Unpickler):
             raise UnsafePayloadError("accdfl_amd: refusing global %s.%s in a model payload" % (module, name))
 
 
-def loads_state_dict(data: bytes) -> "collections.OrderedDict[str, torch.Tensor]":
-    """Decode ``serialize_model`` bytes into the state dict (CPU tensors)."""
+def loads_state_dict(data: bytes, copy: bool = True) -> "collections.OrderedDict[str, torch.Tensor]":
+    """Decode ``serialize_model`` bytes into the state dict (CPU tensors).
+
+    The tensors' element data is parsed in place from the payload (no ``torch.load``
+    pass).  ``copy=True`` gives each tensor its own writable memory; ``copy=False``
+    returns read-only views of the payload (what the ingress path stages to HBM)."""
     obj = _StateDictUnpickler(io.BytesIO(data)).load()
     if not isinstance(obj, dict) or not all(isinstance(k, str) and torch.is_tensor(v) for k, v in obj.items()):
         raise UnsafePayloadError("accdfl_amd: payload is not a state_dict")
+    if copy:
+        meta = getattr(obj, "_metadata", None)
+        obj = collections.OrderedDict((k, v.clone()) for k, v in obj.items())
+        if meta is not None:
+            obj._metadata = meta
     return obj
 
 

@@ -99,3 +99,41 @@ def test_device_model_manager_wire_round():
     back = wire.loads_state_dict(mm.aggregate_serialized(weights))
     for name in names:
         assert same_bits(back[name].numpy(), want[name].numpy(), "f32"), name
+
+
+def test_storage_blob_fast_path_and_fallback():
+    """The nested storage blobs are parsed in place (no torch.load pass); a blob in any
+    other layout (e.g. the zipfile format) goes to torch.load(weights_only=True); a blob
+    naming a foreign global is refused."""
+    from accdfl_amd.core import wire
+
+    for dt in (torch.float32, torch.bfloat16, torch.float16, torch.float64, torch.int64, torch.bool):
+        t = (torch.arange(37) % 3).to(dt)
+        storage = t.untyped_storage()
+        typed = torch.TypedStorage(wrap_storage=storage, dtype=dt, _internal=True)
+        blob = typed.__reduce__()[1][0]  # what pickle.dumps(tensor) embeds
+        parsed = wire._parse_storage_blob(blob)
+        assert parsed.dtype == dt and parsed.size() == 37
+        assert torch.equal(torch.tensor([], dtype=dt).set_(parsed._untyped_storage, 0, (37,), (1,)), t)
+        zipped = io.BytesIO()
+        torch.save(typed, zipped)  # zipfile layout: not the legacy blob
+        back = wire._load_storage_blob(zipped.getvalue())
+        assert back.dtype == dt
+    evil = pickle.dumps(_Evil())
+    with pytest.raises(wire.UnsafePayloadError):
+        wire._parse_storage_blob(pickle.dumps(0x1950A86A20F9469CFC6C) + pickle.dumps(1001) + pickle.dumps(
+            {"little_endian": True}) + evil)
+
+
+def test_copy_and_view_modes():
+    """copy=False: tensors view the decoded blob in place (the ingress path only reads
+    them); copy=True (default): private writable tensors."""
+    from accdfl_amd.core import wire
+
+    m = nn.Linear(300, 200)
+    data = wire.serialize_model(m)
+    views = wire.loads_state_dict(data, copy=False)
+    own = wire.loads_state_dict(data)
+    assert torch.equal(views["weight"], m.weight.detach()) and torch.equal(own["weight"], m.weight.detach())
+    own["weight"].add_(1.0)
+    assert torch.equal(wire.loads_state_dict(data)["weight"], m.weight.detach())
