@@ -101,6 +101,7 @@ def test_device_model_manager_wire_round():
         assert same_bits(back[name].numpy(), want[name].numpy(), "f32"), name
 
 
+@pytest.mark.filterwarnings("ignore:TypedStorage is deprecated")
 def test_storage_blob_fast_path_and_fallback():
     """The nested storage blobs are parsed in place (no torch.load pass); a blob in any
     other layout (e.g. the zipfile format) goes to torch.load(weights_only=True); a blob
