@@ -244,7 +244,7 @@ def host_breakdown(n, p, device):
 
     data = wire.serialize_model(models[0])
     res["wire_payload_MB"] = round(len(data) / 1e6, 1)
-    t("wire_safe_decode_ms", lambda: wire.loads_state_dict(data))
+    t("wire_safe_decode_ms", lambda: wire.loads_state_dict(data, copy=False))
     t("reference_decode_pickle_loads_ms", lambda: pickle.loads(data))  # our own bytes
     sd = wire.loads_state_dict(data)
     t("reference_load_state_dict_ms", lambda: c.load_state_dict(sd))

@@ -138,3 +138,38 @@ def test_copy_and_view_modes():
     assert torch.equal(views["weight"], m.weight.detach()) and torch.equal(own["weight"], m.weight.detach())
     own["weight"].add_(1.0)
     assert torch.equal(wire.loads_state_dict(data)["weight"], m.weight.detach())
+
+
+def test_vm_matches_unpickler_and_reads_in_place():
+    """The state_dict pickle VM: same result as the restricted C unpickler, parameter
+    bytes viewed in place in the payload (no copy)."""
+    from accdfl_amd.core import wire
+
+    m = nn.Sequential(nn.Conv2d(3, 4, 3), nn.BatchNorm2d(4), nn.Linear(5, 6, bias=False))
+    data = wire.serialize_model(m)
+    a = wire._vm_loads(data)
+    b = wire._StateDictUnpickler(io.BytesIO(data)).load()
+    assert list(a.keys()) == list(b.keys()) and a._metadata == b._metadata
+    for k in a:
+        assert a[k].dtype == b[k].dtype and a[k].shape == b[k].shape and torch.equal(a[k], b[k])
+    base = np.frombuffer(data, dtype=np.uint8).ctypes.data
+    assert base <= a["0.weight"].data_ptr() < base + len(data)
+
+
+def test_vm_rejects_truncated_and_garbage():
+    from accdfl_amd.core import wire
+
+    data = wire.serialize_model(nn.Linear(30, 20))
+    for cut in (1, 10, len(data) // 2, len(data) - 1):
+        with pytest.raises(Exception):
+            wire.loads_state_dict(data[:cut])
+    rng = np.random.default_rng(0)
+    for _ in range(200):  # random payloads: an exception, never a hang or a crash
+        junk = bytes(rng.integers(0, 256, size=int(rng.integers(1, 300)), dtype=np.uint8))
+        try:
+            wire.loads_state_dict(b"\x80\x04" + junk)
+        except Exception:
+            pass
+    # a REDUCE on anything but an allowed global is refused
+    with pytest.raises(wire.UnsafePayloadError):
+        wire.loads_state_dict(pickle.dumps({"w": _Evil()}, protocol=4))
