@@ -259,6 +259,43 @@ def host_breakdown(n, p, device):
     return res
 
 
+def wire_ingress(p, device, reps=5):
+    """§8 f1: one peer's serialize_model bytes (25 M fp32) -> HBM PeerSlab row, against the
+    reference's decode (pickle.loads, which also runs a torch.load per storage)."""
+    import pickle
+
+    from torch import nn
+
+    from accdfl_amd.core import wire
+    from accdfl_amd.core.peer_slab import PeerSlab
+
+    m = nn.Module()
+    m.w = nn.Parameter(torch.randn(p, generator=torch.Generator().manual_seed(7)) * 0.05)
+    data = wire.serialize_model(m)
+    slab = PeerSlab([(p,)], torch.float32, capacity=1, device=device)
+
+    def ours():
+        slab.reset()
+        slab.stage(wire.parameter_tensors(wire.loads_state_dict(data, copy=False), m))
+        slab.copy_stream.synchronize()
+
+    def ref_decode():
+        pickle.loads(data)  # bytes this process made: the reference's unserialize step
+
+    out = {}
+    for name, fn in (("ours_decode_and_stage_ms", ours), ("reference_pickle_loads_ms", ref_decode)):
+        fn()
+        ts = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            fn()
+            ts.append(time.perf_counter() - t0)
+        out[name] = round(statistics.median(ts) * 1e3, 2)
+    out["payload_MB"] = round(len(data) / 1e6, 1)
+    out["ours_GBps"] = round(len(data) / (out["ours_decode_and_stage_ms"] / 1e3) / 1e9, 1)
+    return out
+
+
 def small_configs(device, steps=200):
     """Device-resident reduces at the BASELINE configs' own model sizes, launched through a
     prepared dla_plan (what a PeerSlab round pays)."""
@@ -494,6 +531,7 @@ def main():
         torch.cuda.empty_cache()
         if not args.no_host_inclusive and args.dtype == "f32":
             result["host_inclusive"] = host_inclusive(n, p)
+            result["wire_ingress"] = wire_ingress(p, device)
         if not args.no_cpu_baseline and args.dtype == "f32":
             result["cpu_baseline"] = cpu_baseline(n, p, args.cpu_seconds)
     if rank == 0:

@@ -104,26 +104,47 @@ class PeerSlab:
             raise ValueError("PeerSlab.stage_flat: need %d elements of %s" % (self.total, self.dtype))
         return self._stage_flat_list([flat.detach().reshape(-1)])
 
+    # Tensors at least this large go H2D straight from where they live (e.g. the wire
+    # payload): ROCm's pageable H2D runs at the pinned rate on MI355X hosts (14.2 vs 13.9 ms
+    # per 800 MB), so the bounce copy would only add a host memcpy.  Runs of smaller
+    # tensors are packed into the pinned bounce buffer and sent as one copy.
+    DIRECT_BYTES = 1 << 20
+
     def _stage_flat_list(self, flat: List[torch.Tensor]) -> int:
         row = self.n
         if row >= self.capacity:
             self._grow(row + 1)
-        dst = self.buf[row, : self.total]
         cur = torch.cuda.current_stream(self.device)
         self.copy_stream.wait_stream(cur)
         if all(t.device.type == "cpu" for t in flat):
+            esize = self.buf.element_size()
             slot = row & 1
-            bounce = self._bounce_buffer(slot)[: self.total]
-            if len(flat) == 1:
-                bounce.copy_(flat[0])
-            else:
-                torch.cat(flat, out=bounce)
+            bounce = None
+            run_start = None  # element offset where the current run of small tensors begins
+            off = 0
             with torch.cuda.stream(self.copy_stream):
-                dst.copy_(bounce, non_blocking=True)
-                ev = torch.cuda.Event()
-                ev.record(self.copy_stream)
-            self._bounce_ev[slot] = ev
+                for t in flat + [None]:
+                    small = t is not None and t.numel() * esize < self.DIRECT_BYTES
+                    if not small and run_start is not None:  # flush the run of small tensors
+                        self.buf[row, run_start:off].copy_(bounce[run_start:off], non_blocking=True)
+                        run_start = None
+                    if t is None:
+                        break
+                    if small:
+                        if bounce is None:
+                            bounce = self._bounce_buffer(slot)
+                        if run_start is None:
+                            run_start = off
+                        bounce[off:off + t.numel()].copy_(t)
+                    else:
+                        self.buf[row, off:off + t.numel()].copy_(t)  # pageable H2D, no host copy
+                    off += t.numel()
+                if bounce is not None:
+                    ev = torch.cuda.Event()
+                    ev.record(self.copy_stream)
+                    self._bounce_ev[slot] = ev
         else:
+            dst = self.buf[row, : self.total]
             with torch.cuda.stream(self.copy_stream):
                 src = [t.to(self.device, non_blocking=True) for t in flat]
                 if len(src) == 1:

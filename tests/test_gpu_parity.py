@@ -386,3 +386,21 @@ def test_teacher_logit_mean_specials_unaligned_alias():
     _lib.mean_ptrs(_lib.DLA_F32, [r.data_ptr() for r in rows], numel, aliased.data_ptr(),
                    torch.cuda.current_stream().cuda_stream)
     assert same_bits(aliased.cpu().numpy(), _seq_mean([base[k, :numel].numpy() for k in range(n)], None), "f32")
+
+
+def test_peer_slab_mixed_direct_and_bounced_tensors():
+    """Large tensors go H2D directly, runs of small ones through the pinned bounce buffer;
+    the row layout and the reduce are unchanged (bit-exact)."""
+    from accdfl_amd.core.peer_slab import PeerSlab
+
+    shapes = [(5,), (300_001,), (7,), (3, 3), (400_000,), (2,), (1,), (262_144,), (11,)]
+    slab = PeerSlab(shapes, torch.float32, capacity=3)
+    models = [[(torch.randn(s) * 0.05) for s in shapes] for _ in range(6)]
+    for pl in models:
+        slab.stage(pl)
+    w = [0.1, 0.2, 0.3, 0.15, 0.05, 0.2]
+    flat = slab.reduce(w)
+    want = fedavg_bits([torch.cat([p.reshape(-1) for p in pl]).numpy() for pl in models], w, "f32")
+    assert same_bits(_bits(flat, "f32"), want, "f32")
+    for k, pl in enumerate(models):  # each row holds exactly its model
+        assert torch.equal(slab.buf[k, : slab.total].cpu(), torch.cat([p.reshape(-1) for p in pl]))
