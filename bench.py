@@ -259,6 +259,36 @@ def host_breakdown(n, p, device):
     return res
 
 
+def host_inclusive_small(reps=50):
+    """The reference's most frequent call: FedAvg.aggregate on small CPU models (GNLeNet,
+    configs[1]; GL merges N=2 every round, DFL N=8), end to end, next to the torch-CPU op
+    sequence on the same modules (per-call overhead, not bandwidth, decides here)."""
+    from torch import nn
+
+    sys.path.insert(0, ROOT)
+    from oracle.fedavg_oracle import fedavg_modules_torch  # timed CPU baseline
+    from accdfl_amd.core.gradient_aggregation.fedavg import FedAvg
+
+    shapes = [(32, 3, 5, 5), (32,), (32,), (32,), (32, 32, 5, 5), (32,), (32,), (32,), (64, 32, 5, 5), (64,),
+              (64,), (64,), (10, 576), (10,)]
+    out = {}
+    for n in (2, 8):
+        g = torch.Generator().manual_seed(n)
+        models = [nn.ParameterList([nn.Parameter(torch.randn(s, generator=g) * 0.05) for s in shapes])
+                  for _ in range(n)]
+        w = [float(1.0 / n)] * n
+        for name, fn in (("ours_ms", lambda: FedAvg.aggregate(models, w)),
+                         ("cpu_port_ms", lambda: fedavg_modules_torch(models, w))):
+            fn()
+            ts = []
+            for _ in range(reps):
+                t0 = time.perf_counter()
+                fn()
+                ts.append(time.perf_counter() - t0)
+            out.setdefault("gnlenet_n%d" % n, {})[name] = round(statistics.median(ts) * 1e3, 3)
+    return out
+
+
 def wire_ingress(p, device, reps=5):
     """§8 f1: one peer's serialize_model bytes (25 M fp32) -> HBM PeerSlab row, against the
     reference's decode (pickle.loads, which also runs a torch.load per storage)."""
@@ -532,6 +562,7 @@ def main():
         if not args.no_host_inclusive and args.dtype == "f32":
             result["host_inclusive"] = host_inclusive(n, p)
             result["wire_ingress"] = wire_ingress(p, device)
+            result["host_inclusive_small"] = host_inclusive_small()
         if not args.no_cpu_baseline and args.dtype == "f32":
             result["cpu_baseline"] = cpu_baseline(n, p, args.cpu_seconds)
     if rank == 0:

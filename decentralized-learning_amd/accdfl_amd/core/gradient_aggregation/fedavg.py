@@ -37,6 +37,7 @@ from typing import Dict, List, Tuple
 import torch
 from torch import nn
 
+from accdfl_amd import _lib
 from accdfl_amd.core import wsum as _wsum
 from accdfl_amd.core.gradient_aggregation import GradientAggregation
 
@@ -56,8 +57,10 @@ class _HostStaging:
         self.dtype = dtype
         self.rows = 0
         self.pitch = 0
-        self.h_in = self.d_in = self.d_out = None
+        self.h_in = self.d_in = self.d_out = self.h_out = None
         self.copy_stream = torch.cuda.Stream(device)
+        self.plan = None       # prepared launch over (d_in rows, d_out), see _plan_for
+        self.plan_key = None
 
     def ensure(self, rows: int, pitch: int):
         if rows <= self.rows and pitch <= self.pitch:
@@ -67,7 +70,20 @@ class _HostStaging:
         self.h_in = torch.empty((rows, pitch), dtype=self.dtype, pin_memory=True)
         self.d_in = torch.empty((rows, pitch), dtype=self.dtype, device=self.device)
         self.d_out = torch.empty(pitch, dtype=self.dtype, device=self.device)
+        self.h_out = torch.empty(pitch, dtype=self.dtype, pin_memory=True)
         self.rows, self.pitch = rows, pitch
+        self.plan = self.plan_key = None
+
+    def plan_for(self, n: int, total: int, weights) -> "_lib.Plan":
+        """The prepared dla_plan for rows 0..n-1 of d_in -> d_out (cached across calls)."""
+        key = (n, total, self.d_in.data_ptr(), self.d_out.data_ptr())
+        if self.plan_key != key:
+            ptrs = [self.d_in.data_ptr() + k * self.pitch * self.d_in.element_size() for k in range(n)]
+            self.plan = _lib.Plan(_wsum.dtype_code(self.dtype), ptrs, weights, total, self.d_out.data_ptr())
+            self.plan_key = key
+        else:
+            self.plan.set_weights(weights)
+        return self.plan
 
 
 _staging: Dict[Tuple[torch.device, torch.dtype], _HostStaging] = {}
@@ -139,6 +155,82 @@ def _flat_slices(tensors: List[torch.Tensor], numels: List[int], start: int, end
     return out
 
 
+# Below this many input bytes a round is latency-bound: the small path below replaces the
+# per-row pipeline with one H2D, a prepared launch, one D2H and one host unpack
+# (GNLeNet, configs[1]: every call site's common case, e.g. the GL merge of N=2 models).
+_SMALL_ROUND_BYTES = 64 << 20
+
+
+def _start_host_small(device, dtype, peers: List[List[torch.Tensor]], weights, total: int, pitch: int):
+    """Enqueue pack -> one H2D -> prepared launch -> one D2H; returns (staging, stream).
+    The caller holds _staging_lock until _finish_host_small."""
+    n = len(peers)
+    # exact-fit staging per (device, dtype, pitch): the single DMA below moves n * pitch
+    # elements, so it must not inherit the pitch of an earlier large round
+    key = (device, dtype, ("small", pitch))
+    st = _staging.get(key)
+    if st is None:
+        st = _staging[key] = _HostStaging(device, dtype)
+    st.ensure(n, pitch)
+    compute = torch.cuda.current_stream(device)
+    for k in range(n):
+        torch.cat([p.detach().view(-1) for p in peers[k]], out=st.h_in[k, :total])
+    st.d_in[:n].copy_(st.h_in[:n], non_blocking=True)  # one DMA for every row
+    st.plan_for(n, total, weights).launch(int(compute.cuda_stream))
+    st.h_out[:total].copy_(st.d_out[:total], non_blocking=True)
+    return st, compute
+
+
+def _finish_host_small(st, compute, center: List[torch.Tensor], numels: List[int], total: int):
+    compute.synchronize()
+    torch._foreach_copy_([c.view(-1) for c in center], list(torch.split(st.h_out[:total], numels)))
+
+
+def _reduce_host_small(device, dtype, center: List[torch.Tensor], peers: List[List[torch.Tensor]], weights,
+                       numels: List[int], total: int, pitch: int):
+    with _staging_lock:
+        st, compute = _start_host_small(device, dtype, peers, weights, total, pitch)
+        _finish_host_small(st, compute, center, numels, total)
+
+
+def _small_round(models: List[nn.Module], weights) -> "nn.Module | None":
+    """The whole aggregate for a small round of same-layout, one-dtype, contiguous CPU
+    models: the GPU work is enqueued first and the result module is built on the host
+    while it runs.  None when the round does not qualify (the general path handles it)."""
+    peers = [list(m.parameters()) for m in models]
+    p0 = peers[0]
+    if not p0 or not torch.cuda.is_available():
+        return None
+    dtype = p0[0].dtype
+    if dtype not in _wsum.SUPPORTED_DTYPES:
+        return None
+    layout = [(p.shape, p.dtype) for p in p0]
+    for pl in peers:
+        if [(p.shape, p.dtype) for p in pl] != layout:
+            return None
+        for p in pl:
+            if p.device.type != "cpu" or not p.is_contiguous():
+                return None
+    if len({d for _, d in layout}) != 1:
+        return None
+    numels = [p.numel() for p in p0]
+    total = sum(numels)
+    esize = p0[0].element_size()
+    if total == 0 or len(peers) * total * esize >= _SMALL_ROUND_BYTES:
+        return None
+    device = _wsum.require_device(None)
+    with _staging_lock:
+        st, compute = _start_host_small(device, dtype, peers, weights, total,
+                                        _round_up(total, _ALIGN_BYTES // esize))
+        center = _center_copy(models[0], pin=False)  # overlaps the H2D / reduce / D2H
+        params = list(center.parameters())
+        if len(params) != len(numels) or not all(c.is_contiguous() for c in params):
+            compute.synchronize()
+            return None
+        _finish_host_small(st, compute, params, numels, total)
+    return center
+
+
 def _reduce_host_staged(devices: List[torch.device], dtype, center: List[torch.Tensor],
                         peers: List[List[torch.Tensor]], weights):
     """One dtype group, every model contributing to every tensor: pack -> H2D -> reduce -> D2H,
@@ -151,6 +243,10 @@ def _reduce_host_staged(devices: List[torch.device], dtype, center: List[torch.T
         return
     esize = torch.empty((), dtype=dtype).element_size()
     align = _ALIGN_BYTES // esize
+    if (len(peers) * total * esize < _SMALL_ROUND_BYTES and all(c.is_contiguous() for c in center)
+            and all(p.device.type == "cpu" and p.is_contiguous() for pl in peers for p in pl)):
+        _reduce_host_small(devices[0], dtype, center, peers, weights, numels, total, _round_up(total, align))
+        return
     g_max = max(1, min(len(devices), (total * esize) // _MIN_SHARD_BYTES))
     devices = devices[:g_max]
     bounds = bucket_bounds(total, len(devices), align)
@@ -264,7 +360,7 @@ def reduce_parameters(center_params: List[torch.Tensor], peer_params: List[List[
         _reduce_param(device, center_params[i], [peer_params[k][i] for k in ks], [weights[k] for k in ks])
 
 
-def _center_copy(model0: nn.Module) -> nn.Module:
+def _center_copy(model0: nn.Module, pin: bool = True) -> nn.Module:
     """``copy.deepcopy(models[0])`` (fedavg.py:20) whose parameters are fresh,
     uninitialised tensors of the same shape, strides, dtype, device and
     ``requires_grad``: the reduce overwrites every one of them, so copying models[0]'s
@@ -273,7 +369,7 @@ def _center_copy(model0: nn.Module) -> nn.Module:
     D2H copy lands in them directly.  Buffers and every other attribute are deep-copied
     exactly as in the reference."""
     memo = {}
-    pin = torch.cuda.is_available()
+    pin = pin and torch.cuda.is_available()
     for p in model0.parameters():
         if id(p) in memo or type(p) is not nn.Parameter:
             continue  # Parameter subclasses keep the stock deepcopy
@@ -295,7 +391,13 @@ class FedAvg(GradientAggregation):
             assert len(weights) == len(models)
 
         with torch.no_grad():
-            center_model = _center_copy(models[0])
+            if len(models) > 0:
+                small = _small_round(models, list(weights))
+                if small is not None:
+                    return small
+            params0 = list(models[0].parameters())
+            nbytes = sum(p.numel() * p.element_size() for p in params0) * len(models)
+            center_model = _center_copy(models[0], pin=nbytes >= _SMALL_ROUND_BYTES)
             reduce_parameters(list(center_model.parameters()), [list(m.parameters()) for m in models],
                               list(weights))
             return center_model
