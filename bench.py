@@ -74,6 +74,7 @@ def parse():
     ap.add_argument("--sweep-cfgs", default="", help="variant,chunks,grid;... (default: built-in list)")
     ap.add_argument("--no-ceilings", action="store_true", help="skip the probe ceilings in --sweep")
     ap.add_argument("--libs", default="", help="comma list of libdlagg builds to A/B in --sweep (same process)")
+    ap.add_argument("--pads", default="", help="comma list of extra row-pitch bytes to A/B in --sweep")
     return ap.parse_args()
 
 
@@ -361,6 +362,24 @@ def sweep(args, device):
         cfgs = [tuple(int(x) for x in item.split(",")) for item in args.sweep_cfgs.split(";") if item]
     else:
         cfgs = [(v, c, 0, b) for v in (1, 2, 4) for c in (1, 2, 4) for b in (64, 256)]
+    if args.pads:
+        byts = (args.peers + 1) * args.params * es
+        pads = [int(x) for x in args.pads.split(",")]
+        del slab
+        res = {}
+        for rnd in range(5):
+            for pad in pads:
+                pitch = (args.params * es + pad + 15) // 16 * 16 // es
+                sl = make_slab(args.peers, pitch, dt, device, 1000)
+                pp = [sl[k].data_ptr() for k in range(args.peers)]
+                fn = lambda: _lib.wsum_ptrs(code, pp, w, args.params, out.data_ptr(), sp)  # noqa: E731
+                _, ev = time_kernel(fn, 50, 5, 1)
+                res.setdefault(pad, []).append(ev / 50)
+                del sl
+                torch.cuda.empty_cache()  # fresh physical pages for the next allocation
+        for t, pad in sorted((statistics.median(v), k) for k, v in res.items()):
+            print(json.dumps({"pad_bytes": pad, "us": round(t * 1e6, 2), "GB/s": round(byts / t / 1e9, 1)}))
+        return
     if args.libs:
         import ctypes
 
@@ -455,6 +474,11 @@ def measured_ceilings(device, nbytes=1 << 30):
         _, ev = time_kernel(lambda: so.dlp_mread8(arr, each, srcs[0].data_ptr(), sink.data_ptr(), ch, 1, sp()),
                             30, 3, 1)
         res["mread8_ch%d_write_inplace" % ch] = round(9 * each / (ev / 30) / 1e9, 1)
+    so.dlp_policy8.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
+    for rnd in range(3):
+        for pol, name in enumerate(("nt", "sc1", "sc0sc1", "sc0sc1nt", "sc1nt")):
+            _, ev = time_kernel(lambda: so.dlp_policy8(arr, each, dst.data_ptr(), pol, sp()), 30, 3, 1)
+            res["policy8_%s_r%d" % (name, rnd)] = round(9 * each / (ev / 30) / 1e9, 1)
     del srcs
     # tile-interleaved peer layout ([tiles][8 (+1 out)][T]) — one contiguous region per workgroup
     slab9 = torch.empty(9 * each // 4, dtype=torch.float32, device=device).normal_()

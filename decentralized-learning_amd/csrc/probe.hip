@@ -132,9 +132,67 @@ __global__ __launch_bounds__(64) void tiled_kernel(const u32x4* __restrict__ src
   }
 }
 
+// Load cache-policy probe on the FedAvg pattern (8 streams + 1 sc1 write, 64-thread WGs,
+// 1 chunk/lane).  POL: 0 "nt" (compiler builtin), 1 "sc1", 2 "sc0 sc1", 3 "sc0 sc1 nt", 4 "sc1 nt".
+// The asm loads are waited by an asm that takes every loaded register as "+v", so no use
+// can be scheduled before the wait.
+#define DLP_LD(POLSTR, dst, ptr) asm volatile("global_load_dwordx4 %0, %1, off " POLSTR : "=v"(dst) : "v"(ptr) : "memory")
+template <int POL>
+__global__ __launch_bounds__(64) void policy_kernel(const u32x4* s0, const u32x4* s1, const u32x4* s2,
+                                                     const u32x4* s3, const u32x4* s4, const u32x4* s5,
+                                                     const u32x4* s6, const u32x4* s7, int64_t n_chunks,
+                                                     u32x4* __restrict__ dst) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * 64 + threadIdx.x;
+  if (i >= n_chunks) return;
+  const u32x4* src[8] = {s0, s1, s2, s3, s4, s5, s6, s7};
+  u32x4 v[8];
+  if constexpr (POL == 0) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = __builtin_nontemporal_load(src[k] + i);
+  } else {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const u32x4* a = src[k] + i;
+      if constexpr (POL == 1) DLP_LD("sc1", v[k], a);
+      if constexpr (POL == 2) DLP_LD("sc0 sc1", v[k], a);
+      if constexpr (POL == 3) DLP_LD("sc0 sc1 nt", v[k], a);
+      if constexpr (POL == 4) DLP_LD("sc1 nt", v[k], a);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]),
+                 "+v"(v[6]), "+v"(v[7])::"memory");
+  }
+  u32x4 acc = v[0];
+#pragma unroll
+  for (int k = 1; k < 8; ++k) acc ^= v[k];
+  asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(dst + i), "v"(acc) : "memory");
+}
+#undef DLP_LD
+
 }  // namespace
 
 extern "C" {
+
+int dlp_policy8(const void* const* srcs, int64_t bytes_each, void* dst, int pol, void* stream) {
+  if (!srcs || bytes_each < 16) return -1;
+  const int64_t n = bytes_each / 16;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const u32x4* p[8];
+  for (int k = 0; k < 8; ++k) p[k] = static_cast<const u32x4*>(srcs[k]);
+  const dim3 g((n + 63) / 64);
+#define DLP_P(POL) hipLaunchKernelGGL((policy_kernel<POL>), g, dim3(64), 0, s, p[0], p[1], p[2], p[3], p[4], p[5], \
+                                      p[6], p[7], n, static_cast<u32x4*>(dst))
+  switch (pol) {
+    case 0: DLP_P(0); break;
+    case 1: DLP_P(1); break;
+    case 2: DLP_P(2); break;
+    case 3: DLP_P(3); break;
+    case 4: DLP_P(4); break;
+    default: return -1;
+  }
+#undef DLP_P
+  return static_cast<int>(hipGetLastError());
+}
+
 
 // bytes_each per peer (8 peers); layout [tiles][8 or 9][64*chunks*16 B]; out_slot 0/1.
 int dlp_tiled8(void* slab, int64_t bytes_each, void* dst, int chunks, int out_slot, void* stream) {
