@@ -213,6 +213,14 @@ class PeerSlab:
                 p.view(-1).copy_(v, non_blocking=True)  # D2H straight into the result
             torch.cuda.current_stream(self.device).synchronize()
             return
+        if all(p.is_contiguous() for p in params):  # small rounds: one D2H, one host unpack
+            if self._h_out is None or self._h_out.numel() < self.total:
+                self._h_out = torch.empty(self.pitch, dtype=self.dtype, pin_memory=True)
+            h = self._h_out[: self.total]
+            h.copy_(flat, non_blocking=True)
+            torch.cuda.current_stream(self.device).synchronize()
+            torch._foreach_copy_([p.view(-1) for p in params], list(torch.split(h, self.numels)))
+            return
         if self._h_out is None or self._h_out.numel() < self.total:
             self._h_out = torch.empty(self.pitch, dtype=self.dtype, pin_memory=True)
         h = self._h_out[: self.total]
