@@ -66,7 +66,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-inclusive", action="store_true")
     ap.add_argument("--no-small", action="store_true")
-    ap.add_argument("--allgather", action="store_true", help="also time the RCCL all-gather of the buckets")
+    ap.add_argument("--coll-params", type=int, default=0, help="params per rank bucket for the RCCL legs")
+    ap.add_argument("--no-collectives", action="store_true",
+                    help="skip the RCCL legs (all-gather, peer-sharded all-to-all / reduce-scatter) at N > 1")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) for real runs; gloo only to rehearse "
                                                              "several ranks on one GPU")
     ap.add_argument("--sweep", action="store_true", help="interleaved A/B of launch variants, then exit")
@@ -257,6 +259,45 @@ def host_breakdown(n, p, device):
         slab.copy_stream.synchronize()
     t("wire_stage_h2d_ms", stage)
     res["threads"] = torch.get_num_threads()
+    return res
+
+
+def collectives(n, p, dt, es, world, device, slab, w, iters=10):
+    """RCCL over xGMI, reported beside (never inside) `value`, N > 1 only:
+    * allgather: every rank's averaged bucket -> the whole model on every rank;
+    * peer_sharded_exact: peers arrive whole on different ranks (n / world each) ->
+      all-to-all transpose -> the same bit-exact bucket reduce -> all-gather;
+    * peer_sharded_reduce_scatter: local partial fold -> reduce-scatter -> all-gather
+      (stated-tolerance mode)."""
+    from accdfl_amd.core import wsum
+    from accdfl_amd.core.sharding import BucketShardedFedAvg
+
+    res = {}
+    on_gpu = dist.get_backend() == "nccl"
+    cdev = device if on_gpu else torch.device("cpu")  # gloo rehearsal: CPU tensors, GPU reduce
+
+    def reducer(peers, weights, out):
+        if on_gpu:
+            return wsum.wsum(list(peers), weights, out=out)
+        out.copy_(wsum.wsum([t.to(device) for t in peers], weights).cpu())
+        return out
+
+    sh = BucketShardedFedAvg(p * world, dt, device=cdev, reducer=reducer)
+    bucket = torch.zeros(sh.bucket_len, dtype=dt, device=cdev)
+    full = torch.empty(p * world, dtype=dt, device=cdev)
+    wall, _ = time_kernel(lambda: sh.all_gather(bucket, full), iters, 2, world)
+    res["allgather"] = {"ms": round(wall / iters * 1e3, 3), "bytes_out_per_rank": p * world * es,
+                        "GBps_per_rank_in": round((world - 1) * sh.bucket_len * es / (wall / iters) / 1e9, 1)}
+    if n % world == 0:
+        m = n // world
+        local = torch.empty((m, p * world), dtype=dt, device=cdev).normal_(0.0, 0.05)
+        for exact in (True, False):
+            fn = lambda: sh.aggregate_peer_sharded(local, w, exact=exact)  # noqa: E731
+            wall, _ = time_kernel(fn, iters, 2, world)
+            key = "peer_sharded_exact" if exact else "peer_sharded_reduce_scatter"
+            res[key] = {"ms": round(wall / iters * 1e3, 3), "peers_per_rank": m,
+                        "model_params": p * world, "bit_exact": exact}
+        del local
     return res
 
 
@@ -570,14 +611,13 @@ def main():
             "us_per_launch": round(kern_s * 1e6, 2),
         },
     }
-    if args.allgather and world > 1 and args.dist_backend == "nccl":
-        from accdfl_amd.core.sharding import BucketShardedFedAvg
-
-        sh = BucketShardedFedAvg(p * world, dt, device=device)
-        bucket = torch.zeros(sh.bucket_len, dtype=dt, device=device)
-        full = torch.empty(p * world, dtype=dt, device=device)
-        wall_ag, _ = time_kernel(lambda: sh.all_gather(bucket, full), 20, 3, world)
-        result["allgather"] = {"ms": round(wall_ag / 20 * 1e3, 3), "bytes_per_rank_out": p * world * es}
+    if world > 1 and not args.no_collectives:
+        del slab
+        torch.cuda.empty_cache()
+        try:  # same shapes on every rank: a failure raises on all of them, nothing waits
+            result["collectives"] = collectives(n, args.coll_params or p, dt, es, world, device, None, w)
+        except Exception as exc:  # never lose the headline line to an auxiliary leg
+            result["collectives"] = {"error": "%s: %s" % (type(exc).__name__, exc)}
     if rank == 0 and world == 1:
         if not args.no_small:
             result["small_configs"] = small_configs(device)
