@@ -100,6 +100,7 @@ def save_case(name, dt, models, weights):
         "buffers": [[list(b.shape), str(b.dtype).replace("torch.", "")] for b in models[0].buffers()],
         "weights": None if weights is None else [w if isinstance(w, int) else float(w) for w in weights],
         "requires_grad": [bool(p.requires_grad) for p in out.parameters()],
+        "in_requires_grad": [bool(p.requires_grad) for p in models[0].parameters()],
     }
     arrays["meta"] = np.array(json.dumps(meta))
     path = os.path.join(HERE, name + ".npz")
@@ -173,6 +174,11 @@ def main():
     # zip truncation (fedavg.py:24): peer 1 has fewer parameters than peer 0
     trunc_shapes = [[(100,), (50,), (30,)], [(100,)], [(100,), (50,), (30,), (9,)]]
     cases.append(("zip_truncation_n3", "f32", make_peers(3, trunc_shapes, "f32", 5700), [0.2, 0.3, 0.5]))
+    # frozen parameters (requires_grad=False survives the deepcopy, fedavg.py:20)
+    frozen = make_peers(3, [[(40,), (7, 3), (5,)]] * 3, "f32", 5800)
+    for m in frozen:
+        m.ps[1].requires_grad_(False)
+    cases.append(("frozen_param_n3", "f32", frozen, [0.5, 0.25, 0.25]))
     # more peers than one kernel pass takes (multi-pass reduce, list order kept)
     cases.append(("many_peers_n130", "f32", make_peers(130, [[(1000,)]] * 130, "f32", 6000), None))
     cases.append(("many_peers_bf16_n200", "bf16", make_peers(200, [[(520,)]] * 200, "bf16", 7000), dirichlet(200, 7)))

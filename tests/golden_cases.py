@@ -24,6 +24,7 @@ class Case:
     out: List[np.ndarray]               # reference output params (raw bits)
     out_buffers: List[np.ndarray]
     requires_grad: List[bool]
+    in_requires_grad: List[bool]
 
 
 def case_names() -> List[str]:
@@ -42,7 +43,7 @@ def load(name: str) -> Case:
     out = [z["out_%d" % i].reshape(meta["shapes"][0][i]) for i in range(n_out)]
     out_buffers = [z["outb_%d" % j] for j in range(nb)]
     return Case(meta["name"], meta["dtype"], meta["weights"], params, buffers, out, out_buffers,
-                meta["requires_grad"])
+                meta["requires_grad"], meta.get("in_requires_grad", meta["requires_grad"]))
 
 
 def as_float(bits: np.ndarray, dtype: str) -> np.ndarray:
@@ -77,7 +78,9 @@ def build_models(case: Case, device="cpu"):
     class Peer(nn.Module):
         def __init__(self, ps, bs):
             super().__init__()
-            self.ps = nn.ParameterList([nn.Parameter(to_torch(p, case.dtype)) for p in ps])
+            rg = list(case.in_requires_grad) + [True] * max(0, len(ps) - len(case.in_requires_grad))
+            self.ps = nn.ParameterList([nn.Parameter(to_torch(p, case.dtype), requires_grad=r)
+                                        for p, r in zip(ps, rg)])
             for j, b in enumerate(bs):
                 self.register_buffer("b%d" % j, torch.from_numpy(b.copy()))
 

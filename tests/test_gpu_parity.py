@@ -404,3 +404,37 @@ def test_peer_slab_mixed_direct_and_bounced_tensors():
     assert same_bits(_bits(flat, "f32"), want, "f32")
     for k, pl in enumerate(models):  # each row holds exactly its model
         assert torch.equal(slab.buf[k, : slab.total].cpu(), torch.cat([p.reshape(-1) for p in pl]))
+
+
+def test_tied_parameters_and_structure_preserved():
+    """A parameter registered in two submodules (tied weights) appears once in
+    parameters(); the result keeps the tie, like deepcopy(models[0]) does."""
+    from torch import nn
+
+    from accdfl_amd.core.gradient_aggregation.fedavg import FedAvg
+
+    def make(seed):
+        torch.manual_seed(seed)
+        m = nn.Module()
+        m.enc = nn.Linear(16, 8, bias=False)
+        m.dec = nn.Linear(8, 16, bias=True)
+        m.tied = m.enc  # same module twice: its weight is one parameter
+        m.bn = nn.BatchNorm1d(4)
+        return m
+
+    models = [make(s) for s in (1, 2, 3)]
+    w = [0.2, 0.3, 0.5]
+    for placement in ("cpu", "cuda"):
+        ms = [m.to(placement) for m in models]
+        out = FedAvg.aggregate(ms, w)
+        assert out.tied is out.enc and out.tied.weight is out.enc.weight
+        want = fedavg_param_lists_f32(ms, w)
+        for p, q in zip(out.parameters(), want):
+            assert same_bits(p.detach().cpu().numpy(), q, "f32")
+        assert torch.equal(out.bn.running_var.cpu(), ms[0].bn.running_var.cpu())
+
+
+def fedavg_param_lists_f32(models, w):
+    from oracle.fedavg_oracle import fedavg_param_lists
+
+    return fedavg_param_lists([[p.detach().cpu().numpy() for p in m.parameters()] for m in models], w, "f32")
