@@ -5,7 +5,7 @@ import pstats
 import sys
 import time
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))  # repo root
 sys.path.insert(0, os.path.join(ROOT, "decentralized-learning_amd"))
 import torch  # noqa: E402
 from torch import nn  # noqa: E402
