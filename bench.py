@@ -49,6 +49,19 @@ SMALL = {  # BASELINE configs[1] / configs[2] parameter counts
     "femnist_cnn_n32": (32, 1_690_046),
 }
 
+# Every BASELINE.json config as the share ONE GPU reduces: name ->
+# (peers, params of the whole model, dtype, GPUs the config names).  A G-GPU config's
+# per-GPU share is its parameter bucket: params / G of every peer.
+CONFIGS = {
+    "configs[0] spambase LinearModel, 4 peers (CPU plumbing in the reference)": (4, 116, "f32", 1),
+    "configs[1] CIFAR-10 GNLeNet, 8 peers, 1 GPU": (8, 85_354, "f32", 1),
+    "configs[2] FEMNIST CNN, 32 peers, 1 GPU": (32, 1_690_046, "f32", 1),
+    "configs[3] CIFAR-10 GNLeNet, 64 peers, 4 GPUs (per-GPU bucket)": (64, 85_354, "f32", 4),
+    "configs[3'] CIFAR-10 ResNet-8 variant, 64 peers, 4 GPUs (per-GPU bucket)": (64, 4_932_344, "f32", 4),
+    "configs[4] google_speech ResNet-34, 128 peers, bf16, 8 GPUs (per-GPU bucket)": (128, 21_296_355, "bf16", 8),
+    "configs[4] google_speech ResNet-34, 128 peers, bf16, whole model on 1 GPU": (128, 21_296_355, "bf16", 1),
+}
+
 
 def parse():
     ap = argparse.ArgumentParser()
@@ -368,6 +381,32 @@ def wire_ingress(p, device, reps=5):
     return out
 
 
+def baseline_configs(device, steps=50):
+    """Device-resident reduce rate of each BASELINE config's per-GPU share, through a
+    prepared dla_plan (bytes = (N + 1) * share * sizeof)."""
+    from accdfl_amd import _lib
+
+    res = {}
+    for name, (n, params, dts, gpus) in CONFIGS.items():
+        dt = torch.float32 if dts == "f32" else torch.bfloat16
+        es = 4 if dts == "f32" else 2
+        share = -(-params // gpus)
+        pitch = (share + 127) // 128 * 128
+        slab = make_slab(n, pitch, dt, device, 1000)
+        out = torch.empty(share, dtype=dt, device=device)
+        plan = _lib.Plan(_lib.DLA_F32 if dts == "f32" else _lib.DLA_BF16, [slab[k].data_ptr() for k in range(n)],
+                         [float(1.0 / n)] * n, share, out.data_ptr())
+        sp = torch.cuda.current_stream().cuda_stream
+        _, ev = time_kernel(lambda: plan.launch(sp), steps, 10, 1)
+        byts = (n + 1) * share * es
+        res[name] = {"peers": n, "params_per_gpu": share, "dtype": dts, "us_per_reduce": round(ev / steps * 1e6, 2),
+                     "GB/s": round(byts / (ev / steps) / 1e9, 1), "bytes": byts,
+                     "regime": "HBM" if byts > 256 << 20 else "Infinity-Cache / launch-latency"}
+        del slab, out, plan
+        torch.cuda.empty_cache()
+    return res
+
+
 def small_configs(device, steps=200):
     """Device-resident reduces at the BASELINE configs' own model sizes, launched through a
     prepared dla_plan (what a PeerSlab round pays)."""
@@ -621,6 +660,7 @@ def main():
     if rank == 0 and world == 1:
         if not args.no_small:
             result["small_configs"] = small_configs(device)
+            result["baseline_configs"] = baseline_configs(device)
         del slab
         torch.cuda.empty_cache()
         if not args.no_host_inclusive and args.dtype == "f32":
