@@ -94,17 +94,21 @@ def parse():
 
 
 def setup_dist(backend="nccl"):
+    """Returns (rank, world, device, cpu_group): cpu_group is a gloo group for host-side
+    waits that must not park a kernel on any GPU (None at world 1)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dev = torch.device("cuda", local % max(1, torch.cuda.device_count()))
     torch.cuda.set_device(dev)
+    cpu_group = None
     if world > 1:
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group(backend)
-    return rank, world, dev
+        cpu_group = dist.new_group(backend="gloo")
+    return rank, world, dev, cpu_group
 
 
 def barrier(world):
@@ -169,6 +173,16 @@ def cpu_baseline(n, p, budget_s):
         fedavg_flat_torch(peers, w, out)
         times.append(time.perf_counter() - t0)
     med = statistics.median(times)
+    # the same op sequence on ONE thread (BASELINE.md asks for both figures)
+    torch.set_num_threads(1)
+    t1 = []
+    start = time.perf_counter()
+    while (time.perf_counter() - start < budget_s / 2 and len(t1) < 20) or len(t1) < 2:
+        t0 = time.perf_counter()
+        fedavg_flat_torch(peers, w, out)
+        t1.append(time.perf_counter() - t0)
+    torch.set_num_threads(threads)
+    med1 = statistics.median(t1)
     return {
         "value": round((n + 1) * p * 4 / med / 1e9, 3),
         "unit": "GB/s",
@@ -176,6 +190,8 @@ def cpu_baseline(n, p, budget_s):
         "kind": "port",
         "sample": "%d full reduces of %d peers x %d fp32 (torch-CPU op sequence of fedavg.py:20-25), median "
                   "%.1f ms, %.1f s total" % (len(times), n, p, med * 1e3, sum(times)),
+        "value_1thread": round((n + 1) * p * 4 / med1 / 1e9, 3),
+        "sample_1thread": "%d full reduces, median %.1f ms" % (len(t1), med1 * 1e3),
         "cpu": _cpu_model(),
     }
 
@@ -212,6 +228,42 @@ def host_inclusive(n, p, reps=5):
     med = statistics.median(times)
     return {"value": round((n + 1) * p * 4 / med / 1e9, 3), "unit": "GB/s", "ms": round(med * 1e3, 2),
             "path": "FedAvg.aggregate(CPU nn.Modules): deepcopy (params uninitialised, pinned) + pinned pack + H2D + reduce + D2H into the result"}
+
+
+def host_inclusive_sharded(n, p, n_devices, reps=3):
+    """SURVEY.md §8(e) host-inclusive scaling line: FedAvg.aggregate on CPU modules (the
+    reference call sites) with the flat model bucket-sharded over GPUs 0..n_devices-1 of
+    THIS process, each bucket crossing its own GPU's PCIe link.  The same model at every
+    device count (strong scaling); the result is bit-identical for any count."""
+    from torch import nn
+
+    from accdfl_amd.core.gradient_aggregation import fedavg as fa
+
+    gen = torch.Generator().manual_seed(2000)
+    models = []
+    for _ in range(n):
+        m = nn.Module()
+        m.w = nn.Parameter(torch.randn(p, generator=gen) * 0.05)
+        models.append(m)
+    w = [float(1.0 / n)] * n
+    res = {}
+    for g in sorted({1, n_devices}):
+        fa.set_host_devices(list(range(g)))
+        try:
+            fa.FedAvg.aggregate(models, w)
+            times = []
+            for _ in range(reps):
+                t0 = time.perf_counter()
+                fa.FedAvg.aggregate(models, w)
+                times.append(time.perf_counter() - t0)
+        finally:
+            fa.set_host_devices([])
+            fa.release_staging()
+        med = statistics.median(times)
+        res["%d_gpu" % g] = {"ms": round(med * 1e3, 2), "GB/s": round((n + 1) * p * 4 / med / 1e9, 2)}
+    res["path"] = ("FedAvg.aggregate(CPU nn.Modules), %d x %d fp32, bucket-sharded over the GPUs of one "
+                   "process (fedavg.set_host_devices)" % (n, p))
+    return res
 
 
 def host_breakdown(n, p, device):
@@ -381,9 +433,35 @@ def wire_ingress(p, device, reps=5):
     return out
 
 
-def baseline_configs(device, steps=50):
+def _cpu_port_ms(n, share, dt, budget_s=1.5, max_elems=500_000_000):
+    """The reference op sequence (oracle/fedavg_oracle.py, torch-CPU) on the same share,
+    on this host's cores: median ms of a bounded sample, or None above max_elems."""
+    if n * share > max_elems:
+        return None, 0
+    sys.path.insert(0, ROOT)
+    from oracle.fedavg_oracle import fedavg_flat_torch  # timed CPU baseline (kind "port")
+
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    base = torch.randn(share, generator=torch.Generator().manual_seed(1000)) * 0.05
+    peers = [(base * (1.0 + 0.01 * k)).to(dt) for k in range(n)]  # values do not change CPU time
+    w = [float(1.0 / n)] * n
+    out = torch.empty(share, dtype=dt)
+    fedavg_flat_torch(peers, w, out)
+    ts = []
+    start = time.perf_counter()
+    while (time.perf_counter() - start < budget_s and len(ts) < 50) or len(ts) < 3:
+        t0 = time.perf_counter()
+        fedavg_flat_torch(peers, w, out)
+        ts.append(time.perf_counter() - t0)
+    return statistics.median(ts) * 1e3, threads
+
+
+def baseline_configs(device, steps=50, cpu=True):
     """Device-resident reduce rate of each BASELINE config's per-GPU share, through a
-    prepared dla_plan (bytes = (N + 1) * share * sizeof)."""
+    prepared dla_plan (bytes = (N + 1) * share * sizeof), beside the reference op sequence
+    on the host's cores for the same share (flat, one tensor per peer: a lower bound on
+    the reference's per-tensor loop, which pays T dispatches per peer)."""
     from accdfl_amd import _lib
 
     res = {}
@@ -404,6 +482,11 @@ def baseline_configs(device, steps=50):
                      "regime": "HBM" if byts > 256 << 20 else "Infinity-Cache / launch-latency"}
         del slab, out, plan
         torch.cuda.empty_cache()
+        if cpu:
+            ms, threads = _cpu_port_ms(n, share, dt)
+            if ms is not None:
+                res[name].update({"cpu_port_ms": round(ms, 3), "cpu_port_GB/s": round(byts / (ms / 1e3) / 1e9, 2),
+                                  "cpu_threads": threads, "gpu_over_cpu": round(ms * 1e3 / (ev / steps * 1e6), 1)})
     return res
 
 
@@ -574,7 +657,7 @@ def measured_ceilings(device, nbytes=1 << 30):
 
 def main():
     args = parse()
-    rank, world, device = setup_dist(args.dist_backend)
+    rank, world, device, cpu_group = setup_dist(args.dist_backend)
     from accdfl_amd import _lib
     from accdfl_amd.core import wsum
 
@@ -657,6 +740,16 @@ def main():
             result["collectives"] = collectives(n, args.coll_params or p, dt, es, world, device, None, w)
         except Exception as exc:  # never lose the headline line to an auxiliary leg
             result["collectives"] = {"error": "%s: %s" % (type(exc).__name__, exc)}
+    if world > 1 and not args.no_host_inclusive and args.dtype == "f32":
+        # rank 0 alone drives GPUs 0..G-1 from one process (the reference's CPU-module call
+        # sites); the other ranks wait on the CPU (gloo), so no RCCL kernel sits on a GPU
+        if rank == 0:
+            try:
+                g = min(world, torch.cuda.device_count())
+                result["host_inclusive_sharded"] = host_inclusive_sharded(n, p, g)
+            except Exception as exc:  # never lose the headline line to an auxiliary leg
+                result["host_inclusive_sharded"] = {"error": "%s: %s" % (type(exc).__name__, exc)}
+        dist.barrier(group=cpu_group)
     if rank == 0 and world == 1:
         if not args.no_small:
             result["small_configs"] = small_configs(device)

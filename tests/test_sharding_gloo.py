@@ -28,6 +28,15 @@ def _oracle_reducer(peers, weights, out):
     return out
 
 
+def _hip_reducer(peers, weights, out):
+    """The libdlagg kernel on cuda:0 (every rank of the rehearsal shares the one GPU)."""
+    from accdfl_amd.core import wsum
+
+    dev = torch.device("cuda", 0)
+    out.copy_(wsum.wsum([p.to(dev) for p in peers], weights).cpu())
+    return out
+
+
 def _inputs(n_peers, n_elems):
     rng = np.random.default_rng(123)
     peers = (rng.standard_normal((n_peers, n_elems)) * 0.05).astype(np.float32)
@@ -35,7 +44,7 @@ def _inputs(n_peers, n_elems):
     return peers, weights
 
 
-def _worker(rank, world, port, n_peers, n_elems, root, q):
+def _worker(rank, world, port, n_peers, n_elems, root, q, reducer="oracle"):
     import sys
 
     for p in (os.path.join(root, "decentralized-learning_amd"), root):
@@ -46,7 +55,8 @@ def _worker(rank, world, port, n_peers, n_elems, root, q):
         from accdfl_amd.core.sharding import BucketShardedFedAvg
 
         peers, weights = _inputs(n_peers, n_elems)
-        sh = BucketShardedFedAvg(n_elems, torch.float32, reducer=_oracle_reducer)
+        sh = BucketShardedFedAvg(n_elems, torch.float32,
+                                 reducer=_hip_reducer if reducer == "hip" else _oracle_reducer)
         # (1) bucket-sharded: this rank holds its bucket of every peer
         s, e = sh.local_range
         buckets = [torch.from_numpy(peers[k, s:e].copy()) for k in range(n_peers)]
@@ -64,13 +74,26 @@ def _worker(rank, world, port, n_peers, n_elems, root, q):
 
 @pytest.mark.parametrize("world,n_peers,n_elems", [(2, 8, 10_001), (3, 6, 4_099), (2, 4, 37)])
 def test_sharded_fedavg_is_bit_exact(world, n_peers, n_elems):
+    _run_sharded(world, n_peers, n_elems, "oracle")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,n_peers,n_elems", [(2, 8, 1_000_003), (4, 8, 65_537)])
+def test_sharded_fedavg_hip_reducer_is_bit_exact(world, n_peers, n_elems):
+    """The same exchange steps with the libdlagg kernel as each rank's bucket reducer
+    (gloo ranks sharing the box's one GPU; the RCCL transport is the driver's 8-GPU run)."""
+    _run_sharded(world, n_peers, n_elems, "hip")
+
+
+def _run_sharded(world, n_peers, n_elems, reducer):
     from oracle.fedavg_oracle import fedavg_bits
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, n_peers, n_elems, root, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n_peers, n_elems, root, q, reducer))
+             for r in range(world)]
     for p in procs:
         p.start()
     results = [q.get(timeout=240) for _ in range(world)]
