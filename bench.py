@@ -21,6 +21,12 @@ Extra objects on the JSON line:
                 situation): pack + H2D + reduce + D2H, rank 0 at N=1 only
   small_configs device-resident rates of the BASELINE configs 1-2 model sizes
                 (cache-resident / launch-bound; informational)
+  baseline_configs  every BASELINE config at its per-GPU share (prepared launch), with
+                the torch-CPU op sequence timed on the same share beside it
+  host_inclusive_sharded  (N > 1, rank 0) the CPU-module path bucket-sharded over GPUs
+                0..N-1 of one process (each bucket over its own PCIe link), strong scaling
+  collectives   (N > 1) the RCCL legs: all-gather reassembly, exact peer-sharded
+                all-to-all path, reduce-scatter tolerance path
 """
 from __future__ import annotations
 
@@ -227,7 +233,8 @@ def host_inclusive(n, p, reps=5):
         times.append(time.perf_counter() - t0)
     med = statistics.median(times)
     return {"value": round((n + 1) * p * 4 / med / 1e9, 3), "unit": "GB/s", "ms": round(med * 1e3, 2),
-            "path": "FedAvg.aggregate(CPU nn.Modules): deepcopy (params uninitialised, pinned) + pinned pack + H2D + reduce + D2H into the result"}
+            "path": "FedAvg.aggregate(CPU nn.Modules): deepcopy (params uninitialised, pinned) + chunked H2D straight "
+                    "from the parameters + reduce + D2H into the result, chunk c's D2H overlapping chunk c+1's H2D"}
 
 
 def host_inclusive_sharded(n, p, n_devices, reps=3):
@@ -247,8 +254,10 @@ def host_inclusive_sharded(n, p, n_devices, reps=3):
         models.append(m)
     w = [float(1.0 / n)] * n
     res = {}
-    for g in sorted({1, n_devices}):
+    runs = [(1, True)] + ([(n_devices, True), (n_devices, False)] if n_devices > 1 else [])
+    for g, threads in runs:
         fa.set_host_devices(list(range(g)))
+        fa.set_shard_threads(threads)
         try:
             fa.FedAvg.aggregate(models, w)
             times = []
@@ -258,9 +267,11 @@ def host_inclusive_sharded(n, p, n_devices, reps=3):
                 times.append(time.perf_counter() - t0)
         finally:
             fa.set_host_devices([])
+            fa.set_shard_threads(True)
             fa.release_staging()
         med = statistics.median(times)
-        res["%d_gpu" % g] = {"ms": round(med * 1e3, 2), "GB/s": round((n + 1) * p * 4 / med / 1e9, 2)}
+        key = "%d_gpu" % g + ("" if g == 1 else ("_pipelined" if threads else "_packed"))
+        res[key] = {"ms": round(med * 1e3, 2), "GB/s": round((n + 1) * p * 4 / med / 1e9, 2)}
     res["path"] = ("FedAvg.aggregate(CPU nn.Modules), %d x %d fp32, bucket-sharded over the GPUs of one "
                    "process (fedavg.set_host_devices)" % (n, p))
     return res

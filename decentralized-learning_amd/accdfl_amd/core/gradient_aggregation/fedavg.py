@@ -231,6 +231,85 @@ def _small_round(models: List[nn.Module], weights) -> "nn.Module | None":
     return center
 
 
+def _stage_rows(st, dev, k: int, flat: List[torch.Tensor], numels: List[int], s: int, e: int):
+    """Peer k's elements [s, e) -> row k of st.d_in (pinned pack + async H2D on the copy stream)."""
+    parts = _flat_slices(flat, numels, s, e)
+    if all(t.device.type == "cpu" for t in flat):
+        row = st.h_in[k, : e - s]
+        if len(parts) == 1:
+            row.copy_(parts[0])
+        else:
+            torch.cat(parts, out=row)
+        with torch.cuda.device(dev), torch.cuda.stream(st.copy_stream):
+            st.d_in[k, : e - s].copy_(row, non_blocking=True)
+    else:
+        with torch.cuda.device(dev), torch.cuda.stream(st.copy_stream):
+            torch.cat([t.to(dev, non_blocking=True) for t in parts], out=st.d_in[k, : e - s])
+
+
+def _reduce_rows(st, dev, weights, center: List[torch.Tensor], numels: List[int], s: int, e: int, h_out):
+    """Reduce rows 0..n-1 of st.d_in after the copies land, then D2H the bucket [s, e)
+    straight into the result's parameters (h_out is None) or into h_out[s:e]."""
+    compute = torch.cuda.current_stream(dev)
+    compute.wait_stream(st.copy_stream)
+    with torch.cuda.device(dev):
+        _wsum.wsum_rows(st.d_in, weights, e - s, out=st.d_out)
+        dst = _flat_slices(center, numels, s, e) if h_out is None else [h_out[s:e]]
+        off = 0
+        for d in dst:
+            d.copy_(st.d_out[off:off + d.numel()], non_blocking=True)
+            off += d.numel()
+
+
+_PIPE_CHUNKS = 4               # element chunks per bucket in the pipelined host path
+_PIPE_MIN_CHUNK_BYTES = 8 << 20
+
+
+def _bucket_pipelined(st, dev, flats: List[List[torch.Tensor]], numels: List[int], s: int, e: int, weights,
+                      center: List[torch.Tensor], h_out, align: int):
+    """Bucket [s, e) of every peer through one GPU in element chunks: chunk c's H2D copies
+    go straight from the (pageable) parameters, then its reduce and its D2H are enqueued,
+    so the D2H of chunk c runs while chunk c+1 is still coming in (PCIe is full duplex).
+    Every element still folds all peers in list order: the result is unchanged."""
+    n = len(flats)
+    esize = st.d_in.element_size()
+    chunk = max(_PIPE_MIN_CHUNK_BYTES // esize, -(-(e - s) // _PIPE_CHUNKS))
+    chunk = _round_up(chunk, align)
+    compute = torch.cuda.current_stream(dev)
+    with torch.cuda.device(dev):
+        for cs in range(s, e, chunk):
+            ce = min(e, cs + chunk)
+            with torch.cuda.stream(st.copy_stream):
+                for k in range(n):
+                    off = cs - s
+                    for t in _flat_slices(flats[k], numels, cs, ce):
+                        st.d_in[k, off:off + t.numel()].copy_(t if t.device == dev or t.device.type == "cpu"
+                                                              else t.to(dev, non_blocking=True), non_blocking=True)
+                        off += t.numel()
+            compute.wait_stream(st.copy_stream)
+            _wsum.wsum_rows(st.d_in[:, cs - s:ce - s], weights, ce - cs, out=st.d_out[cs - s:ce - s])
+            dst = _flat_slices(center, numels, cs, ce) if h_out is None else [h_out[cs:ce]]
+            off = cs - s
+            for d in dst:
+                d.view(-1).copy_(st.d_out[off:off + d.numel()], non_blocking=True)
+                off += d.numel()
+        compute.synchronize()
+
+
+# How the host-staged path moves a large round: "pipelined" (default) — one Python thread
+# per GPU, each streaming its bucket through _bucket_pipelined (H2D straight from the
+# pageable parameters, no host pack; torch releases the GIL inside the copies, so the GPUs'
+# copies run concurrently) — or "packed": one thread packing every peer into pinned
+# staging peer-major and issuing the DMAs (the packs are serial, the DMAs overlap).
+# ACCDFL_AMD_HOST_PATH=packed selects the latter.
+_SHARD_THREADS = os.environ.get("ACCDFL_AMD_HOST_PATH", "pipelined") != "packed"
+
+
+def set_shard_threads(enabled: bool) -> None:
+    global _SHARD_THREADS
+    _SHARD_THREADS = bool(enabled)
+
+
 def _reduce_host_staged(devices: List[torch.device], dtype, center: List[torch.Tensor],
                         peers: List[List[torch.Tensor]], weights):
     """One dtype group, every model contributing to every tensor: pack -> H2D -> reduce -> D2H,
@@ -251,6 +330,7 @@ def _reduce_host_staged(devices: List[torch.device], dtype, center: List[torch.T
     devices = devices[:g_max]
     bounds = bucket_bounds(total, len(devices), align)
     n = len(peers)
+    flats = [[p.detach().reshape(-1) for p in pl] for pl in peers]
     with _staging_lock:
         stages = []
         for dev, (s, e) in zip(devices, bounds):
@@ -258,42 +338,32 @@ def _reduce_host_staged(devices: List[torch.device], dtype, center: List[torch.T
             st.ensure(n, _round_up(max(e - s, 1), align))
             st.copy_stream.wait_stream(torch.cuda.current_stream(dev))  # previous users of d_in are done
             stages.append(st)
-        for k in range(n):
-            flat = [p.detach().reshape(-1) for p in peers[k]]
-            on_cpu = all(t.device.type == "cpu" for t in flat)
-            for st, dev, (s, e) in zip(stages, devices, bounds):
-                if s == e:
-                    continue
-                parts = _flat_slices(flat, numels, s, e)
-                if on_cpu:
-                    row = st.h_in[k, : e - s]
-                    if len(parts) == 1:
-                        row.copy_(parts[0])
-                    else:
-                        torch.cat(parts, out=row)
-                    with torch.cuda.stream(st.copy_stream):
-                        st.d_in[k, : e - s].copy_(row, non_blocking=True)
-                else:
-                    with torch.cuda.device(dev), torch.cuda.stream(st.copy_stream):
-                        torch.cat([t.to(dev, non_blocking=True) for t in parts], out=st.d_in[k, : e - s])
+        # D2H straight into the result's parameters when they are pinned and dense (see
+        # _center_copy); otherwise through one pinned buffer.
         direct = all(c.is_pinned() and c.is_contiguous() for c in center)
         h_out = None if direct else torch.empty(total, dtype=dtype, pin_memory=True)
-        for st, dev, (s, e) in zip(stages, devices, bounds):
-            if s == e:
-                continue
-            compute = torch.cuda.current_stream(dev)
-            compute.wait_stream(st.copy_stream)
-            with torch.cuda.device(dev):
-                _wsum.wsum_rows(st.d_in, weights, e - s, out=st.d_out)
-                # D2H straight into the result's parameters when they are pinned and dense
-                # (see _center_copy); otherwise through one pinned buffer.
-                dst = _flat_slices(center, numels, s, e) if direct else [h_out[s:e]]
-                off = 0
-                for d in dst:
-                    d.copy_(st.d_out[off:off + d.numel()], non_blocking=True)
-                    off += d.numel()
-        for dev in devices:
-            torch.cuda.current_stream(dev).synchronize()
+        jobs = [(st, dev, s, e) for st, dev, (s, e) in zip(stages, devices, bounds) if s < e]
+        if _SHARD_THREADS:
+            from concurrent.futures import ThreadPoolExecutor
+
+            def bucket(job):
+                st, dev, s, e = job
+                with torch.no_grad():  # grad mode is per thread; the result's parameters are leaves
+                    _bucket_pipelined(st, dev, flats, numels, s, e, weights, center, h_out, align)
+
+            if len(jobs) == 1:
+                bucket(jobs[0])
+            else:
+                with ThreadPoolExecutor(max_workers=len(jobs)) as pool:
+                    list(pool.map(bucket, jobs))  # re-raises the first failure
+        else:
+            for k in range(n):  # peer-major: every GPU's DMA starts as early as possible
+                for st, dev, s, e in jobs:
+                    _stage_rows(st, dev, k, flats[k], numels, s, e)
+            for st, dev, s, e in jobs:
+                _reduce_rows(st, dev, weights, center, numels, s, e, h_out)
+            for dev in devices:
+                torch.cuda.current_stream(dev).synchronize()
         if not direct:
             for c, o in zip(center, torch.split(h_out, numels)):
                 c.copy_(o.view_as(c))

@@ -310,10 +310,12 @@ def test_device_model_manager_falls_back_on_mixed_layouts():
         assert same_bits(p.detach().numpy(), q, "f32")
 
 
+@pytest.mark.parametrize("threads", [True, False])
 @pytest.mark.parametrize("dtype", ["f32", "bf16"])
-def test_host_path_sharded_over_devices(dtype):
+def test_host_path_sharded_over_devices(dtype, threads):
     """CPU models bucket-sharded over several devices (here three shards on cuda:0: the
-    same code path as three GPUs) — buckets cut through parameter tensors, result bit-exact."""
+    same code path as three GPUs) — buckets cut through parameter tensors, result bit-exact,
+    with one host thread per GPU and with the serial peer-major issue."""
     from torch import nn
 
     from accdfl_amd.core.gradient_aggregation import fedavg as fa
@@ -326,10 +328,12 @@ def test_host_path_sharded_over_devices(dtype):
         models.append(m)
     w = [0.3, 0.1, 0.2, 0.25, 0.15]
     fa.set_host_devices(["cuda:0", "cuda:0", "cuda:0"])
+    fa.set_shard_threads(threads)
     try:
         out = fa.FedAvg.aggregate(models, w)
     finally:
         fa.set_host_devices([])
+        fa.set_shard_threads(True)
     for i, p in enumerate(out.parameters()):
         want = fedavg_bits([gc.as_float(_bits(m[i].detach().reshape(-1), dtype), dtype) for m in models], w, dtype)
         assert same_bits(gc.as_float(_bits(p.detach().reshape(-1), dtype), dtype), want, dtype), i
