@@ -21,7 +21,7 @@ LIB_PATH = os.environ.get("DLAGG_LIB", os.path.join(PKG_ROOT, "lib", "libdlagg.s
 
 # dtype codes (include/dlagg.h)
 DLA_F32, DLA_BF16, DLA_F16, DLA_F64 = 0, 1, 2, 3
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 HIPCC_FLAGS = [
     "--offload-arch=gfx950",
@@ -46,6 +46,7 @@ EXPORTED = (
     "dla_plan_launch",
     "dla_plan_destroy",
     "dla_mean",
+    "dla_host_copy_batch",
 )
 
 
@@ -119,6 +120,9 @@ class _Lib:
         so.dla_plan_launch.restype = ctypes.c_int
         so.dla_mean.argtypes = [ctypes.c_int, ctypes.POINTER(vp), ctypes.c_int, ctypes.c_int64, vp, vp]
         so.dla_mean.restype = ctypes.c_int
+        so.dla_host_copy_batch.argtypes = [ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(ctypes.c_int64),
+                                           ctypes.c_int]
+        so.dla_host_copy_batch.restype = ctypes.c_int
         so.dla_plan_destroy.argtypes = [vp]
         so.dla_plan_destroy.restype = None
         v = so.dla_version()
@@ -210,6 +214,16 @@ def wsum_multi_ptrs(dtype_code: int, peer_ptrs: Sequence[int], out_ptrs: Sequenc
     rc = L.so.dla_wsum_multi(dtype_code, t, _ptr_array(peer_ptrs), _ptr_array(out_ptrs), num, _dbl_array(weights),
                              n, stream_ptr)
     L.check(rc, "dla_wsum_multi")
+
+
+def host_copy_batch(dst_ptrs: Sequence[int], src_ptrs: Sequence[int], nbytes: Sequence[int]) -> None:
+    """dla_host_copy_batch: dst_ptrs[i] <- src_ptrs[i] (host memory), nbytes[i] bytes each."""
+    L = lib()
+    m = len(nbytes)
+    rc = L.so.dla_host_copy_batch((ctypes.c_void_p * m)(*dst_ptrs), (ctypes.c_void_p * m)(*src_ptrs),
+                                  (ctypes.c_int64 * m)(*nbytes), m)
+    if rc != 0:
+        L.check(rc, "dla_host_copy_batch")
 
 
 class Plan:

@@ -173,8 +173,21 @@ def _start_host_small(device, dtype, peers: List[List[torch.Tensor]], weights, t
         st = _staging[key] = _HostStaging(device, dtype)
     st.ensure(n, pitch)
     compute = torch.cuda.current_stream(device)
+    # flatten every peer into its pinned row with one native batched memcpy (a torch.cat per
+    # peer costs ~30 us of dispatch and threading for a 341 KB GNLeNet row)
+    esize = st.h_in.element_size()
+    row_bytes = st.h_in.stride(0) * esize
+    base = st.h_in.data_ptr()
+    dsts, srcs, nbytes = [], [], []
     for k in range(n):
-        torch.cat([p.detach().view(-1) for p in peers[k]], out=st.h_in[k, :total])
+        off = base + k * row_bytes
+        for p in peers[k]:
+            b = p.numel() * esize
+            dsts.append(off)
+            srcs.append(p.data_ptr())
+            nbytes.append(b)
+            off += b
+    _lib.host_copy_batch(dsts, srcs, nbytes)
     st.d_in[:n].copy_(st.h_in[:n], non_blocking=True)  # one DMA for every row
     st.plan_for(n, total, weights).launch(int(compute.cuda_stream))
     st.h_out[:total].copy_(st.d_out[:total], non_blocking=True)
@@ -182,8 +195,17 @@ def _start_host_small(device, dtype, peers: List[List[torch.Tensor]], weights, t
 
 
 def _finish_host_small(st, compute, center: List[torch.Tensor], numels: List[int], total: int):
+    """Wait for the D2H, then scatter the averaged row into the (contiguous) result tensors."""
     compute.synchronize()
-    torch._foreach_copy_([c.view(-1) for c in center], list(torch.split(st.h_out[:total], numels)))
+    esize = st.h_out.element_size()
+    src = st.h_out.data_ptr()
+    dsts, srcs, nbytes = [], [], []
+    for c, m in zip(center, numels):
+        dsts.append(c.data_ptr())
+        srcs.append(src)
+        nbytes.append(m * esize)
+        src += m * esize
+    _lib.host_copy_batch(dsts, srcs, nbytes)
 
 
 def _reduce_host_small(device, dtype, center: List[torch.Tensor], peers: List[List[torch.Tensor]], weights,

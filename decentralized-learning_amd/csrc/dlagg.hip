@@ -858,4 +858,17 @@ int dla_mean(int dtype, const void* const* peers, int n_peers, int64_t n_elems, 
   return DLA_OK;
 }
 
+int dla_host_copy_batch(void* const* dsts, const void* const* srcs, const int64_t* bytes, int n) {
+  g_last_error.clear();
+  if (n < 0 || (n > 0 && (!dsts || !srcs || !bytes))) return fail(DLA_E_INVALID, "dla_host_copy_batch: bad table");
+  for (int i = 0; i < n; ++i) {
+    if (bytes[i] < 0) return fail(DLA_E_INVALID, "dla_host_copy_batch: negative size at " + std::to_string(i));
+    if (bytes[i] > 0 && (!dsts[i] || !srcs[i]))
+      return fail(DLA_E_INVALID, "dla_host_copy_batch: null pointer at " + std::to_string(i));
+  }
+  for (int i = 0; i < n; ++i)
+    if (bytes[i] > 0) std::memcpy(dsts[i], srcs[i], static_cast<size_t>(bytes[i]));
+  return DLA_OK;
+}
+
 }  // extern "C"

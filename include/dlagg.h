@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define DLA_ABI_VERSION 2
+#define DLA_ABI_VERSION 3
 
 /* element dtypes of the peer buffers and of the output */
 #define DLA_F32 0
@@ -122,6 +122,15 @@ int dla_plan_create(dla_plan_t** plan, int dtype, const void* const* peers, cons
 int dla_plan_set_weights(dla_plan_t* plan, const double* weights);
 int dla_plan_launch(const dla_plan_t* plan, void* stream);
 void dla_plan_destroy(dla_plan_t* plan);
+
+/* Host-side staging for CPU-resident peers (no GPU work, HOST pointers only):
+ * dsts[i] <- srcs[i] for i < n, bytes[i] bytes each, in one call.  Replaces the
+ * per-parameter flatten of `m.parameters()` (the zip order of fedavg.py:24) into a
+ * pinned staging row before the H2D copy, and the unflatten of the averaged row back
+ * into the result's parameters (fedavg.py:20, 25: the values land in the deepcopy's
+ * tensors).  One native call instead of a torch op per tensor: the GL merge of two
+ * GNLeNet models (configs[1]) packs 28 tensors per round.  Regions must not overlap. */
+int dla_host_copy_batch(void* const* dsts, const void* const* srcs, const int64_t* bytes, int n);
 
 #ifdef __cplusplus
 }

@@ -44,7 +44,7 @@ def test_library_version_and_argument_errors(lib_path):
     from accdfl_amd import _lib
 
     L = _lib.lib()
-    assert L.so.dla_version() == 2
+    assert L.so.dla_version() == 3
     assert L.max_peers_per_pass == 128
     # n_peers = 0 -> DLA_E_INVALID with a message
     rc = L.so.dla_wsum(0, None, None, 0, 10, None, None)
@@ -64,6 +64,30 @@ def test_library_version_and_argument_errors(lib_path):
     for bad in (_lib.LaunchCfg(3, 0, 0, 0), _lib.LaunchCfg(4, 3, 0, 0), _lib.LaunchCfg(4, 1, 0, 128)):
         with pytest.raises(_lib.DlaggError):
             _lib.wsum_ptrs(0, [4096], [1.0], 64, 8192, 0, bad)
+
+
+def test_host_copy_batch_runs_on_cpu(lib_path):
+    """dla_host_copy_batch is host-only: it gathers and scatters here without a GPU."""
+    import numpy as np
+
+    from accdfl_amd import _lib
+
+    rng = np.random.default_rng(0)
+    srcs = [rng.standard_normal(s).astype(np.float32) for s in (3, 0, 1000, 17)]
+    row = np.zeros(sum(a.size for a in srcs), dtype=np.float32)
+    dsts, off = [], 0
+    for a in srcs:
+        dsts.append(row.ctypes.data + off * 4)
+        off += a.size
+    _lib.host_copy_batch(dsts, [a.ctypes.data for a in srcs], [a.nbytes for a in srcs])
+    assert np.array_equal(row, np.concatenate(srcs))
+    back = [np.empty_like(a) for a in srcs]
+    _lib.host_copy_batch([b.ctypes.data for b in back], dsts, [a.nbytes for a in srcs])
+    assert all(np.array_equal(a, b) for a, b in zip(srcs, back))
+    with pytest.raises(_lib.DlaggError, match="null"):
+        _lib.host_copy_batch([0], [srcs[0].ctypes.data], [12])
+    with pytest.raises(_lib.DlaggError, match="negative"):
+        _lib.host_copy_batch([row.ctypes.data], [srcs[0].ctypes.data], [-1])
 
 
 def _tiny_models(n):
