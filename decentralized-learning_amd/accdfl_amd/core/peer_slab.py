@@ -22,6 +22,7 @@ from typing import List, Optional, Sequence
 import torch
 from torch import nn
 
+from accdfl_amd import _lib
 from accdfl_amd.core import wsum as _wsum
 
 _ALIGN_BYTES = 256
@@ -122,10 +123,13 @@ class PeerSlab:
             bounce = None
             run_start = None  # element offset where the current run of small tensors begins
             off = 0
+            pending = ([], [], [])  # (dst, src, bytes) of the run: one native batched memcpy
             with torch.cuda.stream(self.copy_stream):
                 for t in flat + [None]:
                     small = t is not None and t.numel() * esize < self.DIRECT_BYTES
                     if not small and run_start is not None:  # flush the run of small tensors
+                        _lib.host_copy_batch(*pending)
+                        pending = ([], [], [])
                         self.buf[row, run_start:off].copy_(bounce[run_start:off], non_blocking=True)
                         run_start = None
                     if t is None:
@@ -135,7 +139,9 @@ class PeerSlab:
                             bounce = self._bounce_buffer(slot)
                         if run_start is None:
                             run_start = off
-                        bounce[off:off + t.numel()].copy_(t)
+                        pending[0].append(bounce.data_ptr() + off * esize)
+                        pending[1].append(t.data_ptr())
+                        pending[2].append(t.numel() * esize)
                     else:
                         self.buf[row, off:off + t.numel()].copy_(t)  # pageable H2D, no host copy
                     off += t.numel()
@@ -172,14 +178,19 @@ class PeerSlab:
         cur.wait_stream(self.copy_stream)
         return _wsum.wsum_rows(self.buf, weights, self.total, out=out)
 
+    def _offsets(self) -> List[int]:
+        offs, o = [], 0
+        for m in self.numels:
+            offs.append(o)
+            o += m
+        return offs
+
     def unflatten(self, flat: torch.Tensor) -> List[torch.Tensor]:
         return [t.view(s) for t, s in zip(torch.split(flat[: self.total], self.numels), self.shapes)]
 
     def _reduce_planned(self, weights: Optional[Sequence[float]]) -> torch.Tensor:
         """reduce() into the slab's own result buffer through a cached dla_plan (the
         same rows and output every round: only the launch is paid)."""
-        from accdfl_amd import _lib
-
         n = self.n
         if not weights:
             weights = [float(1. / n) for _ in range(n)]
@@ -213,13 +224,15 @@ class PeerSlab:
                 p.view(-1).copy_(v, non_blocking=True)  # D2H straight into the result
             torch.cuda.current_stream(self.device).synchronize()
             return
-        if all(p.is_contiguous() for p in params):  # small rounds: one D2H, one host unpack
-            if self._h_out is None or self._h_out.numel() < self.total:
+        if all(p.is_contiguous() and p.device.type == "cpu" for p in params):  # small rounds: one D2H,
+            if self._h_out is None or self._h_out.numel() < self.total:      # one native host scatter
                 self._h_out = torch.empty(self.pitch, dtype=self.dtype, pin_memory=True)
             h = self._h_out[: self.total]
             h.copy_(flat, non_blocking=True)
             torch.cuda.current_stream(self.device).synchronize()
-            torch._foreach_copy_([p.view(-1) for p in params], list(torch.split(h, self.numels)))
+            esize = h.element_size()
+            srcs = [h.data_ptr() + o * esize for o in self._offsets()]
+            _lib.host_copy_batch([p.data_ptr() for p in params], srcs, [m * esize for m in self.numels])
             return
         if self._h_out is None or self._h_out.numel() < self.total:
             self._h_out = torch.empty(self.pitch, dtype=self.dtype, pin_memory=True)

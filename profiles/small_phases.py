@@ -63,8 +63,24 @@ def unpack():
     torch._foreach_copy_([c.view(-1) for c in cparams], list(torch.split(st.h_out[:total], numels)))
 
 
+from types import SimpleNamespace  # noqa: E402
+
+from accdfl_amd.core.gradient_aggregation import GradientAggregationMethod  # noqa: E402
+from accdfl_amd.core.model_manager import DeviceModelManager  # noqa: E402
+
+mm = DeviceModelManager(None, SimpleNamespace(gradient_aggregation=GradientAggregationMethod.FEDAVG), 0, capacity=n)
+
+
+def dmm_round():
+    mm.reset_incoming_trained_models()
+    for k, m in enumerate(models):
+        mm.process_incoming_trained_model(k, m)
+    return mm.aggregate_trained_models(w)
+
+
 torch.set_grad_enabled(False)
 res = {
+    "device_model_manager_round_us": t(dmm_round),
     "aggregate_us": t(lambda: fa.FedAvg.aggregate(models, w)),
     "parameters_lists_us": t(lambda: [list(m.parameters()) for m in models]),
     "center_copy_us": t(lambda: fa._center_copy(models[0], pin=False)),
