@@ -76,7 +76,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--peers", type=int, default=NS_PEERS)
     ap.add_argument("--params", type=int, default=NS_PARAMS)
-    ap.add_argument("--dtype", default="f32", choices=["f32", "bf16", "f16"])
+    ap.add_argument("--dtype", default="f32", choices=["f32", "bf16", "f16", "f64"])
     ap.add_argument("--variant", type=int, default=0)
     ap.add_argument("--chunks", type=int, default=0)
     ap.add_argument("--grid", type=int, default=0)
@@ -92,6 +92,8 @@ def parse():
                                                              "several ranks on one GPU")
     ap.add_argument("--sweep", action="store_true", help="interleaved A/B of launch variants, then exit")
     ap.add_argument("--host-breakdown", action="store_true", help="time the host-inclusive phases, then exit")
+    ap.add_argument("--configs-only", action="store_true",
+                    help="print the per-BASELINE-config device-resident table (no CPU legs), then exit")
     ap.add_argument("--sweep-cfgs", default="", help="variant,chunks,grid;... (default: built-in list)")
     ap.add_argument("--no-ceilings", action="store_true", help="skip the probe ceilings in --sweep")
     ap.add_argument("--libs", default="", help="comma list of libdlagg builds to A/B in --sweep (same process)")
@@ -468,6 +470,32 @@ def _cpu_port_ms(n, share, dt, budget_s=1.5, max_elems=500_000_000):
     return statistics.median(ts) * 1e3, threads
 
 
+def time_graph(launch, per_graph=20, reps=10):
+    """Seconds per launch with `per_graph` launches captured in one HIP graph and replayed
+    `reps` times: the device-side cost of a reduce without the host's per-launch overhead
+    (which bounds back-to-back eager launches of a few-microsecond kernel)."""
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        launch(s.cuda_stream)  # warm
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        sp = torch.cuda.current_stream().cuda_stream
+        for _ in range(per_graph):
+            launch(sp)
+    g.replay()
+    torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record()
+    for _ in range(reps):
+        g.replay()
+    ev1.record()
+    torch.cuda.synchronize()
+    del g
+    return ev0.elapsed_time(ev1) / 1e3 / (reps * per_graph)
+
+
 def baseline_configs(device, steps=50, cpu=True):
     """Device-resident reduce rate of each BASELINE config's per-GPU share, through a
     prepared dla_plan (bytes = (N + 1) * share * sizeof), beside the reference op sequence
@@ -487,9 +515,11 @@ def baseline_configs(device, steps=50, cpu=True):
                          [float(1.0 / n)] * n, share, out.data_ptr())
         sp = torch.cuda.current_stream().cuda_stream
         _, ev = time_kernel(lambda: plan.launch(sp), steps, 10, 1)
+        tg = time_graph(plan.launch)
         byts = (n + 1) * share * es
         res[name] = {"peers": n, "params_per_gpu": share, "dtype": dts, "us_per_reduce": round(ev / steps * 1e6, 2),
                      "GB/s": round(byts / (ev / steps) / 1e9, 1), "bytes": byts,
+                     "us_per_reduce_graph": round(tg * 1e6, 2), "GB/s_graph": round(byts / tg / 1e9, 1),
                      "regime": "HBM" if byts > 256 << 20 else "Infinity-Cache / launch-latency"}
         del slab, out, plan
         torch.cuda.empty_cache()
@@ -524,8 +554,8 @@ def sweep(args, device):
     from accdfl_amd import _lib
     from accdfl_amd.core import wsum
 
-    dt = {"f32": torch.float32, "bf16": torch.bfloat16, "f16": torch.float16}[args.dtype]
-    es = 4 if args.dtype == "f32" else 2
+    dt = {"f32": torch.float32, "bf16": torch.bfloat16, "f16": torch.float16, "f64": torch.float64}[args.dtype]
+    es = {"f32": 4, "f64": 8}.get(args.dtype, 2)
     slab = make_slab(args.peers, (args.params + 127) // 128 * 128, dt, device, 1000)  # 16-B aligned rows
     out = torch.empty(args.params, dtype=dt, device=device)
     w = [float(1.0 / args.peers)] * args.peers
@@ -678,6 +708,10 @@ def main():
         return
     if args.host_breakdown:
         print(json.dumps(host_breakdown(args.peers, args.params, device)))
+        return
+    if args.configs_only:
+        for name, row in baseline_configs(device, cpu=False).items():
+            print(json.dumps(dict(config=name, **row)))
         return
     dt = {"f32": torch.float32, "bf16": torch.bfloat16, "f16": torch.float16}[args.dtype]
     es = 4 if args.dtype == "f32" else 2

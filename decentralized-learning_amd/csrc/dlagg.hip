@@ -56,6 +56,9 @@ int fail(int code, const std::string& msg) {
 // always exactly representable in the storage dtype (the reference stores the
 // running sum in the parameter tensor after every add).
 
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
 template <int DT> struct Ops;
 
 template <> struct Ops<DLA_F32> {
@@ -75,6 +78,11 @@ template <> struct Ops<DLA_F32> {
   __device__ static elem_t from_acc(acc_t a) { return a; }
   __device__ static acc_t zero_mul(acc_t x) { return x * 0.0f; }                 // fedavg.py:22
   __device__ static acc_t step(acc_t acc, w_t w, acc_t x) { return acc + w * x; } // fedavg.py:25
+  // one word per lane in the wide kernel: 4 bytes = 1 element
+  using word_t = uint32_t;
+  static constexpr int WE = 1;
+  __device__ static void unpack_w(word_t v, acc_t* x) { x[0] = __uint_as_float(v); }
+  __device__ static word_t pack_w(const acc_t* a) { return __float_as_uint(a[0]); }
 };
 
 template <> struct Ops<DLA_F64> {
@@ -94,6 +102,13 @@ template <> struct Ops<DLA_F64> {
   __device__ static elem_t from_acc(acc_t a) { return a; }
   __device__ static acc_t zero_mul(acc_t x) { return x * 0.0; }
   __device__ static acc_t step(acc_t acc, w_t w, acc_t x) { return acc + w * x; }
+  using word_t = u32x2;  // 8 bytes = 1 element
+  static constexpr int WE = 1;
+  __device__ static void unpack_w(word_t v, acc_t* x) { x[0] = __hiloint2double(v.y, v.x); }
+  __device__ static word_t pack_w(const acc_t* a) {
+    word_t w = {static_cast<uint32_t>(__double2loint(a[0])), static_cast<uint32_t>(__double2hiint(a[0]))};
+    return w;
+  }
 };
 
 // bf16: op-math float, every product and every sum rounded RNE to bf16
@@ -131,6 +146,15 @@ template <> struct Ops<DLA_BF16> {
   __device__ static acc_t zero_mul(acc_t x) { return x * 0.0f; }  // +-0 or NaN: already bf16-exact
   __device__ static acc_t step(acc_t acc, w_t w, acc_t x) {
     return round_bf16(acc + round_bf16(w * x));
+  }
+  using word_t = uint32_t;  // 4 bytes = 2 elements
+  static constexpr int WE = 2;
+  __device__ static void unpack_w(word_t v, acc_t* x) {
+    x[0] = __uint_as_float(v << 16);
+    x[1] = __uint_as_float(v & 0xffff0000u);
+  }
+  __device__ static word_t pack_w(const acc_t* a) {
+    return (__float_as_uint(a[0]) >> 16) | (__float_as_uint(a[1]) & 0xffff0000u);
   }
 };
 
@@ -179,6 +203,13 @@ template <> struct Ops<DLA_F16> {
   __device__ static elem_t from_acc(acc_t a) { return static_cast<uint16_t>(f_to_half_bits(a)); }
   __device__ static acc_t zero_mul(acc_t x) { return x * 0.0f; }  // +-0 or NaN: already f16-exact
   __device__ static acc_t step(acc_t acc, w_t w, acc_t x) { return round_f16(acc + round_f16(w * x)); }
+  using word_t = uint32_t;  // 4 bytes = 2 elements
+  static constexpr int WE = 2;
+  __device__ static void unpack_w(word_t v, acc_t* x) {
+    x[0] = half_bits_to_f(v & 0xffffu);
+    x[1] = half_bits_to_f(v >> 16);
+  }
+  __device__ static word_t pack_w(const acc_t* a) { return f_to_half_bits(a[0]) | (f_to_half_bits(a[1]) << 16); }
 };
 
 // ------------------------------------------------------------ kernel arguments
@@ -188,8 +219,6 @@ struct PeerTable {
   const void* p[KMAX];
   W w[KMAX];
 };
-
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 template <bool NT>
 __device__ inline uint4 load16(const uint4* p) {
@@ -293,24 +322,62 @@ __device__ __attribute__((always_inline)) inline void fold_tile(
     if (live[c]) store16<SP>(out + idx[c], O::pack(acc[c]));
 }
 
-// Ragged tail (n_elems not a multiple of E): one element per lane, lanes < tail.
+// Ragged tail: elements first..n_elems-1, fewer than one chunk (at most 7), folded by the
+// first wave of the block.  The peers' values are gathered lane-parallel (lane l loads
+// peer k0+l: 64 loads in flight), transposed through LDS, and lane t folds element t over
+// the peers in list order.  A one-lane-per-element loop over the peers waits n_peers
+// memory latencies in sequence (12 of the 13 us of a 64-peer x 21 339-element f32 reduce);
+// broadcasting every value to every lane instead makes the fold a serial VALU chain of
+// n_peers x 7 steps (28 us for one bf16 tail element over 128 peers).
 template <int DT, bool ACC_IN>
 __device__ __attribute__((always_inline)) inline void fold_tail(
     const void* const* __restrict__ p, const typename Ops<DT>::w_t* __restrict__ w, int n_peers,
-    int64_t n_chunks, int64_t n_elems, void* __restrict__ out_v) {
+    int64_t first, int64_t n_elems, void* __restrict__ out_v) {
   using O = Ops<DT>;
   using acc_t = typename O::acc_t;
   using elem_t = typename O::elem_t;
-  const int64_t j = n_chunks * O::E + threadIdx.x;
-  if (j >= n_elems) return;
+  constexpr int kMaxTail = O::E - 1;  // a tail is shorter than one 16-byte chunk
+  __shared__ elem_t stage[kMaxTail][64];
+  const int n_tail = static_cast<int>(n_elems - first);
+  if (n_tail <= 0 || threadIdx.x >= 64) return;  // one wave: LDS order within a wave needs no barrier
+  const int lane = threadIdx.x;
+  const bool owner = lane < n_tail;                // lane t folds tail element t
   elem_t* o = static_cast<elem_t*>(out_v);
-  acc_t acc = ACC_IN ? O::to_acc(o[j]) : acc_t(0);
-  for (int k = 0; k < n_peers; ++k) {
-    const acc_t x = O::to_acc(static_cast<const elem_t*>(p[k])[j]);
-    if (!ACC_IN && k == 0) acc = O::zero_mul(x);
-    acc = O::step(acc, w[k], x);
+  const int64_t mine_j = first + (owner ? lane : 0);
+  acc_t acc = ACC_IN ? O::to_acc(o[mine_j]) : acc_t(0);
+  for (int k0 = 0; k0 < n_peers; k0 += 64) {
+    const int k = k0 + lane < n_peers ? k0 + lane : n_peers - 1;
+    const elem_t* src = static_cast<const elem_t*>(p[k]);
+    elem_t v[kMaxTail];
+#pragma unroll
+    for (int t = 0; t < kMaxTail; ++t) v[t] = src[first + (t < n_tail ? t : n_tail - 1)];
+#pragma unroll
+    for (int t = 0; t < kMaxTail; ++t) stage[t][lane] = v[t];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int m = n_peers - k0 < 64 ? n_peers - k0 : 64;
+    if (owner) {
+      const elem_t* row = stage[lane];
+      for (int l0 = 0; l0 < m; l0 += 8) {  // 8 LDS reads in flight, then 8 ordered steps
+        elem_t x[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) x[i] = row[l0 + i];  // all 64 slots are filled (clamped peers)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          if (l0 + i < m) {
+            const acc_t xi = O::to_acc(x[i]);
+            if (!ACC_IN && k0 + l0 + i == 0) acc = O::zero_mul(xi);  // fedavg.py:22
+            acc = O::step(acc, w[k0 + l0 + i], xi);                  // fedavg.py:25
+          }
+        }
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // reads done before the next block's writes
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
-  o[j] = O::from_acc(acc);
+  if (owner) o[mine_j] = O::from_acc(acc);
 }
 
 // ------------------------------------------------ register-stream kernel
@@ -322,10 +389,101 @@ __global__ __launch_bounds__(BS) void wsum_stream_kernel(
     int64_t n_elems, void* __restrict__ out_v) {
   const int64_t tile_chunks = static_cast<int64_t>(BS) * CH;
   const int64_t n_tiles = (n_chunks + tile_chunks - 1) / tile_chunks;
-  for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x)
+  // A ragged tail gets the grid's last workgroup to itself, so it overlaps the tiles.
+  const bool has_tail = n_elems > n_chunks * Ops<DT>::E;
+  const int64_t main_grid = static_cast<int64_t>(gridDim.x) - (has_tail ? 1 : 0);
+  if (has_tail && blockIdx.x == main_grid) {
+    fold_tail<DT, ACC_IN>(tab.p, tab.w, n_peers, n_chunks * Ops<DT>::E, n_elems, out_v);
+    return;
+  }
+  for (int64_t tile = blockIdx.x; tile < n_tiles; tile += main_grid)
     fold_tile<DT, BS, CH, NT, SP, ACC_IN>(tab.p, tab.w, n_peers, tile * tile_chunks, n_chunks,
                                           static_cast<uint4*>(out_v));
-  if (blockIdx.x == 0) fold_tail<DT, ACC_IN>(tab.p, tab.w, n_peers, n_chunks, n_elems, out_v);
+}
+
+// ------------------------------------------------ word-per-lane ("wide") kernel
+// For a small share reduced over many peers (configs[3]: 64 peers x 21 339 fp32 elements
+// per GPU) the 16-byte register stream has too few lanes to cover the memory latency:
+// 84 workgroups wait for 8 groups of 8 peers one after the other (13 us, 0.43 TB/s).
+// Here each lane owns one 4-byte word (8 for f64) and issues the loads of G peers at
+// once before folding them in list order, so a pass of up to G peers costs about one
+// memory latency, with 4x the lanes of the 16-byte stream.  Same fold as fold_tile.
+template <typename W>
+__device__ inline W load_word_nt(const W* p) {
+  return __builtin_nontemporal_load(p);  // global_load_dword[x2] ... nt
+}
+__device__ inline void store_word_sc1(uint32_t* p, uint32_t v) {
+  asm volatile("global_store_dword %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+}
+__device__ inline void store_word_sc1(u32x2* p, u32x2 v) {
+  asm volatile("global_store_dwordx2 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+}
+
+// Fold G loaded words in list order.  FULL (every slot a live peer): no per-peer
+// conditions, so the weights load as one batch; otherwise peers g >= m are skipped.
+template <int DT, int G, bool FULL, bool ACC_IN>
+__device__ __attribute__((always_inline)) inline void fold_words(
+    const typename Ops<DT>::word_t (&v)[G], const typename Ops<DT>::w_t* __restrict__ w, int m, bool first_round,
+    typename Ops<DT>::acc_t (&acc)[Ops<DT>::WE]) {
+  using O = Ops<DT>;
+  using acc_t = typename O::acc_t;
+  typename O::w_t wk[G];
+#pragma unroll
+  for (int g = 0; g < G; ++g) wk[g] = w[g];
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    if (FULL || g < m) {
+      acc_t x[O::WE];
+      O::unpack_w(v[g], x);
+#pragma unroll
+      for (int e = 0; e < O::WE; ++e) {
+        if (!ACC_IN && g == 0 && first_round) acc[e] = O::zero_mul(x[e]);  // fedavg.py:22
+        acc[e] = O::step(acc[e], wk[g], x[e]);                              // fedavg.py:25
+      }
+    }
+  }
+}
+
+template <int DT, int KMAX, int G, bool ACC_IN>
+__global__ __launch_bounds__(64) void wsum_wide_kernel(
+    const PeerTable<typename Ops<DT>::w_t, KMAX> tab, int n_peers, int64_t n_words,
+    int64_t n_elems, void* __restrict__ out_v) {
+  using O = Ops<DT>;
+  using acc_t = typename O::acc_t;
+  using word_t = typename O::word_t;
+  constexpr int WE = O::WE;
+  const int64_t main_grid = (n_words + 63) / 64;
+  if (blockIdx.x >= main_grid) {  // the ragged-tail workgroup (at most WE - 1 elements)
+    fold_tail<DT, ACC_IN>(tab.p, tab.w, n_peers, n_words * WE, n_elems, out_v);
+    return;
+  }
+  {
+    const int64_t j = static_cast<int64_t>(blockIdx.x) * 64 + threadIdx.x;
+    const bool live = j < n_words;
+    const int64_t i = live ? j : n_words - 1;  // clamped: loads stay unpredicated
+    word_t* out = static_cast<word_t*>(out_v);
+    acc_t acc[WE];
+    if constexpr (ACC_IN) O::unpack_w(out[i], acc);
+    // Rounds unrolled: every table index is a compile-time constant, so the pointers and
+    // weights arrive in batched s_load_dwordx16 reads instead of one scalar load and wait
+    // per peer (which cost ~5 us per 64-peer round before).
+#pragma unroll
+    for (int r = 0; r < (KMAX + G - 1) / G; ++r) {
+      const int k0 = r * G;
+      if (k0 >= n_peers) break;
+      word_t v[G];
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        const int k = k0 + g < n_peers ? k0 + g : n_peers - 1;
+        v[g] = load_word_nt(static_cast<const word_t*>(tab.p[k]) + i);
+      }
+      if (k0 + G <= n_peers)
+        fold_words<DT, G, true, ACC_IN>(v, tab.w + k0, G, k0 == 0, acc);
+      else
+        fold_words<DT, G, false, ACC_IN>(v, tab.w + k0, n_peers - k0, k0 == 0, acc);
+    }
+    if (live) store_word_sc1(out + i, O::pack_w(acc));
+  }
 }
 
 // ------------------------------------------------ multi-tensor kernel
@@ -354,7 +512,7 @@ __global__ __launch_bounds__(kBlock) void wsum_multi_kernel(
   if (tile * kBlock < n_chunks)
     fold_tile<DT, kBlock, 1, true, SP, false>(tab.p[s], tab.w, n_peers, tile * kBlock, n_chunks,
                                       static_cast<uint4*>(tab.out[s]));
-  if (tile == 0) fold_tail<DT, false>(tab.p[s], tab.w, n_peers, n_chunks, n_elems, tab.out[s]);
+  if (tile == 0) fold_tail<DT, false>(tab.p[s], tab.w, n_peers, n_chunks * Ops<DT>::E, n_elems, tab.out[s]);
 }
 
 // ------------------------------------------------ teacher-logit mean (§8 f4)
@@ -450,7 +608,8 @@ __global__ __launch_bounds__(kBlock) void wsum_scalar_kernel(
 // ------------------------------------------------------------------ launching
 
 struct Launch {
-  int variant;      // 1 plain/plain, 2 nt/plain, 4 nt/sc1 (load/store cache policy)
+  int variant;      // 1 plain/plain, 2 nt/plain, 4 nt/sc1 (load/store cache policy); 8 wide kernel
+  bool auto_kernel; // variant not forced: the wide kernel may be picked by shape (use_wide)
   int block;        // 64 or 256 threads; 0 = pick (shape_for)
   int chunks;       // 1, 2, 4; 0 = pick (shape_for)
   int grid_blocks;  // 0 = one workgroup per tile
@@ -474,11 +633,28 @@ void shape_for(int64_t n_chunks, int n_peers, int elems_per_chunk, int* block, i
   *chunks = 1;
 }
 
+// The wide kernel (one word per lane, up to 64 peers in flight) is picked for
+//  * small shares over more than 8 peers, where the 16-byte stream leaves the chip mostly idle
+//    while each lane waits group after group (64 x 21 339 fp32, configs[3]: 12.8 -> 5.1 us;
+//    128 x 85 354 fp32: 29.3 -> 9.2 us);
+//  * 16-bit dtypes over more than 32 peers at any size (128 x 2 662 045 bf16, configs[4]'s
+//    per-GPU share: 115.1 -> 111.4 us; 128 x 665 511 bf16: 35.4 -> 32.3 us).
+// f32 shares of >= 128 K chunks keep the stream (32 x 1 690 046: 34.5 vs 35.8 us; 64 x 1 233 086:
+// 48.2 vs 52.4 us).  Interleaved A/B on MI355X: profiles/r01_ab_wide*.log.
+constexpr int64_t kWideMaxChunks = 64 * 1024;
+bool use_wide(int64_t n_chunks, int n_peers, int elems_per_chunk) {
+  if (n_peers <= kGroup) return false;
+  return n_chunks < kWideMaxChunks || (elems_per_chunk == 8 && n_peers > 32);
+}
+
 Launch resolve(const dla_launch_cfg_t* cfg) {
   // default: nt loads + sc1 stores (+3.5 % over plain stores on every box measured)
-  Launch l{4, 0, 0, 0};
+  Launch l{4, true, 0, 0, 0};
   if (cfg) {
-    if (cfg->variant) l.variant = cfg->variant;
+    if (cfg->variant) {
+      l.variant = cfg->variant;
+      l.auto_kernel = false;
+    }
     l.block = cfg->block;
     l.chunks = cfg->chunks;
     l.grid_blocks = cfg->grid_blocks;
@@ -492,11 +668,11 @@ hipError_t launch_stream(const PeerTable<typename Ops<DT>::w_t, KMAX>& tab, int 
   constexpr int E = Ops<DT>::E;
   const int64_t n_chunks = n_elems / E;
   const int64_t tile_chunks = static_cast<int64_t>(BS) * CH;
-  int64_t tiles = (n_chunks + tile_chunks - 1) / tile_chunks;
-  if (tiles < 1) tiles = 1;  // block 0 still handles the ragged tail
+  const int64_t tiles = (n_chunks + tile_chunks - 1) / tile_chunks;
   int64_t grid = grid_blocks > 0 ? grid_blocks : tiles;
   if (grid > tiles) grid = tiles;
-  if (grid > 0x7fffffff) grid = 0x7fffffff;
+  if (grid > 0x7ffffffe) grid = 0x7ffffffe;
+  if (n_elems > n_chunks * E) ++grid;  // + the ragged-tail workgroup
   hipLaunchKernelGGL((wsum_stream_kernel<DT, KMAX, BS, CH, NT, SP, ACC_IN>), dim3(static_cast<unsigned>(grid)),
                      dim3(BS), 0, s, tab, n, n_chunks, n_elems, out);
   return hipGetLastError();
@@ -524,6 +700,21 @@ hipError_t launch_chunks(const PeerTable<typename Ops<DT>::w_t, KMAX>& tab, int 
 }
 
 template <int DT, int KMAX, bool ACC_IN>
+hipError_t launch_wide(const PeerTable<typename Ops<DT>::w_t, KMAX>& tab, int n, int64_t n_elems, void* out,
+                       hipStream_t s) {
+  // peers in flight per lane: every peer of the pass up to 64 words (f64: 32 double words)
+  constexpr int kWordCap = sizeof(typename Ops<DT>::word_t) == 8 ? 32 : 64;
+  constexpr int G = KMAX < kWordCap ? KMAX : kWordCap;
+  const int64_t n_words = n_elems / Ops<DT>::WE;
+  int64_t grid = (n_words + 63) / 64;
+  if (n_elems > n_words * Ops<DT>::WE) ++grid;  // + the ragged-tail workgroup
+  if (grid > 0x7fffffff) return hipErrorInvalidValue;
+  hipLaunchKernelGGL((wsum_wide_kernel<DT, KMAX, G, ACC_IN>), dim3(static_cast<unsigned>(grid)), dim3(64), 0, s,
+                     tab, n, n_words, n_elems, out);
+  return hipGetLastError();
+}
+
+template <int DT, int KMAX, bool ACC_IN>
 hipError_t launch_pass(const PeerTable<typename Ops<DT>::w_t, KMAX>& tab, int n, int64_t n_elems,
                        void* out, hipStream_t s, const Launch& l, bool aligned) {
   if (!aligned) {
@@ -534,6 +725,8 @@ hipError_t launch_pass(const PeerTable<typename Ops<DT>::w_t, KMAX>& tab, int n,
                        dim3(kBlock), 0, s, tab, n, n_elems, out);
     return hipGetLastError();
   }
+  if (l.variant == 8 || (l.auto_kernel && use_wide(n_elems / Ops<DT>::E, n, Ops<DT>::E)))
+    return launch_wide<DT, KMAX, ACC_IN>(tab, n, n_elems, out, s);
   int block = l.block, chunks = l.chunks;
   if (!block || !chunks) {
     int b, c;
@@ -695,8 +888,8 @@ int wsum_impl(int dtype, const void* const* peers, const double* weights, int n_
                                      std::to_string(kMaxPeersPerPass));
   }
   const Launch l = resolve(cfg);
-  if (l.variant != 1 && l.variant != 2 && l.variant != 4)
-    return fail(DLA_E_CONFIG, "dla_wsum: unsupported variant " + std::to_string(l.variant) + " (1, 2 or 4)");
+  if (l.variant != 1 && l.variant != 2 && l.variant != 4 && l.variant != 8)
+    return fail(DLA_E_CONFIG, "dla_wsum: unsupported variant " + std::to_string(l.variant) + " (1, 2, 4 or 8)");
   if (l.chunks != 0 && l.chunks != 1 && l.chunks != 2 && l.chunks != 4)
     return fail(DLA_E_CONFIG, "dla_wsum: chunks must be 0 (auto), 1, 2 or 4");
   if (l.block != 0 && l.block != 64 && l.block != 256)

@@ -58,9 +58,13 @@ extern "C" {
 
 /* Launch tuning knobs for dla_wsum_ex (0 = library default for each field). */
 typedef struct dla_launch_cfg {
-  int variant;      /* 0 = default (4); cache policy of the register stream:
+  int variant;      /* 0 = by shape: 4, or 8 for a small share over more than 8 peers
+                       (and 16-bit dtypes over more than 32 peers);
+                       cache policy of the 16-byte register stream:
                        1 = plain loads / plain stores   2 = nt loads / plain stores
-                       4 = nt loads / sc1 stores (write-through, line not kept in L2)    */
+                       4 = nt loads / sc1 stores (write-through, line not kept in L2)
+                       8 = word-per-lane kernel (nt loads, sc1 stores, up to 64 peers
+                           in flight per lane; chunks/block/grid are ignored)            */
   int chunks;       /* 16-byte chunks per lane per peer per tile: 1, 2, 4; 0 = by shape  */
   int grid_blocks;  /* workgroups; 0 = one per work tile (no grid-stride loop)           */
   int block;        /* threads per workgroup: 64 or 256; 0 = by shape                    */

@@ -120,7 +120,7 @@ def _bits(t, dtype):
 
 
 LAUNCH_CFGS = [(v, c, g, b) for v in (1, 2, 4) for c in (1, 2, 4) for b in (64, 256) for g in (0,)] + [
-    (4, 1, 512, 64), (2, 2, 300, 256), (4, 4, 1000, 256), (0, 0, 0, 0)]
+    (4, 1, 512, 64), (2, 2, 300, 256), (4, 4, 1000, 256), (0, 0, 0, 0), (8, 0, 0, 0)]
 
 
 @pytest.mark.parametrize("dtype", ["f32", "bf16", "f16", "f64"])
@@ -138,6 +138,29 @@ def test_every_launch_variant_is_bit_exact(dtype):
         out = wsum.wsum(dev, w, cfg=cfg)
         torch.cuda.synchronize()
         assert same_bits(_bits(out, dtype), want, dtype), (dtype, variant, chunks, grid, block)
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16", "f16", "f64"])
+@pytest.mark.parametrize("n", [1, 9, 33, 64, 129, 200])
+@pytest.mark.parametrize("numel", [1, 2, 63, 21_339, 100_007])
+def test_wide_kernel_bit_exact(dtype, n, numel):
+    """Word-per-lane kernel (variant 8; auto-picked for small shares over > 8 peers) and the
+    16-byte stream's lane-parallel ragged tail (up to 7 tail elements for 16-bit dtypes),
+    every dtype, single and multi-pass peer counts."""
+    from accdfl_amd import _lib
+    from accdfl_amd.core import wsum
+
+    peers = _random_peers(n, numel, dtype, seed=n * 7 + numel)
+    specials = [-0.0, float("inf"), float("-inf"), float("nan"), 1e-40, -3e38]
+    for i, v in enumerate(specials):  # IEEE specials spread over peers and lanes
+        peers[(3 * i) % n][(11 * i) % numel] = v
+    w = [float(x) for x in np.random.default_rng(n).dirichlet(np.ones(n))]
+    want = c_wsum([_bits(p, dtype) for p in peers], w, dtype)
+    dev = [p.cuda() for p in peers]
+    for cfg in (_lib.LaunchCfg(8, 0, 0, 0), None, _lib.LaunchCfg(4, 1, 0, 64), _lib.LaunchCfg(4, 4, 0, 256)):
+        out = wsum.wsum(dev, w, cfg=cfg)
+        torch.cuda.synchronize()
+        assert same_bits(_bits(out, dtype), want, dtype), (dtype, n, numel, cfg)
 
 
 @pytest.mark.parametrize("n", [1, 2, 3, 7, 8, 9, 16, 31, 32, 33, 64, 127, 128, 129, 257])
