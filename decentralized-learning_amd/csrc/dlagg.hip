@@ -19,10 +19,14 @@
 // peers loaded in groups of 8 so each lane keeps 8*CH*16 B in flight before the
 // first add.  Loads are non-temporal (each byte is read once); the output is
 // stored sc1 (write-through, not kept in the XCD L2), which measured +3.5 % over
-// plain stores on the 8 x 25 M fp32 north-star reduce (profiles/r01_*).  No LDS:
-// each lane folds only its own elements, so there is no cross-lane exchange to
-// stage, and LDS-DMA staging buys nothing for a pure stream at this occupancy
-// (the register stream already keeps >300 KiB in flight per CU).
+// plain stores on the 8 x 25 M fp32 north-star reduce (profiles/r01_*).  No LDS in
+// the stream: each lane folds only its own elements, so there is no cross-lane
+// exchange to stage, and LDS-DMA staging buys nothing for a pure stream at this
+// occupancy (the register stream already keeps >300 KiB in flight per CU).  LDS is
+// used only to transpose the peers' values of a ragged tail (< one chunk), which
+// one wave gathers lane-parallel in its own workgroup.
+// Small shares over many peers take a word-per-lane kernel (wsum_wide_kernel) that
+// keeps up to 64 peers' loads in flight per lane.
 //
 // Compiled with -ffp-contract=off; the pragma below repeats it so no build line
 // can re-enable FMA contraction for these functions.
@@ -382,7 +386,7 @@ __device__ __attribute__((always_inline)) inline void fold_tail(
 
 // ------------------------------------------------ register-stream kernel
 // One flat buffer per peer; tiles dealt to workgroups (grid-stride when the grid
-// is smaller than the tile count); block 0 also folds the ragged tail.
+// is smaller than the tile count); one extra workgroup folds the ragged tail.
 template <int DT, int KMAX, int BS, int CH, bool NT, int SP, bool ACC_IN>
 __global__ __launch_bounds__(BS) void wsum_stream_kernel(
     const PeerTable<typename Ops<DT>::w_t, KMAX> tab, int n_peers, int64_t n_chunks,
@@ -402,12 +406,12 @@ __global__ __launch_bounds__(BS) void wsum_stream_kernel(
 }
 
 // ------------------------------------------------ word-per-lane ("wide") kernel
-// For a small share reduced over many peers (configs[3]: 64 peers x 21 339 fp32 elements
-// per GPU) the 16-byte register stream has too few lanes to cover the memory latency:
-// 84 workgroups wait for 8 groups of 8 peers one after the other (13 us, 0.43 TB/s).
-// Here each lane owns one 4-byte word (8 for f64) and issues the loads of G peers at
-// once before folding them in list order, so a pass of up to G peers costs about one
-// memory latency, with 4x the lanes of the 16-byte stream.  Same fold as fold_tile.
+// For a small share reduced over many peers the 16-byte register stream has too few lanes
+// to cover the memory latency: each lane waits for its groups of 8 peers one after the
+// other (128 peers x 85 354 fp32: 16 waits per lane, 24 us; 9 us here).  Here each lane owns
+// one 4-byte word (8 for f64) and issues the loads of G peers at once before folding them
+// in list order, so a pass of up to G peers costs about one memory latency, with 4x the
+// lanes of the 16-byte stream.  Same fold as fold_tile.
 template <typename W>
 __device__ inline W load_word_nt(const W* p) {
   return __builtin_nontemporal_load(p);  // global_load_dword[x2] ... nt
