@@ -12,7 +12,7 @@ Algorithmic bytes per step per rank = (N + 1) * P * 4 (N peer reads + 1 output w
 value = sum over ranks of bytes / max-over-ranks step time.
 
 Extra objects on the JSON line:
-  roofline      dominant kernel (wsum_stream_kernel): achieved GB/s from HIP events on
+  roofline      dominant kernel (the one dla_select_kernel names): achieved GB/s from HIP events on
                 the launch stream over the timed region vs 8 TB/s HBM peak; traffic =
                 PMC HBM bytes per launch from profiles/ (null if not collected)
   cpu_baseline  the reference's torch-CPU op sequence (oracle/fedavg_oracle.py, kind
@@ -768,7 +768,7 @@ def main():
         },
         "roofline": {
             "bound": "hbm",
-            "kernel": "wsum_stream_kernel",
+            "kernel": _lib.select_kernel(code, n, p) if cfg is None else "wsum_stream_kernel (forced launch cfg)",
             "achieved": round(achieved, 1),
             "peak": HBM_PEAK_GBPS,
             "unit": "GB/s",

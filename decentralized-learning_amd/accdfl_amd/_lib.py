@@ -21,7 +21,7 @@ LIB_PATH = os.environ.get("DLAGG_LIB", os.path.join(PKG_ROOT, "lib", "libdlagg.s
 
 # dtype codes (include/dlagg.h)
 DLA_F32, DLA_BF16, DLA_F16, DLA_F64 = 0, 1, 2, 3
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 HIPCC_FLAGS = [
     "--offload-arch=gfx950",
@@ -37,6 +37,7 @@ EXPORTED = (
     "dla_version",
     "dla_last_error",
     "dla_max_peers_per_pass",
+    "dla_select_kernel",
     "dla_wsum",
     "dla_wsum_ex",
     "dla_wsum_slab",
@@ -98,6 +99,8 @@ class _Lib:
         so.dla_version.restype = ctypes.c_int
         so.dla_last_error.restype = ctypes.c_char_p
         so.dla_max_peers_per_pass.restype = ctypes.c_int
+        so.dla_select_kernel.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int64]
+        so.dla_select_kernel.restype = ctypes.c_char_p
         so.dla_wsum.argtypes = [ctypes.c_int, ctypes.POINTER(vp), ctypes.POINTER(ctypes.c_double), ctypes.c_int,
                                 ctypes.c_int64, vp, vp]
         so.dla_wsum.restype = ctypes.c_int
@@ -186,6 +189,11 @@ def wsum_ptrs(dtype_code: int, peer_ptrs: Sequence[int], weights: Sequence[float
         rc = L.so.dla_wsum_ex(dtype_code, _ptr_array(peer_ptrs), _dbl_array(weights), n, n_elems, out_ptr,
                               stream_ptr, ctypes.byref(cfg))
     L.check(rc, "dla_wsum")
+
+
+def select_kernel(dtype_code: int, n_peers: int, n_elems: int) -> str:
+    """dla_select_kernel: the kernel family a default dla_wsum launch uses for this shape."""
+    return lib().so.dla_select_kernel(dtype_code, n_peers, n_elems).decode()
 
 
 def mean_ptrs(dtype_code: int, peer_ptrs: Sequence[int], n_elems: int, out_ptr: int, stream_ptr: int) -> None:

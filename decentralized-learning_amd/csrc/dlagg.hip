@@ -243,9 +243,11 @@ __device__ inline void store16(uint4* p, const uint4& v) {
   if constexpr (SP == 1) {
     __builtin_nontemporal_store(w, reinterpret_cast<u32x4*>(p));  // global_store_dwordx4 ... nt
   } else if constexpr (SP == 2) {
-    asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(w) : "memory");
+    // s_nop 1 inside the string: a store of more than 8 bytes reads its data VGPRs after
+    // issue, and hipcc does not pad an asm store, so its next VALU could overwrite them.
+    asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(w) : "memory");
   } else if constexpr (SP == 3) {
-    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(p), "v"(w) : "memory");
+    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1\n\ts_nop 1" ::"v"(p), "v"(w) : "memory");
   } else {
     *reinterpret_cast<u32x4*>(p) = w;
   }
@@ -403,6 +405,93 @@ __global__ __launch_bounds__(BS) void wsum_stream_kernel(
   for (int64_t tile = blockIdx.x; tile < n_tiles; tile += main_grid)
     fold_tile<DT, BS, CH, NT, SP, ACC_IN>(tab.p, tab.w, n_peers, tile * tile_chunks, n_chunks,
                                           static_cast<uint4*>(out_v));
+}
+
+// ------------------------------------------------ peer-major big-tile kernel
+// The north-star shape (<= 8 peers, large P): one wave owns a "big tile" of 64 * BT
+// contiguous 16-byte chunks (16 KiB of output at BT = 16).  It streams peer 0's 16 KiB,
+// then peer 1's, ... (the loads of peer k+1 are in flight while peer k is folded, and the
+// other waves of the CU cover the rest), then writes its 16 KiB.  Per element the fold is
+// the same list-order sequence as fold_tile.  Measured on MI355X (profiles/phase_probe.py):
+// 8 x 25 M fp32 133.2 us against 138.2 us for the 1-chunk-per-lane stream; BT = 8 gives
+// 141.9 us, BT = 24 / 32 lose occupancy (164.8 / 185.6 us).  The pattern's own ceiling on
+// the same box: 8-stream read alone 116.4-117.5 us + the 100 MB sc1 write alone 14.8 us.
+template <int DT, int NP, int BT>
+__device__ __attribute__((always_inline)) inline void fold_big_tile(
+    const void* const* __restrict__ p, const typename Ops<DT>::w_t* __restrict__ w, int64_t base,
+    int64_t n_chunks, uint4* __restrict__ out) {
+  using O = Ops<DT>;
+  using acc_t = typename O::acc_t;
+  constexpr int E = O::E;
+  // chunk c of this lane: base + c * 64 (full tiles only: one base plus immediate offsets)
+  auto at = [&](int c) -> int64_t { return base + c * 64; };
+  // pointers and weights into registers first: the compiler barrier below must not force
+  // them to be re-read from the kernel-argument segment
+  const u32x4* src[NP];
+  typename O::w_t wv[NP];
+#pragma unroll
+  for (int k = 0; k < NP; ++k) {
+    src[k] = static_cast<const u32x4*>(p[k]);
+    wv[k] = w[k];
+  }
+  acc_t acc[BT][E];
+  u32x4 a[BT], b[BT];
+#pragma unroll
+  for (int c = 0; c < BT; ++c) a[c] = __builtin_nontemporal_load(src[0] + at(c));
+#pragma unroll
+  for (int k = 0; k < NP; ++k) {
+    if (k + 1 < NP) {
+#pragma unroll
+      for (int c = 0; c < BT; ++c) b[c] = __builtin_nontemporal_load(src[k + 1] + at(c));
+    }
+    asm volatile("" ::: "memory");  // peer k+2's loads stay below peer k's fold: two buffers
+    const typename O::w_t wk = wv[k];
+#pragma unroll
+    for (int c = 0; c < BT; ++c) {
+      acc_t x[E];
+      O::unpack(make_uint4(a[c].x, a[c].y, a[c].z, a[c].w), x);
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        if (k == 0) acc[c][e] = O::zero_mul(x[e]);  // fedavg.py:22
+        acc[c][e] = O::step(acc[c][e], wk, x[e]);   // fedavg.py:25
+      }
+    }
+    if (k + 1 < NP) {
+#pragma unroll
+      for (int c = 0; c < BT; ++c) a[c] = b[c];
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < BT; ++c)
+    store16<2>(out + at(c), O::pack(acc[c]));
+}
+
+// NP: the exact peer count (1..8), so the peer loop is fully static.  Workgroups
+// [0, n_full) fold the full big tiles; then one workgroup folds the partial last tile (as
+// 64-chunk stream tiles) and one the ragged tail, when there are any.
+template <int DT, int NP, int BT>
+__global__ __launch_bounds__(64) void wsum_bigtile_kernel(const PeerTable<typename Ops<DT>::w_t, 8> tab,
+                                                          int64_t n_chunks, int64_t n_elems,
+                                                          void* __restrict__ out_v) {
+  constexpr int64_t kTile = 64 * BT;
+  const int64_t n_full = n_chunks / kTile;
+  const int64_t b = blockIdx.x;
+  uint4* out = static_cast<uint4*>(out_v);
+  if (b < n_full) {
+    // Written as a grid-stride loop although it runs once per workgroup: inside a loop hipcc
+    // keeps the two-buffer schedule (peer k+1's 16 loads in flight while peer k folds, ~16-20
+    // loads outstanding, <= 256 VGPRs); as straight-line code it waits for every load before
+    // each fold and spills the peers' data into AGPRs.
+    for (int64_t t = b; t < n_full; t += gridDim.x)
+      fold_big_tile<DT, NP, BT>(tab.p, tab.w, t * kTile + threadIdx.x, n_chunks, out);
+    return;
+  }
+  if (b == n_full && n_full * kTile < n_chunks) {  // the partial last tile
+    for (int64_t t0 = n_full * kTile; t0 < n_chunks; t0 += 64)
+      fold_tile<DT, 64, 1, true, 2, false>(tab.p, tab.w, NP, t0, n_chunks, out);
+    return;
+  }
+  fold_tail<DT, false>(tab.p, tab.w, NP, n_chunks * Ops<DT>::E, n_elems, out_v);  // no-op without a tail
 }
 
 // ------------------------------------------------ word-per-lane ("wide") kernel
@@ -651,6 +740,20 @@ bool use_wide(int64_t n_chunks, int n_peers, int elems_per_chunk) {
   return n_chunks < kWideMaxChunks || (elems_per_chunk == 8 && n_peers > 32);
 }
 
+// The peer-major big-tile kernel (16 KiB of output per wave) where it beats the 64 x 1
+// stream in interleaved A/B on MI355X (profiles/r01_ab_bigtile*.log):
+//  * fp32, exactly 8 peers, >= 1 M chunks: 8 x 25 M 134.7 vs 137.9 us (rocprofv3: 133.2 us),
+//    8 x 12.5 M 66.3 vs 69.0, 8 x 4 M 21.7 vs 24.3; with 7, 6, 5 or 3 peers the stream wins
+//    by 2-8 % (7 x 25 M 119.6 vs 116.6), and below 1 M chunks the MALL-resident sizes flip;
+//  * fp64, >= 4 peers, >= 512 K chunks: 8 x 12.5 M 134.7 vs 162.1, 4 x 12.5 M 77.3 vs 86.4,
+//    8 x 1 M 10.6 vs 13.0 (2 peers tie, 1 peer loses).
+constexpr int kBigTileChunks = 16;
+bool use_bigtile(int64_t n_chunks, int elems_per_chunk, int n_peers) {
+  if (elems_per_chunk == 4) return n_peers == 8 && n_chunks >= (int64_t{1} << 20);
+  if (elems_per_chunk == 2) return n_peers >= 4 && n_chunks >= (int64_t{1} << 19);
+  return false;
+}
+
 Launch resolve(const dla_launch_cfg_t* cfg) {
   // default: nt loads + sc1 stores (+3.5 % over plain stores on every box measured)
   Launch l{4, true, 0, 0, 0};
@@ -718,6 +821,33 @@ hipError_t launch_wide(const PeerTable<typename Ops<DT>::w_t, KMAX>& tab, int n,
   return hipGetLastError();
 }
 
+template <int DT>
+hipError_t launch_bigtile(const PeerTable<typename Ops<DT>::w_t, 8>& tab, int n, int64_t n_elems, void* out,
+                          hipStream_t s) {
+  constexpr int BT = kBigTileChunks;
+  const int64_t n_chunks = n_elems / Ops<DT>::E;
+  int64_t grid = n_chunks / (64 * BT);
+  if (grid * 64 * BT < n_chunks) ++grid;        // + the partial-tile workgroup
+  if (n_elems > n_chunks * Ops<DT>::E) ++grid;  // + the ragged-tail workgroup
+  if (grid < 1 || grid > 0x7fffffff) return hipErrorInvalidValue;
+  const dim3 g(static_cast<unsigned>(grid)), b(64);
+#define DLA_BIGTILE(NPV) \
+  hipLaunchKernelGGL((wsum_bigtile_kernel<DT, NPV, BT>), g, b, 0, s, tab, n_chunks, n_elems, out)
+  switch (n) {
+    case 1: DLA_BIGTILE(1); break;
+    case 2: DLA_BIGTILE(2); break;
+    case 3: DLA_BIGTILE(3); break;
+    case 4: DLA_BIGTILE(4); break;
+    case 5: DLA_BIGTILE(5); break;
+    case 6: DLA_BIGTILE(6); break;
+    case 7: DLA_BIGTILE(7); break;
+    case 8: DLA_BIGTILE(8); break;
+    default: return hipErrorInvalidValue;
+  }
+#undef DLA_BIGTILE
+  return hipGetLastError();
+}
+
 template <int DT, int KMAX, bool ACC_IN>
 hipError_t launch_pass(const PeerTable<typename Ops<DT>::w_t, KMAX>& tab, int n, int64_t n_elems,
                        void* out, hipStream_t s, const Launch& l, bool aligned) {
@@ -731,6 +861,10 @@ hipError_t launch_pass(const PeerTable<typename Ops<DT>::w_t, KMAX>& tab, int n,
   }
   if (l.variant == 8 || (l.auto_kernel && use_wide(n_elems / Ops<DT>::E, n, Ops<DT>::E)))
     return launch_wide<DT, KMAX, ACC_IN>(tab, n, n_elems, out, s);
+  if constexpr (KMAX == 8 && !ACC_IN && (DT == DLA_F32 || DT == DLA_F64)) {
+    if (l.variant == 16 || (l.auto_kernel && use_bigtile(n_elems / Ops<DT>::E, Ops<DT>::E, n)))
+      return launch_bigtile<DT>(tab, n, n_elems, out, s);
+  }
   int block = l.block, chunks = l.chunks;
   if (!block || !chunks) {
     int b, c;
@@ -892,8 +1026,8 @@ int wsum_impl(int dtype, const void* const* peers, const double* weights, int n_
                                      std::to_string(kMaxPeersPerPass));
   }
   const Launch l = resolve(cfg);
-  if (l.variant != 1 && l.variant != 2 && l.variant != 4 && l.variant != 8)
-    return fail(DLA_E_CONFIG, "dla_wsum: unsupported variant " + std::to_string(l.variant) + " (1, 2, 4 or 8)");
+  if (l.variant != 1 && l.variant != 2 && l.variant != 4 && l.variant != 8 && l.variant != 16)
+    return fail(DLA_E_CONFIG, "dla_wsum: unsupported variant " + std::to_string(l.variant) + " (1, 2, 4, 8 or 16)");
   if (l.chunks != 0 && l.chunks != 1 && l.chunks != 2 && l.chunks != 4)
     return fail(DLA_E_CONFIG, "dla_wsum: chunks must be 0 (auto), 1, 2 or 4");
   if (l.block != 0 && l.block != 64 && l.block != 256)
@@ -930,6 +1064,17 @@ int dla_version(void) { return DLA_ABI_VERSION; }
 const char* dla_last_error(void) { return g_last_error.c_str(); }
 
 int dla_max_peers_per_pass(void) { return kMaxPeersPerPass; }
+
+const char* dla_select_kernel(int dtype, int n_peers, int64_t n_elems) {
+  const int es = elem_size(dtype);
+  if (es == 0 || n_peers < 1 || n_elems < 0) return "";
+  const int e = 16 / es;  // elements per 16-byte chunk
+  const int first_pass = n_peers < kMaxPeersPerPass ? n_peers : kMaxPeersPerPass;
+  if (use_wide(n_elems / e, first_pass, e)) return "wsum_wide_kernel";
+  if (n_peers <= 8 && (dtype == DLA_F32 || dtype == DLA_F64) && use_bigtile(n_elems / e, e, n_peers))
+    return "wsum_bigtile_kernel";
+  return "wsum_stream_kernel";
+}
 
 int dla_wsum(int dtype, const void* const* peers, const double* weights, int n_peers, int64_t n_elems,
              void* out, void* stream) {

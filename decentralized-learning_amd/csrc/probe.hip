@@ -50,6 +50,77 @@ __global__ __launch_bounds__(256) void copy_kernel(const u32x4* __restrict__ src
   }
 }
 
+// Peer-major "big tile" FedAvg probe (f32, 8 peers): one wave owns 64*CH contiguous
+// chunks (CH*1 KiB of output); it streams peer 0's CH chunks, then peer 1's, ... (the loads
+// of peer k+1 are in flight while peer k is folded), then writes its CH chunks.  With a
+// persistent grid the chip reads in long phases and writes in short bursts, instead of
+// mixing 8 reads and 1 write at every tile.  Same per-element fold order as the product.
+template <int CH, int PF>
+__global__ __launch_bounds__(64) void bigtile_kernel(const u32x4* s0, const u32x4* s1, const u32x4* s2,
+                                                     const u32x4* s3, const u32x4* s4, const u32x4* s5,
+                                                     const u32x4* s6, const u32x4* s7, float w0, float w1,
+                                                     float w2, float w3, float w4, float w5, float w6, float w7,
+                                                     int64_t n_chunks, u32x4* __restrict__ dst) {
+  const u32x4* src[8] = {s0, s1, s2, s3, s4, s5, s6, s7};
+  const float w[8] = {w0, w1, w2, w3, w4, w5, w6, w7};
+  const int64_t n_big = n_chunks / (64 * CH);  // full big tiles only (the probe ignores the rest)
+  for (int64_t big = blockIdx.x; big < n_big; big += gridDim.x) {
+    const int64_t base = big * 64 * CH + threadIdx.x;
+    float acc[CH][4];
+    u32x4 a[CH], b[CH];
+#pragma unroll
+    for (int c = 0; c < CH; ++c) a[c] = __builtin_nontemporal_load(src[0] + base + c * 64);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      if (PF == 2 && k + 1 < 8) {
+#pragma unroll
+        for (int c = 0; c < CH; ++c) b[c] = __builtin_nontemporal_load(src[k + 1] + base + c * 64);
+      }
+      asm volatile("" ::: "memory");  // keep peer k+2's loads below peer k's fold (two buffers)
+#pragma unroll
+      for (int c = 0; c < CH; ++c) {
+        const float x[4] = {__uint_as_float(a[c].x), __uint_as_float(a[c].y), __uint_as_float(a[c].z),
+                            __uint_as_float(a[c].w)};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          if (k == 0) acc[c][e] = x[e] * 0.0f;
+          acc[c][e] = acc[c][e] + w[k] * x[e];
+        }
+      }
+      if constexpr (PF == 2) {
+#pragma unroll
+        for (int c = 0; c < CH; ++c) a[c] = b[c];
+      } else if (k + 1 < 8) {  // one buffer: the next peer's loads issue after this fold
+#pragma unroll
+        for (int c = 0; c < CH; ++c) a[c] = __builtin_nontemporal_load(src[k + 1] + base + c * 64);
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      const u32x4 v = {__float_as_uint(acc[c][0]), __float_as_uint(acc[c][1]), __float_as_uint(acc[c][2]),
+                       __float_as_uint(acc[c][3])};
+      asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(dst + base + c * 64), "v"(v) : "memory");
+    }
+  }
+}
+
+// Pure write stream: every lane stores CH 16-byte chunks of a constant (SC1: sc1 stores).
+template <int CH, bool SC1>
+__global__ __launch_bounds__(256) void write_kernel(u32x4* __restrict__ dst, int64_t n_chunks, uint32_t val) {
+  const int64_t base = static_cast<int64_t>(blockIdx.x) * 256 * CH + threadIdx.x;
+  const u32x4 v = {val, val ^ 1u, val ^ 2u, val ^ 3u};
+#pragma unroll
+  for (int c = 0; c < CH; ++c) {
+    const int64_t i = base + c * 256;
+    if (i < n_chunks) {
+      if constexpr (SC1)
+        asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(dst + i), "v"(v) : "memory");
+      else
+        dst[i] = v;
+    }
+  }
+}
+
 // The FedAvg access pattern without the arithmetic: each lane loads the same 16-byte
 // chunk offset from N_SRC separate buffers (all issued first), folds them, and
 // (WRITE) stores the fold to dst — isolates multi-stream reads vs the output write.
@@ -81,7 +152,7 @@ __global__ __launch_bounds__(256) void mread_kernel(const u32x4* const* __restri
     if constexpr (WRITE) {
       if (base + c * 256 < n_chunks) {
         if (sc1)
-          asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(dst + idx[c]), "v"(acc) : "memory");
+          asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(dst + idx[c]), "v"(acc) : "memory");
         else
           dst[idx[c]] = acc;
       }
@@ -128,7 +199,7 @@ __global__ __launch_bounds__(64) void tiled_kernel(const u32x4* __restrict__ src
 #pragma unroll
     for (int k = 1; k < NS; ++k) acc ^= v[k][c];
     u32x4* o = OUT_SLOT ? const_cast<u32x4*>(base) + NS * T + c * 64 + threadIdx.x : dst + tile * T + c * 64 + threadIdx.x;
-    asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(o), "v"(acc) : "memory");
+    asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(o), "v"(acc) : "memory");
   }
 }
 
@@ -164,7 +235,7 @@ __global__ __launch_bounds__(64) void policy_kernel(const u32x4* s0, const u32x4
   u32x4 acc = v[0];
 #pragma unroll
   for (int k = 1; k < 8; ++k) acc ^= v[k];
-  asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(dst + i), "v"(acc) : "memory");
+  asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(dst + i), "v"(acc) : "memory");
 }
 #undef DLP_LD
 
@@ -236,6 +307,49 @@ int dlp_copy(const void* src, void* dst, int64_t bytes, int nt, void* stream) {
   else
     hipLaunchKernelGGL((copy_kernel<4, false>), dim3(grid), dim3(256), 0, s, static_cast<const u32x4*>(src),
                        static_cast<u32x4*>(dst), n);
+  return static_cast<int>(hipGetLastError());
+}
+
+// bigtile_kernel over 8 peers of bytes_each; chunks in {4, 8, 16}; grid 0 = one WG per big tile.
+int dlp_bigtile8(const void* const* srcs, const float* w, int64_t bytes_each, void* dst, int chunks, int grid,
+                 void* stream) {
+  if (!srcs || !w || bytes_each < 16) return -1;
+  const int64_t n = bytes_each / 16;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const u32x4* p[8];
+  for (int k = 0; k < 8; ++k) p[k] = static_cast<const u32x4*>(srcs[k]);
+#define DLP_B(CHV, PFV)                                                                                     \
+  do {                                                                                                      \
+    const int64_t nb = n / (64 * CHV);                                                     \
+    const int64_t g = grid > 0 && grid < nb ? grid : nb;                                                    \
+    hipLaunchKernelGGL((bigtile_kernel<CHV, PFV>), dim3(g), dim3(64), 0, s, p[0], p[1], p[2], p[3], p[4], p[5],  \
+                       p[6], p[7], w[0], w[1], w[2], w[3], w[4], w[5], w[6], w[7], n,                       \
+                       static_cast<u32x4*>(dst));                                                           \
+  } while (0)
+  // chunks: 4, 8, 16, 24, 32 two peers in flight; 116, 124, 132 (100 + CH) one peer in flight
+  if (chunks == 4) DLP_B(4, 2);
+  else if (chunks == 8) DLP_B(8, 2);
+  else if (chunks == 16) DLP_B(16, 2);
+  else if (chunks == 24) DLP_B(24, 2);
+  else if (chunks == 32) DLP_B(32, 2);
+  else if (chunks == 116) DLP_B(16, 1);
+  else if (chunks == 124) DLP_B(24, 1);
+  else if (chunks == 132) DLP_B(32, 1);
+  else return -1;
+#undef DLP_B
+  return static_cast<int>(hipGetLastError());
+}
+
+// Write `bytes` (multiple of 16) of a constant; sc1 = 1 for sc1 stores.
+int dlp_write(void* dst, int64_t bytes, int sc1, void* stream) {
+  if (!dst || bytes < 16) return -1;
+  const int64_t n = bytes / 16;
+  const int64_t grid = (n + 1023) / 1024;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (sc1)
+    hipLaunchKernelGGL((write_kernel<4, true>), dim3(grid), dim3(256), 0, s, static_cast<u32x4*>(dst), n, 0x3f800000u);
+  else
+    hipLaunchKernelGGL((write_kernel<4, false>), dim3(grid), dim3(256), 0, s, static_cast<u32x4*>(dst), n, 0x3f800000u);
   return static_cast<int>(hipGetLastError());
 }
 

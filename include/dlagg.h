@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define DLA_ABI_VERSION 3
+#define DLA_ABI_VERSION 4
 
 /* element dtypes of the peer buffers and of the output */
 #define DLA_F32 0
@@ -58,13 +58,17 @@ extern "C" {
 
 /* Launch tuning knobs for dla_wsum_ex (0 = library default for each field). */
 typedef struct dla_launch_cfg {
-  int variant;      /* 0 = by shape: 4, or 8 for a small share over more than 8 peers
-                       (and 16-bit dtypes over more than 32 peers);
+  int variant;      /* 0 = by shape: 4; 8 for a small share over more than 8 peers
+                       (and 16-bit dtypes over more than 32 peers); 16 for large fp32
+                       shares over exactly 8 peers and fp64 over 4..8;
                        cache policy of the 16-byte register stream:
                        1 = plain loads / plain stores   2 = nt loads / plain stores
                        4 = nt loads / sc1 stores (write-through, line not kept in L2)
                        8 = word-per-lane kernel (nt loads, sc1 stores, up to 64 peers
-                           in flight per lane; chunks/block/grid are ignored)            */
+                           in flight per lane; chunks/block/grid are ignored)
+                      16 = peer-major big-tile kernel (fp32 / fp64, <= 8 peers: 16 KiB of
+                           output per wave, one peer's 16 KiB streamed at a time;
+                           chunks/block/grid are ignored; other dtypes take 4)         */
   int chunks;       /* 16-byte chunks per lane per peer per tile: 1, 2, 4; 0 = by shape  */
   int grid_blocks;  /* workgroups; 0 = one per work tile (no grid-stride loop)           */
   int block;        /* threads per workgroup: 64 or 256; 0 = by shape                    */
@@ -115,6 +119,12 @@ int dla_mean(int dtype, const void* const* peers, int n_peers, int64_t n_elems, 
 
 /* Largest peer count one kernel pass takes (kernel-argument pointer table). */
 int dla_max_peers_per_pass(void);
+
+/* Name of the kernel family dla_wsum picks (default launch, 16-byte aligned buffers) for
+ * this dtype, peer count and size: "wsum_bigtile_kernel", "wsum_wide_kernel" or
+ * "wsum_stream_kernel" (static string; "" for invalid arguments).  For profilers and
+ * benchmarks that must name the dominant kernel.  ABI v4. */
+const char* dla_select_kernel(int dtype, int n_peers, int64_t n_elems);
 
 /* Prepared reduce: validates and stores the peer/out pointers once, so a round
  * that reduces the same device buffers again (a PeerSlab every round, a benchmark

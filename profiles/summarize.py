@@ -34,21 +34,32 @@ if stats:
 # kernel with the largest total time (the same instantiation also serves the small
 # configs at other grid sizes, so the per-name stats file mixes them).
 kname, kgrid = None, None
+# the kernel the bench's headline launch used, as the bench line names it (dla_select_kernel)
+bench_kernel, bench_peers = KERNEL, 8
+trace_log = os.path.join(out_dir, "trace.log")
+if os.path.exists(trace_log):
+    for line in open(trace_log):
+        if line.startswith("{"):
+            try:
+                d = json.loads(line)
+                bench_kernel = d["roofline"]["kernel"].split()[0]
+                bench_peers = int(d["config"]["n_peers"])
+            except (ValueError, KeyError):
+                pass
+summary["bench_kernel"] = bench_kernel
 trace = find("*kernel_trace.csv")
 if trace:
     groups = {}
     for r in rows(trace):
-        if KERNEL not in r["Kernel_Name"]:
+        if bench_kernel + "<" not in r["Kernel_Name"]:
             continue
         key = (r["Kernel_Name"], r["Grid_Size_X"])
         groups.setdefault(key, []).append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
-    # the bench's north-star launch: f32 (Ops<0>), <= 8 peers (PeerTable<.., 8>), 64-thread
-    # workgroups x 1 chunk per lane (the default shape for f32), one workgroup per tile
-    n_peers_ = int(args[args.index("--peers") + 1]) if "--peers" in args else 8
-    params_ = int(args[args.index("--params") + 1]) if "--params" in args else 25_000_000
-    ns_grid = str(-(-(params_ // 4) // 64) * 64)
-    ns = {k: v for k, v in groups.items() if k[1] == ns_grid and k[0].split("wsum_stream_kernel<")[1].startswith(
-        "0, %d," % (8 if n_peers_ <= 8 else 32 if n_peers_ <= 32 else 128))}
+    # the bench's north-star launch: f32 (Ops<0>), its peer count (big-tile: template NP; stream /
+    # wide: the PeerTable size), the group with the most total time among those
+    kmax = 8 if bench_peers <= 8 else 32 if bench_peers <= 32 else 128
+    lead = "0, %d," % (bench_peers if bench_kernel == "wsum_bigtile_kernel" else kmax)
+    ns = {k: v for k, v in groups.items() if k[0].split(bench_kernel + "<")[1].startswith(lead)}
     groups = ns or groups
     if groups:
         (kname, kgrid), durs = max(groups.items(), key=lambda kv: sum(kv[1]))

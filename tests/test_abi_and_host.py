@@ -44,8 +44,19 @@ def test_library_version_and_argument_errors(lib_path):
     from accdfl_amd import _lib
 
     L = _lib.lib()
-    assert L.so.dla_version() == 3
+    assert L.so.dla_version() == 4
     assert L.max_peers_per_pass == 128
+    # kernel selection by shape (host-only query): north star, configs[3] share, configs[4] share,
+    # configs[2], GNLeNet 8 peers, fp64 north-star shape, few peers, invalid arguments
+    assert _lib.select_kernel(0, 8, 25_000_000) == "wsum_bigtile_kernel"
+    assert _lib.select_kernel(0, 64, 21_339) == "wsum_wide_kernel"
+    assert _lib.select_kernel(1, 128, 2_662_045) == "wsum_wide_kernel"
+    assert _lib.select_kernel(0, 32, 1_690_046) == "wsum_stream_kernel"
+    assert _lib.select_kernel(0, 8, 85_354) == "wsum_stream_kernel"
+    assert _lib.select_kernel(3, 8, 12_500_000) == "wsum_bigtile_kernel"
+    assert _lib.select_kernel(0, 4, 25_000_000) == "wsum_stream_kernel"
+    assert _lib.select_kernel(1, 8, 50_000_000) == "wsum_stream_kernel"
+    assert _lib.select_kernel(9, 8, 100) == "" and _lib.select_kernel(0, 0, 100) == ""
     # n_peers = 0 -> DLA_E_INVALID with a message
     rc = L.so.dla_wsum(0, None, None, 0, 10, None, None)
     assert rc == -1 and b"n_peers" in L.so.dla_last_error()

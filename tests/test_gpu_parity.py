@@ -120,7 +120,7 @@ def _bits(t, dtype):
 
 
 LAUNCH_CFGS = [(v, c, g, b) for v in (1, 2, 4) for c in (1, 2, 4) for b in (64, 256) for g in (0,)] + [
-    (4, 1, 512, 64), (2, 2, 300, 256), (4, 4, 1000, 256), (0, 0, 0, 0), (8, 0, 0, 0)]
+    (4, 1, 512, 64), (2, 2, 300, 256), (4, 4, 1000, 256), (0, 0, 0, 0), (8, 0, 0, 0), (16, 0, 0, 0)]
 
 
 @pytest.mark.parametrize("dtype", ["f32", "bf16", "f16", "f64"])
@@ -161,6 +161,28 @@ def test_wide_kernel_bit_exact(dtype, n, numel):
         out = wsum.wsum(dev, w, cfg=cfg)
         torch.cuda.synchronize()
         assert same_bits(_bits(out, dtype), want, dtype), (dtype, n, numel, cfg)
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16", "f16", "f64"])
+@pytest.mark.parametrize("n", [1, 2, 5, 8])
+@pytest.mark.parametrize("numel", [3, 4096 * 16, 4096 * 16 + 4, 4096 * 16 * 3 + 7, (1 << 20) + 1])
+def test_bigtile_kernel_bit_exact(dtype, n, numel):
+    """Peer-major big-tile kernel (variant 16; auto-picked for fp32 shares of >= 1 M chunks over
+    <= 8 peers): exact multiples of the 16 KiB tile, partial last tiles, shares smaller than one
+    tile, ragged tails, 1..8 peers, IEEE specials."""
+    from accdfl_amd import _lib
+    from accdfl_amd.core import wsum
+
+    peers = _random_peers(n, numel, dtype, seed=n * 13 + numel)
+    specials = [-0.0, float("inf"), float("-inf"), float("nan"), 1e-40, -3e38]
+    for i, v in enumerate(specials):
+        peers[(3 * i) % n][(4099 * i) % numel] = v
+    w = [float(x) for x in np.random.default_rng(n + 1).dirichlet(np.ones(n))]
+    want = c_wsum([_bits(p, dtype) for p in peers], w, dtype)
+    dev = [p.cuda() for p in peers]
+    out = wsum.wsum(dev, w, cfg=_lib.LaunchCfg(16, 0, 0, 0))
+    torch.cuda.synchronize()
+    assert same_bits(_bits(out, dtype), want, dtype), (dtype, n, numel)
 
 
 @pytest.mark.parametrize("n", [1, 2, 3, 7, 8, 9, 16, 31, 32, 33, 64, 127, 128, 129, 257])

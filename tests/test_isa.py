@@ -40,6 +40,19 @@ def test_every_dtype_has_its_kernels(funcs):
         assert re.search(r"wsum_scalar_kernelILi%dE" % dt, names), dt
 
 
+def test_wide_asm_stores_are_padded(funcs):
+    """Every inline-asm 16-byte sc1 store is followed by s_nop: a store of more than 8 bytes
+    reads its data VGPRs after issue, and hipcc pads nothing after an asm statement, so the
+    next VALU could overwrite the data before the store has read it."""
+    n = 0
+    for name, body in funcs.items():
+        for i, ins in enumerate(body):
+            if ins.startswith("global_store_dwordx4") and "sc1" in ins:
+                n += 1
+                assert i + 1 < len(body) and body[i + 1].startswith("s_nop"), (name, ins, body[i + 1:i + 2])
+    assert n > 0
+
+
 def test_north_star_kernel_streams_dwordx4(funcs):
     """The f32 8-peer kernel (the bench's) loads 16 B per lane per peer with nt and stores sc1."""
     ns = [b for n, b in funcs.items() if re.search(r"wsum_stream_kernelILi0ELi8ELi64ELi1ELb1ELi2ELb0E", n)]
@@ -49,3 +62,18 @@ def test_north_star_kernel_streams_dwordx4(funcs):
     stores = [i for i in body if i.startswith("global_store_dwordx4")]
     assert len(loads) >= 8 and all(" nt" in i for i in loads)
     assert stores and all("sc1" in i for i in stores)
+
+
+def test_bigtile_kernel_streams_dwordx4(funcs):
+    """The fp32 8-peer big-tile kernel (north-star default): 16-byte nt loads, sc1 stores, no spills,
+    and at most 256 VGPRs + a few AGPRs (the two-buffer schedule, not every peer's data hoisted)."""
+    bt = [b for n, b in funcs.items() if re.search(r"wsum_bigtile_kernelILi0ELi8ELi16E", n)]
+    assert bt
+    body = bt[0]
+    loads = [i for i in body if i.startswith("global_load_dwordx4")]
+    stores = [i for i in body if i.startswith("global_store_dwordx4")]
+    assert len(loads) >= 16 * 8 and all(" nt" in i for i in loads)
+    assert stores and all("sc1" in i for i in stores)
+    assert not [i for i in body if i.startswith("scratch_")]
+    agprs = [int(x) for ins in body for x in re.findall(r"\ba\[?(\d+)", ins)]
+    assert max(agprs + [0]) < 64
