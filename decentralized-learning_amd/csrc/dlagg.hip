@@ -173,13 +173,14 @@ __device__ inline f32x2 round_bf16x2(f32x2 v) {
   __builtin_memcpy(&bits, &h, 4);
   return f32x2{__uint_as_float(bits << 16), __uint_as_float(bits & 0xffff0000u)};
 }
-__device__ inline void bf16_step2(float (&acc)[2], float w, uint32_t word) {
+__device__ inline void bf16_step2(float& a0, float& a1, float w, uint32_t word) {
   const f32x2 x = {__uint_as_float(word << 16), __uint_as_float(word & 0xffff0000u)};
-  const f32x2 prod = round_bf16x2(x * w);                     // fedavg.py:25 w * p1
-  const f32x2 sum = round_bf16x2(f32x2{acc[0], acc[1]} + prod);  // c1.add_(...)
-  acc[0] = sum.x;
-  acc[1] = sum.y;
+  const f32x2 prod = round_bf16x2(x * w);               // fedavg.py:25 w * p1
+  const f32x2 sum = round_bf16x2(f32x2{a0, a1} + prod);  // c1.add_(...)
+  a0 = sum.x;
+  a1 = sum.y;
 }
+__device__ inline void bf16_step2(float (&acc)[2], float w, uint32_t word) { bf16_step2(acc[0], acc[1], w, word); }
 
 __device__ inline float half_bits_to_f(uint32_t h) {
   _Float16 v;
@@ -279,7 +280,39 @@ __device__ inline void store16(uint4* p, const uint4& v) {
 // kGroup so a group's kGroup*CH loads all issue before the first wait.
 // ACC_IN: the running sum starts from `out` (second and later passes of a reduce
 // with more than KMAX peers) instead of p0 * 0.
-template <int DT, int BS, int CH, bool NT, int SP, bool ACC_IN>
+// One peer's 16-byte chunk folded into its E running sums (fedavg.py:22 when `first`, then
+// fedavg.py:25).  PK (bf16 peer tables of more than 8): pairwise through bf16_step2 (packed
+// fp32 ops, one packed conversion per rounding): 16 x 21.3 M bf16 121.9 -> 118.8 us, 32 x 2 M
+// 22.9 -> 21.5 (profiles/r01_ab_pkstream3.log).  Tables of <= 8 peers keep fold_tile's
+// element-wise form, which schedules their loads better (routing them through this helper
+// measured 4 x 25 M 43.8 -> 51.6 us).  Other dtypes: element-wise Ops::step.
+template <int DT, bool PK>
+__device__ __attribute__((always_inline)) inline void fold_chunk(typename Ops<DT>::acc_t (&acc)[Ops<DT>::E],
+                                                                 typename Ops<DT>::w_t wk, const uint4& v,
+                                                                 bool first) {
+  using O = Ops<DT>;
+  if constexpr (DT == DLA_BF16 && PK) {
+    const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+    if (first) {
+      typename O::acc_t x[O::E];
+      O::unpack(v, x);
+#pragma unroll
+      for (int e = 0; e < O::E; ++e) acc[e] = O::zero_mul(x[e]);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) bf16_step2(acc[2 * i], acc[2 * i + 1], wk, w4[i]);
+  } else {
+    typename O::acc_t x[O::E];
+    O::unpack(v, x);
+#pragma unroll
+    for (int e = 0; e < O::E; ++e) {
+      if (first) acc[e] = O::zero_mul(x[e]);
+      acc[e] = O::step(acc[e], wk, x[e]);
+    }
+  }
+}
+
+template <int DT, int BS, int CH, bool NT, int SP, bool ACC_IN, bool PK = false>
 __device__ __attribute__((always_inline)) inline void fold_tile(
     const void* const* __restrict__ p, const typename Ops<DT>::w_t* __restrict__ w, int n_peers,
     int64_t base0, int64_t n_chunks, uint4* __restrict__ out) {
@@ -315,12 +348,16 @@ __device__ __attribute__((always_inline)) inline void fold_tile(
       const typename O::w_t wk = w[k0 + g];
 #pragma unroll
       for (int c = 0; c < CH; ++c) {
-        acc_t x[E];
-        O::unpack(v[g][c], x);
+        if constexpr (PK) {
+          fold_chunk<DT, PK>(acc[c], wk, v[g][c], !ACC_IN && g == 0 && k0 == 0);
+        } else {
+          acc_t x[E];
+          O::unpack(v[g][c], x);
 #pragma unroll
-        for (int e = 0; e < E; ++e) {
-          if (!ACC_IN && g == 0 && k0 == 0) acc[c][e] = O::zero_mul(x[e]);  // fedavg.py:22
-          acc[c][e] = O::step(acc[c][e], wk, x[e]);                          // fedavg.py:25
+          for (int e = 0; e < E; ++e) {
+            if (!ACC_IN && g == 0 && k0 == 0) acc[c][e] = O::zero_mul(x[e]);  // fedavg.py:22
+            acc[c][e] = O::step(acc[c][e], wk, x[e]);                          // fedavg.py:25
+          }
         }
       }
     }
@@ -333,12 +370,16 @@ __device__ __attribute__((always_inline)) inline void fold_tile(
     for (int c = 0; c < CH; ++c) v[c] = load16<NT>(src + idx[c]);
 #pragma unroll
     for (int c = 0; c < CH; ++c) {
-      acc_t x[E];
-      O::unpack(v[c], x);
+      if constexpr (PK) {
+        fold_chunk<DT, PK>(acc[c], wk, v[c], !ACC_IN && k0 == 0);
+      } else {
+        acc_t x[E];
+        O::unpack(v[c], x);
 #pragma unroll
-      for (int e = 0; e < E; ++e) {
-        if (!ACC_IN && k0 == 0) acc[c][e] = O::zero_mul(x[e]);
-        acc[c][e] = O::step(acc[c][e], wk, x[e]);
+        for (int e = 0; e < E; ++e) {
+          if (!ACC_IN && k0 == 0) acc[c][e] = O::zero_mul(x[e]);
+          acc[c][e] = O::step(acc[c][e], wk, x[e]);
+        }
       }
     }
   }
@@ -422,8 +463,8 @@ __global__ __launch_bounds__(BS) void wsum_stream_kernel(
     return;
   }
   for (int64_t tile = blockIdx.x; tile < n_tiles; tile += main_grid)
-    fold_tile<DT, BS, CH, NT, SP, ACC_IN>(tab.p, tab.w, n_peers, tile * tile_chunks, n_chunks,
-                                          static_cast<uint4*>(out_v));
+    fold_tile<DT, BS, CH, NT, SP, ACC_IN, (KMAX > 8)>(tab.p, tab.w, n_peers, tile * tile_chunks, n_chunks,
+                                                       static_cast<uint4*>(out_v));
 }
 
 // ------------------------------------------------ peer-major big-tile kernel
@@ -639,7 +680,7 @@ __global__ __launch_bounds__(kBlock) void wsum_multi_kernel(
   const int64_t n_elems = tab.n_elems[s];
   const int64_t n_chunks = n_elems / Ops<DT>::E;
   if (tile * kBlock < n_chunks)
-    fold_tile<DT, kBlock, 1, true, SP, false>(tab.p[s], tab.w, n_peers, tile * kBlock, n_chunks,
+    fold_tile<DT, kBlock, 1, true, SP, false, (NP > 8)>(tab.p[s], tab.w, n_peers, tile * kBlock, n_chunks,
                                       static_cast<uint4*>(tab.out[s]));
   if (tile == 0) fold_tail<DT, false>(tab.p[s], tab.w, n_peers, n_chunks * Ops<DT>::E, n_elems, tab.out[s]);
 }
