@@ -204,6 +204,29 @@ __device__ inline float pin(float f) {
 }
 __device__ inline float round_f16(float f) { return static_cast<float>(static_cast<_Float16>(pin(f))); }
 
+// Two f16 FedAvg steps on one 32-bit word of two f16 values (element 0 in the low half), as
+// Ops<DLA_F16>::step on both: packed fp32 multiply / add, one v_cvt_pk_f16_f32 (RNE) per
+// rounding.  The product and the sum are pinned as rounded fp32 pairs first, for the same
+// reason as pin(): no fused mix-precision form may skip the fp32 rounding.
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+__device__ inline f32x2 pin2(f32x2 v) {
+  asm("" : "+v"(v));
+  return v;
+}
+__device__ inline f32x2 round_f16x2(f32x2 v) {
+  const f16x2 h = __builtin_convertvector(pin2(v), f16x2);  // v_cvt_pk_f16_f32
+  return __builtin_convertvector(h, f32x2);
+}
+__device__ inline void f16_step2(float& a0, float& a1, float w, uint32_t word) {
+  f16x2 xh;
+  __builtin_memcpy(&xh, &word, 4);
+  const f32x2 x = __builtin_convertvector(xh, f32x2);
+  const f32x2 prod = round_f16x2(x * w);               // fedavg.py:25 w * p1
+  const f32x2 sum = round_f16x2(f32x2{a0, a1} + prod);  // c1.add_(...)
+  a0 = sum.x;
+  a1 = sum.y;
+}
+
 template <> struct Ops<DLA_F16> {
   using acc_t = float;
   using w_t = float;
@@ -281,17 +304,19 @@ __device__ inline void store16(uint4* p, const uint4& v) {
 // ACC_IN: the running sum starts from `out` (second and later passes of a reduce
 // with more than KMAX peers) instead of p0 * 0.
 // One peer's 16-byte chunk folded into its E running sums (fedavg.py:22 when `first`, then
-// fedavg.py:25).  PK (bf16 peer tables of more than 8): pairwise through bf16_step2 (packed
-// fp32 ops, one packed conversion per rounding): 16 x 21.3 M bf16 121.9 -> 118.8 us, 32 x 2 M
-// 22.9 -> 21.5 (profiles/r01_ab_pkstream3.log).  Tables of <= 8 peers keep fold_tile's
-// element-wise form, which schedules their loads better (routing them through this helper
-// measured 4 x 25 M 43.8 -> 51.6 us).  Other dtypes: element-wise Ops::step.
+// fedavg.py:25).  PK: 16-bit pairs through bf16_step2 / f16_step2 (packed fp32 ops, one
+// packed conversion per rounding).  fold_tile uses it for peer tables of more than 8
+// (16 x 21.3 M bf16 121.9 -> 118.8 us, f16 168.3 -> 118.9) and for f16 groups of 8 with
+// smaller tables (8 x 50 M f16 191.8 -> 142.4).  bf16 tables of <= 8 peers and the
+// one-peer-at-a-time remainder of small tables keep the element-wise form, which schedules
+// their loads better (packed: 8 x 50 M bf16 138.0 -> 141.6, 4 x 25 M 43.8 -> 51.6; f16
+// 4 x 25 M 38.8 -> 40.9).  Other dtypes: element-wise Ops::step.
 template <int DT, bool PK>
 __device__ __attribute__((always_inline)) inline void fold_chunk(typename Ops<DT>::acc_t (&acc)[Ops<DT>::E],
                                                                  typename Ops<DT>::w_t wk, const uint4& v,
                                                                  bool first) {
   using O = Ops<DT>;
-  if constexpr (DT == DLA_BF16 && PK) {
+  if constexpr ((DT == DLA_BF16 || DT == DLA_F16) && PK) {
     const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
     if (first) {
       typename O::acc_t x[O::E];
@@ -300,7 +325,12 @@ __device__ __attribute__((always_inline)) inline void fold_chunk(typename Ops<DT
       for (int e = 0; e < O::E; ++e) acc[e] = O::zero_mul(x[e]);
     }
 #pragma unroll
-    for (int i = 0; i < 4; ++i) bf16_step2(acc[2 * i], acc[2 * i + 1], wk, w4[i]);
+    for (int i = 0; i < 4; ++i) {
+      if constexpr (DT == DLA_BF16)
+        bf16_step2(acc[2 * i], acc[2 * i + 1], wk, w4[i]);
+      else
+        f16_step2(acc[2 * i], acc[2 * i + 1], wk, w4[i]);
+    }
   } else {
     typename O::acc_t x[O::E];
     O::unpack(v, x);
@@ -312,7 +342,7 @@ __device__ __attribute__((always_inline)) inline void fold_chunk(typename Ops<DT
   }
 }
 
-template <int DT, int BS, int CH, bool NT, int SP, bool ACC_IN, bool PK = false>
+template <int DT, int BS, int CH, bool NT, int SP, bool ACC_IN, bool PK = false, bool PKR = PK>
 __device__ __attribute__((always_inline)) inline void fold_tile(
     const void* const* __restrict__ p, const typename Ops<DT>::w_t* __restrict__ w, int n_peers,
     int64_t base0, int64_t n_chunks, uint4* __restrict__ out) {
@@ -370,8 +400,8 @@ __device__ __attribute__((always_inline)) inline void fold_tile(
     for (int c = 0; c < CH; ++c) v[c] = load16<NT>(src + idx[c]);
 #pragma unroll
     for (int c = 0; c < CH; ++c) {
-      if constexpr (PK) {
-        fold_chunk<DT, PK>(acc[c], wk, v[c], !ACC_IN && k0 == 0);
+      if constexpr (PKR) {
+        fold_chunk<DT, PKR>(acc[c], wk, v[c], !ACC_IN && k0 == 0);
       } else {
         acc_t x[E];
         O::unpack(v[c], x);
@@ -449,7 +479,10 @@ __device__ __attribute__((always_inline)) inline void fold_tail(
 // ------------------------------------------------ register-stream kernel
 // One flat buffer per peer; tiles dealt to workgroups (grid-stride when the grid
 // is smaller than the tile count); one extra workgroup folds the ragged tail.
-template <int DT, int KMAX, int BS, int CH, bool NT, int SP, bool ACC_IN>
+// PKG: packed f16 pair folds in full groups of 8 for an 8-peer table (chosen at launch when
+// the pass has 8 peers: the packed group path, even unused, slows the one-peer-at-a-time
+// loop of smaller passes; 4 x 25 M f16 39.0 vs 44.3 us).
+template <int DT, int KMAX, int BS, int CH, bool NT, int SP, bool ACC_IN, bool PKG = false>
 __global__ __launch_bounds__(BS) void wsum_stream_kernel(
     const PeerTable<typename Ops<DT>::w_t, KMAX> tab, int n_peers, int64_t n_chunks,
     int64_t n_elems, void* __restrict__ out_v) {
@@ -463,7 +496,7 @@ __global__ __launch_bounds__(BS) void wsum_stream_kernel(
     return;
   }
   for (int64_t tile = blockIdx.x; tile < n_tiles; tile += main_grid)
-    fold_tile<DT, BS, CH, NT, SP, ACC_IN, (KMAX > 8)>(tab.p, tab.w, n_peers, tile * tile_chunks, n_chunks,
+    fold_tile<DT, BS, CH, NT, SP, ACC_IN, (KMAX > 8 || PKG), (KMAX > 8)>(tab.p, tab.w, n_peers, tile * tile_chunks, n_chunks,
                                                        static_cast<uint4*>(out_v));
 }
 
@@ -596,6 +629,14 @@ __device__ __attribute__((always_inline)) inline void fold_words(
           acc[1] = O::zero_mul(x[1]);
         }
         bf16_step2(acc, wk[g], v[g]);  // fedavg.py:25
+      } else if constexpr (DT == DLA_F16) {  // likewise, v_cvt_pk_f16_f32 per rounding
+        if (!ACC_IN && g == 0 && first_round) {
+          acc_t x[2];
+          O::unpack_w(v[g], x);
+          acc[0] = O::zero_mul(x[0]);  // fedavg.py:22
+          acc[1] = O::zero_mul(x[1]);
+        }
+        f16_step2(acc[0], acc[1], wk[g], v[g]);  // fedavg.py:25
       } else {
         acc_t x[O::WE];
         O::unpack_w(v[g], x);
@@ -680,7 +721,7 @@ __global__ __launch_bounds__(kBlock) void wsum_multi_kernel(
   const int64_t n_elems = tab.n_elems[s];
   const int64_t n_chunks = n_elems / Ops<DT>::E;
   if (tile * kBlock < n_chunks)
-    fold_tile<DT, kBlock, 1, true, SP, false, (NP > 8)>(tab.p[s], tab.w, n_peers, tile * kBlock, n_chunks,
+    fold_tile<DT, kBlock, 1, true, SP, false, (NP > 8 || DT == DLA_F16), (NP > 8)>(tab.p[s], tab.w, n_peers, tile * kBlock, n_chunks,
                                       static_cast<uint4*>(tab.out[s]));
   if (tile == 0) fold_tail<DT, false>(tab.p[s], tab.w, n_peers, n_chunks * Ops<DT>::E, n_elems, tab.out[s]);
 }
@@ -857,6 +898,13 @@ hipError_t launch_stream(const PeerTable<typename Ops<DT>::w_t, KMAX>& tab, int 
   if (grid > tiles) grid = tiles;
   if (grid > 0x7ffffffe) grid = 0x7ffffffe;
   if (n_elems > n_chunks * E) ++grid;  // + the ragged-tail workgroup
+  if constexpr (DT == DLA_F16 && KMAX == 8) {
+    if (n == kGroup) {
+      hipLaunchKernelGGL((wsum_stream_kernel<DT, KMAX, BS, CH, NT, SP, ACC_IN, true>),
+                         dim3(static_cast<unsigned>(grid)), dim3(BS), 0, s, tab, n, n_chunks, n_elems, out);
+      return hipGetLastError();
+    }
+  }
   hipLaunchKernelGGL((wsum_stream_kernel<DT, KMAX, BS, CH, NT, SP, ACC_IN>), dim3(static_cast<unsigned>(grid)),
                      dim3(BS), 0, s, tab, n, n_chunks, n_elems, out);
   return hipGetLastError();

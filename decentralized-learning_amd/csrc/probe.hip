@@ -329,7 +329,10 @@ int dlp_bigtile8(const void* const* srcs, const float* w, int64_t bytes_each, vo
   // chunks: 4, 8, 16, 24, 32 two peers in flight; 116, 124, 132 (100 + CH) one peer in flight
   if (chunks == 4) DLP_B(4, 2);
   else if (chunks == 8) DLP_B(8, 2);
+  else if (chunks == 12) DLP_B(12, 2);
   else if (chunks == 16) DLP_B(16, 2);
+  else if (chunks == 20) DLP_B(20, 2);
+  else if (chunks == 120) DLP_B(20, 1);
   else if (chunks == 24) DLP_B(24, 2);
   else if (chunks == 32) DLP_B(32, 2);
   else if (chunks == 116) DLP_B(16, 1);

@@ -56,7 +56,7 @@ def main():
         "read8+w_sc1": lambda: so.dlp_mread8(arr, each, out.data_ptr(), sink.data_ptr(), 1, 2, sp()),
         "wsum": lambda: _lib.wsum_ptrs(0, ptrs, w, p, out.data_ptr(), sp()),
     }
-    for ch in (16, 24, 32, 116, 124):
+    for ch in (12, 16, 20, 116, 120):
         for grid in (0, 256 * 8):
             legs["bigtile_ch%d_grid%d" % (ch, grid)] = (
                 lambda ch=ch, grid=grid: so.dlp_bigtile8(arr, wf, each, out.data_ptr(), ch, grid, sp()))
