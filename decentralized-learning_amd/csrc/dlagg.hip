@@ -562,8 +562,8 @@ __device__ __attribute__((always_inline)) inline void fold_big_tile(
 // NP: the exact peer count (1..8), so the peer loop is fully static.  Workgroups
 // [0, n_full) fold the full big tiles; then one workgroup folds the partial last tile (as
 // 64-chunk stream tiles) and one the ragged tail, when there are any.
-template <int DT, int NP, int BT>
-__global__ __launch_bounds__(64) void wsum_bigtile_kernel(const PeerTable<typename Ops<DT>::w_t, 8> tab,
+template <int DT, int NP, int BT, int KMAX = 8>
+__global__ __launch_bounds__(64) void wsum_bigtile_kernel(const PeerTable<typename Ops<DT>::w_t, KMAX> tab,
                                                           int64_t n_chunks, int64_t n_elems,
                                                           void* __restrict__ out_v) {
   constexpr int64_t kTile = 64 * BT;
@@ -859,16 +859,36 @@ bool use_wide(int64_t n_chunks, int n_peers, int elems_per_chunk) {
 }
 
 // The peer-major big-tile kernel (16 KiB of output per wave) where it beats the 64 x 1
-// stream in interleaved A/B on MI355X (profiles/r01_ab_bigtile*.log):
-//  * fp32, exactly 8 peers, >= 1 M chunks: 8 x 25 M 134.7 vs 137.9 us (rocprofv3: 133.2 us),
-//    8 x 12.5 M 66.3 vs 69.0, 8 x 4 M 21.7 vs 24.3; with 7, 6, 5 or 3 peers the stream wins
-//    by 2-8 % (7 x 25 M 119.6 vs 116.6), and below 1 M chunks the MALL-resident sizes flip;
-//  * fp64, >= 4 peers, >= 512 K chunks: 8 x 12.5 M 134.7 vs 162.1, 4 x 12.5 M 77.3 vs 86.4,
+// stream in interleaved A/B on MI355X (profiles/r01_ab_bigtile*.log, r01s6_ab_bigtile_*.log):
+//  * fp32, 8, 16 or 32 peers, when the big tiles fill their last round of resident waves.  The
+//    kernel runs one wave per SIMD (270 VGPRs), so 256 CUs x 4 = 1024 tiles are in flight;
+//    a launch whose tile count ends just past a multiple of 1024 leaves most of the chip idle
+//    in its last round and loses to the stream.  Measured (big tile vs stream, us):
+//      8 x 25 M (5.96 rounds) 134.4 vs 137.5, 8 x 12.5 M (2.98) 66.3 vs 69.0, 8 x 4 M (0.95)
+//      21.7 vs 24.3; but 8 x 21.3 M (5.08) 117.5 vs 116.9, 8 x 22.5 M (5.36) 123.0 vs 122.7,
+//      8 x 26 M (6.20) 144.3 vs 142.5;
+//      16 x 12.5 M (2.98) 124.5 vs 132.5, 16 x 16 M (3.81) 163.0 vs 167.5, 16 x 24.5 M (5.84)
+//      247.8 vs 259.7; but 16 x 14 M (3.34) 150.3 vs 147.2, 16 x 21.3 M (5.08) 226.4 vs 224.3.
+//      32 x 4.11 M (0.98) 79.8 vs 84.5, 32 x 8.2 M (1.96) 156.0 vs 172.8;
+//      but below the 256 MiB Infinity Cache the stream wins: 8 x 3.4 M (0.81) 20.0 vs 17.8.
+//    Rule: 8, 16 or 32 peers, >= 256 MiB of input, the last (or only) round >= 80 % full.  With 7, 6, 5 or 3 fp32
+//    peers the stream wins by 2-8 % (7 x 25 M 119.6 vs 116.6);
+//  * fp64, 4-8 peers, >= 512 K chunks: 8 x 12.5 M 134.7 vs 162.1, 4 x 12.5 M 77.3 vs 86.4,
 //    8 x 1 M 10.6 vs 13.0 (2 peers tie, 1 peer loses).
 constexpr int kBigTileChunks = 16;
+constexpr int64_t kBigTileSlots = 256 * 4;  // MI355X: 256 CUs x 4 SIMDs x 1 big-tile wave
+bool bigtile_rounds_full(int64_t n_chunks) {
+  const int64_t tile = 64 * kBigTileChunks;
+  const int64_t tiles = (n_chunks + tile - 1) / tile;
+  const int64_t last = tiles % kBigTileSlots;
+  return tiles > 0 && (last == 0 || last * 5 >= kBigTileSlots * 4);
+}
+constexpr int64_t kMallBytes = int64_t{256} << 20;  // Infinity Cache: smaller inputs favour the stream
 bool use_bigtile(int64_t n_chunks, int elems_per_chunk, int n_peers) {
-  if (elems_per_chunk == 4) return n_peers == 8 && n_chunks >= (int64_t{1} << 20);
-  if (elems_per_chunk == 2) return n_peers >= 4 && n_chunks >= (int64_t{1} << 19);
+  if (elems_per_chunk == 4)
+    return (n_peers == 8 || n_peers == 16 || n_peers == 32) && bigtile_rounds_full(n_chunks) &&
+           n_peers * n_chunks * 16 >= kMallBytes;
+  if (elems_per_chunk == 2) return n_peers >= 4 && n_peers <= 8 && n_chunks >= (int64_t{1} << 19);
   return false;
 }
 
@@ -946,8 +966,8 @@ hipError_t launch_wide(const PeerTable<typename Ops<DT>::w_t, KMAX>& tab, int n,
   return hipGetLastError();
 }
 
-template <int DT>
-hipError_t launch_bigtile(const PeerTable<typename Ops<DT>::w_t, 8>& tab, int n, int64_t n_elems, void* out,
+template <int DT, int KMAX>
+hipError_t launch_bigtile(const PeerTable<typename Ops<DT>::w_t, KMAX>& tab, int n, int64_t n_elems, void* out,
                           hipStream_t s) {
   constexpr int BT = kBigTileChunks;
   const int64_t n_chunks = n_elems / Ops<DT>::E;
@@ -957,17 +977,25 @@ hipError_t launch_bigtile(const PeerTable<typename Ops<DT>::w_t, 8>& tab, int n,
   if (grid < 1 || grid > 0x7fffffff) return hipErrorInvalidValue;
   const dim3 g(static_cast<unsigned>(grid)), b(64);
 #define DLA_BIGTILE(NPV) \
-  hipLaunchKernelGGL((wsum_bigtile_kernel<DT, NPV, BT>), g, b, 0, s, tab, n_chunks, n_elems, out)
-  switch (n) {
-    case 1: DLA_BIGTILE(1); break;
-    case 2: DLA_BIGTILE(2); break;
-    case 3: DLA_BIGTILE(3); break;
-    case 4: DLA_BIGTILE(4); break;
-    case 5: DLA_BIGTILE(5); break;
-    case 6: DLA_BIGTILE(6); break;
-    case 7: DLA_BIGTILE(7); break;
-    case 8: DLA_BIGTILE(8); break;
-    default: return hipErrorInvalidValue;
+  hipLaunchKernelGGL((wsum_bigtile_kernel<DT, NPV, BT, KMAX>), g, b, 0, s, tab, n_chunks, n_elems, out)
+  if constexpr (KMAX == 32) {  // 16 or 32 fp32 peers
+    switch (n) {
+      case 16: DLA_BIGTILE(16); break;
+      case 32: DLA_BIGTILE(32); break;
+      default: return hipErrorInvalidValue;
+    }
+  } else {
+    switch (n) {
+      case 1: DLA_BIGTILE(1); break;
+      case 2: DLA_BIGTILE(2); break;
+      case 3: DLA_BIGTILE(3); break;
+      case 4: DLA_BIGTILE(4); break;
+      case 5: DLA_BIGTILE(5); break;
+      case 6: DLA_BIGTILE(6); break;
+      case 7: DLA_BIGTILE(7); break;
+      case 8: DLA_BIGTILE(8); break;
+      default: return hipErrorInvalidValue;
+    }
   }
 #undef DLA_BIGTILE
   return hipGetLastError();
@@ -988,7 +1016,11 @@ hipError_t launch_pass(const PeerTable<typename Ops<DT>::w_t, KMAX>& tab, int n,
     return launch_wide<DT, KMAX, ACC_IN>(tab, n, n_elems, out, s);
   if constexpr (KMAX == 8 && !ACC_IN && (DT == DLA_F32 || DT == DLA_F64)) {
     if (l.variant == 16 || (l.auto_kernel && use_bigtile(n_elems / Ops<DT>::E, Ops<DT>::E, n)))
-      return launch_bigtile<DT>(tab, n, n_elems, out, s);
+      return launch_bigtile<DT, KMAX>(tab, n, n_elems, out, s);
+  }
+  if constexpr (KMAX == 32 && !ACC_IN && DT == DLA_F32) {
+    if (l.variant == 16 || (l.auto_kernel && use_bigtile(n_elems / Ops<DT>::E, Ops<DT>::E, n)))
+      return launch_bigtile<DT, KMAX>(tab, n, n_elems, out, s);
   }
   int block = l.block, chunks = l.chunks;
   if (!block || !chunks) {
@@ -1196,7 +1228,7 @@ const char* dla_select_kernel(int dtype, int n_peers, int64_t n_elems) {
   const int e = 16 / es;  // elements per 16-byte chunk
   const int first_pass = n_peers < kMaxPeersPerPass ? n_peers : kMaxPeersPerPass;
   if (use_wide(n_elems / e, first_pass, e)) return "wsum_wide_kernel";
-  if (n_peers <= 8 && (dtype == DLA_F32 || dtype == DLA_F64) && use_bigtile(n_elems / e, e, n_peers))
+  if ((dtype == DLA_F32 || dtype == DLA_F64) && use_bigtile(n_elems / e, e, n_peers))
     return "wsum_bigtile_kernel";
   return "wsum_stream_kernel";
 }

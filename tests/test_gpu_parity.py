@@ -185,6 +185,40 @@ def test_bigtile_kernel_bit_exact(dtype, n, numel):
     assert same_bits(_bits(out, dtype), want, dtype), (dtype, n, numel)
 
 
+@pytest.mark.parametrize("n", [16, 32])
+@pytest.mark.parametrize("numel", [3, 4096 * 16 + 4, 4096 * 16 * 3 + 7, (1 << 20) + 1])
+def test_bigtile_kernel_many_peers_bit_exact(n, numel):
+    """Big-tile kernel over the 32-entry peer table (16 peers auto-picked when the tiles fill
+    their last round, 32 forced): partial tiles, ragged tails, IEEE specials."""
+    from accdfl_amd import _lib
+    from accdfl_amd.core import wsum
+
+    peers = _random_peers(n, numel, "f32", seed=n * 17 + numel)
+    for i, v in enumerate([-0.0, float("inf"), float("-inf"), float("nan"), 1e-40, -3e38]):
+        peers[(5 * i) % n][(4099 * i) % numel] = v
+    w = [float(x) for x in np.random.default_rng(n + 3).dirichlet(np.ones(n))]
+    want = c_wsum([_bits(p, "f32") for p in peers], w, "f32")
+    out = wsum.wsum([p.cuda() for p in peers], w, cfg=_lib.LaunchCfg(16, 0, 0, 0))
+    torch.cuda.synchronize()
+    assert same_bits(_bits(out, "f32"), want, "f32"), (n, numel)
+
+
+def test_bigtile_kernel_auto_16_peers_full_round():
+    """16 fp32 peers whose big tiles fill exactly two rounds of resident waves: the default
+    launch picks the big-tile kernel (dla_select_kernel says so) and stays bit-exact."""
+    from accdfl_amd import _lib
+    from accdfl_amd.core import wsum
+
+    n, numel = 16, 2048 * 4096 - 5  # 2048 tiles (the last one partial) + a ragged tail, 512 MiB
+    assert _lib.select_kernel(0, n, numel) == "wsum_bigtile_kernel"
+    peers = _random_peers(n, numel, "f32", seed=99)
+    w = [float(x) for x in np.random.default_rng(7).dirichlet(np.ones(n))]
+    want = c_wsum([_bits(p, "f32") for p in peers], w, "f32")
+    out = wsum.wsum([p.cuda() for p in peers], w)
+    torch.cuda.synchronize()
+    assert same_bits(_bits(out, "f32"), want, "f32")
+
+
 @pytest.mark.parametrize("n", [1, 2, 3, 7, 8, 9, 16, 31, 32, 33, 64, 127, 128, 129, 257])
 def test_peer_counts(n):
     from accdfl_amd.core import wsum
