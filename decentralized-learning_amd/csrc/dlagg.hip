@@ -559,28 +559,32 @@ __device__ __attribute__((always_inline)) inline void fold_big_tile(
     store16<2>(out + at(c), O::pack(acc[c]));
 }
 
-// NP: the exact peer count (1..8), so the peer loop is fully static.  Workgroups
-// [0, n_full) fold the full big tiles; then one workgroup folds the partial last tile (as
-// 64-chunk stream tiles) and one the ragged tail, when there are any.
+// NP: the exact peer count, so the peer loop is fully static.  Workgroups [0, n_big) fold
+// big tiles; the next n_seg_wg workgroups fold chunks [n_big * kTile, n_chunks) as 64-chunk
+// stream segments, strided over those workgroups; one more folds the ragged tail, if any.
+// Default launch: n_big = every full tile and one segment workgroup for the partial last
+// tile.  Balanced launch (variant 17): n_big = whole rounds of resident big tiles only, and
+// the rest spread over up to one round of segment workgroups, so a partial last round does
+// not leave most of the chip idle.
 template <int DT, int NP, int BT, int KMAX = 8>
 __global__ __launch_bounds__(64) void wsum_bigtile_kernel(const PeerTable<typename Ops<DT>::w_t, KMAX> tab,
                                                           int64_t n_chunks, int64_t n_elems,
+                                                          int64_t n_big, int64_t n_seg_wg,
                                                           void* __restrict__ out_v) {
   constexpr int64_t kTile = 64 * BT;
-  const int64_t n_full = n_chunks / kTile;
   const int64_t b = blockIdx.x;
   uint4* out = static_cast<uint4*>(out_v);
-  if (b < n_full) {
+  if (b < n_big) {
     // Written as a grid-stride loop although it runs once per workgroup: inside a loop hipcc
     // keeps the two-buffer schedule (peer k+1's 16 loads in flight while peer k folds, ~16-20
     // loads outstanding, <= 256 VGPRs); as straight-line code it waits for every load before
     // each fold and spills the peers' data into AGPRs.
-    for (int64_t t = b; t < n_full; t += gridDim.x)
+    for (int64_t t = b; t < n_big; t += gridDim.x)
       fold_big_tile<DT, NP, BT>(tab.p, tab.w, t * kTile + threadIdx.x, n_chunks, out);
     return;
   }
-  if (b == n_full && n_full * kTile < n_chunks) {  // the partial last tile
-    for (int64_t t0 = n_full * kTile; t0 < n_chunks; t0 += 64)
+  if (b < n_big + n_seg_wg) {  // the chunks after the big tiles, as 64-chunk segments
+    for (int64_t t0 = n_big * kTile + (b - n_big) * 64; t0 < n_chunks; t0 += n_seg_wg * 64)
       fold_tile<DT, 64, 1, true, 2, false>(tab.p, tab.w, NP, t0, n_chunks, out);
     return;
   }
@@ -871,25 +875,36 @@ bool use_wide(int64_t n_chunks, int n_peers, int elems_per_chunk) {
 //      247.8 vs 259.7; but 16 x 14 M (3.34) 150.3 vs 147.2, 16 x 21.3 M (5.08) 226.4 vs 224.3.
 //      32 x 4.11 M (0.98) 79.8 vs 84.5, 32 x 8.2 M (1.96) 156.0 vs 172.8;
 //      but below the 256 MiB Infinity Cache the stream wins: 8 x 3.4 M (0.81) 20.0 vs 17.8.
-//    Rule: 8, 16 or 32 peers, >= 256 MiB of input, the last (or only) round >= 80 % full.  With 7, 6, 5 or 3 fp32
+//    Rule: 8, 16 or 32 peers, >= 256 MiB of input, the last (or only) round >= 80 % full.
+//    Otherwise, from one full round up, the balanced launch (variant 17) keeps the big tiles
+//    for the whole rounds and spreads the rest over one round of 64-chunk segment workgroups
+//    (profiles/r01s6_ab_bigtile_balanced.log, big tile / balanced / stream, us):
+//      8 x 21.3 M 117.7 / 114.1 / 116.9, 8 x 26 M 143.6 / 139.4 / 142.7,
+//      16 x 21.3 M 226.4 / 211.9 / 224.0, 16 x 14 M 150.5 / 139.6 / 148.0,
+//      32 x 6.25 M 131.9 / 121.1 / 130.7; at a full last round it loses
+//      (16 x 12.5 M 124.4 / 127.3 / 132.3) or ties (8 x 25 M 134.5 / 134.3 / 138.5).  With 7, 6, 5 or 3 fp32
 //    peers the stream wins by 2-8 % (7 x 25 M 119.6 vs 116.6);
 //  * fp64, 4-8 peers, >= 512 K chunks: 8 x 12.5 M 134.7 vs 162.1, 4 x 12.5 M 77.3 vs 86.4,
 //    8 x 1 M 10.6 vs 13.0 (2 peers tie, 1 peer loses).
 constexpr int kBigTileChunks = 16;
 constexpr int64_t kBigTileSlots = 256 * 4;  // MI355X: 256 CUs x 4 SIMDs x 1 big-tile wave
-bool bigtile_rounds_full(int64_t n_chunks) {
+// 0: no big tiles; 16: big tiles; 17: big tiles for the whole rounds, the partial last round
+// spread over one round of segment workgroups (the launch variants of the same names).
+int bigtile_kind(int64_t n_chunks) {
   const int64_t tile = 64 * kBigTileChunks;
   const int64_t tiles = (n_chunks + tile - 1) / tile;
   const int64_t last = tiles % kBigTileSlots;
-  return tiles > 0 && (last == 0 || last * 5 >= kBigTileSlots * 4);
+  if (tiles > 0 && (last == 0 || last * 5 >= kBigTileSlots * 4)) return 16;
+  return tiles >= kBigTileSlots ? 17 : 0;
 }
 constexpr int64_t kMallBytes = int64_t{256} << 20;  // Infinity Cache: smaller inputs favour the stream
-bool use_bigtile(int64_t n_chunks, int elems_per_chunk, int n_peers) {
+int use_bigtile(int64_t n_chunks, int elems_per_chunk, int n_peers) {
   if (elems_per_chunk == 4)
-    return (n_peers == 8 || n_peers == 16 || n_peers == 32) && bigtile_rounds_full(n_chunks) &&
-           n_peers * n_chunks * 16 >= kMallBytes;
-  if (elems_per_chunk == 2) return n_peers >= 4 && n_peers <= 8 && n_chunks >= (int64_t{1} << 19);
-  return false;
+    return (n_peers == 8 || n_peers == 16 || n_peers == 32) && n_peers * n_chunks * 16 >= kMallBytes
+               ? bigtile_kind(n_chunks)
+               : 0;
+  if (elems_per_chunk == 2) return n_peers >= 4 && n_peers <= 8 && n_chunks >= (int64_t{1} << 19) ? 16 : 0;
+  return 0;
 }
 
 Launch resolve(const dla_launch_cfg_t* cfg) {
@@ -968,16 +983,24 @@ hipError_t launch_wide(const PeerTable<typename Ops<DT>::w_t, KMAX>& tab, int n,
 
 template <int DT, int KMAX>
 hipError_t launch_bigtile(const PeerTable<typename Ops<DT>::w_t, KMAX>& tab, int n, int64_t n_elems, void* out,
-                          hipStream_t s) {
+                          hipStream_t s, bool balanced) {
   constexpr int BT = kBigTileChunks;
+  constexpr int64_t kTile = 64 * BT;
   const int64_t n_chunks = n_elems / Ops<DT>::E;
-  int64_t grid = n_chunks / (64 * BT);
-  if (grid * 64 * BT < n_chunks) ++grid;        // + the partial-tile workgroup
+  const int64_t n_full = n_chunks / kTile;
+  int64_t n_big = n_full, n_seg_wg = n_full * kTile < n_chunks ? 1 : 0;  // + the partial-tile workgroup
+  if (balanced) {
+    n_big = n_full / kBigTileSlots * kBigTileSlots;
+    const int64_t segs = (n_chunks - n_big * kTile + 63) / 64;
+    n_seg_wg = segs < kBigTileSlots ? segs : kBigTileSlots;
+  }
+  int64_t grid = n_big + n_seg_wg;
   if (n_elems > n_chunks * Ops<DT>::E) ++grid;  // + the ragged-tail workgroup
   if (grid < 1 || grid > 0x7fffffff) return hipErrorInvalidValue;
   const dim3 g(static_cast<unsigned>(grid)), b(64);
-#define DLA_BIGTILE(NPV) \
-  hipLaunchKernelGGL((wsum_bigtile_kernel<DT, NPV, BT, KMAX>), g, b, 0, s, tab, n_chunks, n_elems, out)
+#define DLA_BIGTILE(NPV)                                                                                      \
+  hipLaunchKernelGGL((wsum_bigtile_kernel<DT, NPV, BT, KMAX>), g, b, 0, s, tab, n_chunks, n_elems, n_big, n_seg_wg, \
+                     out)
   if constexpr (KMAX == 32) {  // 16 or 32 fp32 peers
     switch (n) {
       case 16: DLA_BIGTILE(16); break;
@@ -1015,12 +1038,12 @@ hipError_t launch_pass(const PeerTable<typename Ops<DT>::w_t, KMAX>& tab, int n,
   if (l.variant == 8 || (l.auto_kernel && use_wide(n_elems / Ops<DT>::E, n, Ops<DT>::E)))
     return launch_wide<DT, KMAX, ACC_IN>(tab, n, n_elems, out, s);
   if constexpr (KMAX == 8 && !ACC_IN && (DT == DLA_F32 || DT == DLA_F64)) {
-    if (l.variant == 16 || (l.auto_kernel && use_bigtile(n_elems / Ops<DT>::E, Ops<DT>::E, n)))
-      return launch_bigtile<DT, KMAX>(tab, n, n_elems, out, s);
+    const int kind = l.auto_kernel ? use_bigtile(n_elems / Ops<DT>::E, Ops<DT>::E, n) : l.variant;
+    if (kind == 16 || kind == 17) return launch_bigtile<DT, KMAX>(tab, n, n_elems, out, s, kind == 17);
   }
   if constexpr (KMAX == 32 && !ACC_IN && DT == DLA_F32) {
-    if (l.variant == 16 || (l.auto_kernel && use_bigtile(n_elems / Ops<DT>::E, Ops<DT>::E, n)))
-      return launch_bigtile<DT, KMAX>(tab, n, n_elems, out, s);
+    const int kind = l.auto_kernel ? use_bigtile(n_elems / Ops<DT>::E, Ops<DT>::E, n) : l.variant;
+    if (kind == 16 || kind == 17) return launch_bigtile<DT, KMAX>(tab, n, n_elems, out, s, kind == 17);
   }
   int block = l.block, chunks = l.chunks;
   if (!block || !chunks) {
@@ -1183,8 +1206,9 @@ int wsum_impl(int dtype, const void* const* peers, const double* weights, int n_
                                      std::to_string(kMaxPeersPerPass));
   }
   const Launch l = resolve(cfg);
-  if (l.variant != 1 && l.variant != 2 && l.variant != 4 && l.variant != 8 && l.variant != 16)
-    return fail(DLA_E_CONFIG, "dla_wsum: unsupported variant " + std::to_string(l.variant) + " (1, 2, 4, 8 or 16)");
+  if (l.variant != 1 && l.variant != 2 && l.variant != 4 && l.variant != 8 && l.variant != 16 && l.variant != 17)
+    return fail(DLA_E_CONFIG,
+                "dla_wsum: unsupported variant " + std::to_string(l.variant) + " (1, 2, 4, 8, 16 or 17)");
   if (l.chunks != 0 && l.chunks != 1 && l.chunks != 2 && l.chunks != 4)
     return fail(DLA_E_CONFIG, "dla_wsum: chunks must be 0 (auto), 1, 2 or 4");
   if (l.block != 0 && l.block != 64 && l.block != 256)

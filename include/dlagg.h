@@ -59,16 +59,19 @@ extern "C" {
 /* Launch tuning knobs for dla_wsum_ex (0 = library default for each field). */
 typedef struct dla_launch_cfg {
   int variant;      /* 0 = by shape: 4; 8 for a small share over more than 8 peers
-                       (and 16-bit dtypes over more than 32 peers); 16 for large fp32
-                       shares over exactly 8 peers and fp64 over 4..8;
+                       (and 16-bit dtypes over more than 32 peers); 16 for fp32 shares
+                       over 8, 16 or 32 peers beyond 256 MiB whose big tiles fill >= 80 %
+                       of their last round of 1024 resident waves, and fp64 over 4..8;
                        cache policy of the 16-byte register stream:
                        1 = plain loads / plain stores   2 = nt loads / plain stores
                        4 = nt loads / sc1 stores (write-through, line not kept in L2)
                        8 = word-per-lane kernel (nt loads, sc1 stores, up to 64 peers
                            in flight per lane; chunks/block/grid are ignored)
-                      16 = peer-major big-tile kernel (fp32 / fp64, <= 8 peers: 16 KiB of
-                           output per wave, one peer's 16 KiB streamed at a time;
-                           chunks/block/grid are ignored; other dtypes take 4)         */
+                      16 = peer-major big-tile kernel (fp32 <= 8, 16 or 32 peers, fp64 <= 8:
+                           16 KiB of output per wave, one peer's 16 KiB streamed at a
+                           time; chunks/block/grid are ignored; other dtypes take 4)
+                      17 = 16 with the partial last round of big tiles spread over one
+                           round of 64-chunk segment workgroups                       */
   int chunks;       /* 16-byte chunks per lane per peer per tile: 1, 2, 4; 0 = by shape  */
   int grid_blocks;  /* workgroups; 0 = one per work tile (no grid-stride loop)           */
   int block;        /* threads per workgroup: 64 or 256; 0 = by shape                    */

@@ -55,12 +55,14 @@ def test_library_version_and_argument_errors(lib_path):
     assert _lib.select_kernel(0, 8, 85_354) == "wsum_stream_kernel"
     assert _lib.select_kernel(3, 8, 12_500_000) == "wsum_bigtile_kernel"
     assert _lib.select_kernel(0, 4, 25_000_000) == "wsum_stream_kernel"
-    # big tiles only when they fill their last round of 1024 resident waves (>= 80 %) and the
-    # input exceeds the 256 MiB Infinity Cache
+    # big tiles when the input exceeds the 256 MiB Infinity Cache and they fill their last
+    # round of 1024 resident waves (>= 80 %), or there is at least one full round (balanced
+    # launch: the partial last round goes to segment workgroups)
     assert _lib.select_kernel(0, 16, 12_500_000) == "wsum_bigtile_kernel"
-    assert _lib.select_kernel(0, 16, 21_296_355) == "wsum_stream_kernel"
-    assert _lib.select_kernel(0, 8, 21_300_000) == "wsum_stream_kernel"
+    assert _lib.select_kernel(0, 16, 21_296_355) == "wsum_bigtile_kernel"
+    assert _lib.select_kernel(0, 8, 21_300_000) == "wsum_bigtile_kernel"
     assert _lib.select_kernel(0, 8, 3_400_000) == "wsum_stream_kernel"
+    assert _lib.select_kernel(0, 32, 3_000_000) == "wsum_stream_kernel"  # 0.72 of one round
     assert _lib.select_kernel(0, 32, 4_110_000) == "wsum_bigtile_kernel"
     assert _lib.select_kernel(0, 32, 8_200_000) == "wsum_bigtile_kernel"
     assert _lib.select_kernel(0, 24, 8_200_000) == "wsum_stream_kernel"

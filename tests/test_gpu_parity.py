@@ -203,6 +203,30 @@ def test_bigtile_kernel_many_peers_bit_exact(n, numel):
     assert same_bits(_bits(out, "f32"), want, "f32"), (n, numel)
 
 
+@pytest.mark.parametrize("n", [3, 8, 16, 32])
+@pytest.mark.parametrize("numel", [5, 4096 * 16 * 3 + 7, 1104 * 4096 + 77])
+def test_bigtile_kernel_balanced_bit_exact(n, numel):
+    """Balanced big-tile launch (variant 17): whole rounds of 1024 big tiles, the rest spread
+    over 64-chunk segment workgroups (1104 tiles: one round + 80 tiles of segments; smaller
+    shares: segments only), ragged tails, IEEE specials."""
+    from accdfl_amd import _lib
+    from accdfl_amd.core import wsum
+
+    peers = _random_peers(n, numel, "f32", seed=n * 31 + numel)
+    for i, v in enumerate([-0.0, float("inf"), float("-inf"), float("nan"), 1e-40, -3e38]):
+        peers[(5 * i) % n][(4099 * i + 4096 * 1024 * (i % 2)) % numel] = v
+    w = [float(x) for x in np.random.default_rng(n + 5).dirichlet(np.ones(n))]
+    want = c_wsum([_bits(p, "f32") for p in peers], w, "f32")
+    out = wsum.wsum([p.cuda() for p in peers], w, cfg=_lib.LaunchCfg(17, 0, 0, 0))
+    torch.cuda.synchronize()
+    assert same_bits(_bits(out, "f32"), want, "f32"), (n, numel)
+    if n >= 16 and numel > 4096 * 1024:  # > 256 MiB, 1.08 rounds: the default picks variant 17
+        assert _lib.select_kernel(0, n, numel) == "wsum_bigtile_kernel"
+        out = wsum.wsum([p.cuda() for p in peers], w)
+        torch.cuda.synchronize()
+        assert same_bits(_bits(out, "f32"), want, "f32"), (n, numel, "auto")
+
+
 def test_bigtile_kernel_auto_16_peers_full_round():
     """16 fp32 peers whose big tiles fill exactly two rounds of resident waves: the default
     launch picks the big-tile kernel (dla_select_kernel says so) and stays bit-exact."""
