@@ -885,7 +885,10 @@ bool use_wide(int64_t n_chunks, int n_peers, int elems_per_chunk) {
 //      (16 x 12.5 M 124.4 / 127.3 / 132.3) or ties (8 x 25 M 134.5 / 134.3 / 138.5).  With 7, 6, 5 or 3 fp32
 //    peers the stream wins by 2-8 % (7 x 25 M 119.6 vs 116.6);
 //  * fp64, 4-8 peers, >= 512 K chunks: 8 x 12.5 M 134.7 vs 162.1, 4 x 12.5 M 77.3 vs 86.4,
-//    8 x 1 M 10.6 vs 13.0 (2 peers tie, 1 peer loses).
+//    8 x 1 M 10.6 vs 13.0 (2 peers tie, 1 peer loses).  From one full round up the balanced
+//    launch wins at every fp64 shape measured, full last round included (big tile / balanced /
+//    stream: 8 x 10.65 M 119.6 / 116.3 / 137.5, 8 x 12.5 M 134.5 / 132.8 / 161.7,
+//    4 x 10.65 M 65.9 / 64.7 / 72.9; profiles/r01s8_ab_f64_balanced.log).
 constexpr int kBigTileChunks = 16;
 constexpr int64_t kBigTileSlots = 256 * 4;  // MI355X: 256 CUs x 4 SIMDs x 1 big-tile wave
 // 0: no big tiles; 16: big tiles; 17: big tiles for the whole rounds, the partial last round
@@ -903,7 +906,10 @@ int use_bigtile(int64_t n_chunks, int elems_per_chunk, int n_peers) {
     return (n_peers == 8 || n_peers == 16 || n_peers == 32) && n_peers * n_chunks * 16 >= kMallBytes
                ? bigtile_kind(n_chunks)
                : 0;
-  if (elems_per_chunk == 2) return n_peers >= 4 && n_peers <= 8 && n_chunks >= (int64_t{1} << 19) ? 16 : 0;
+  if (elems_per_chunk == 2) {  // fp64: balanced from one full round up, even when the last is full
+    if (n_peers < 4 || n_peers > 8 || n_chunks < (int64_t{1} << 19)) return 0;
+    return n_chunks >= kBigTileSlots * 64 * kBigTileChunks ? 17 : 16;
+  }
   return 0;
 }
 

@@ -203,6 +203,24 @@ def test_bigtile_kernel_many_peers_bit_exact(n, numel):
     assert same_bits(_bits(out, "f32"), want, "f32"), (n, numel)
 
 
+@pytest.mark.parametrize("n", [4, 8])
+@pytest.mark.parametrize("numel", [2048 * 16 * 3 + 3, 1104 * 2048 + 1])
+def test_bigtile_kernel_balanced_f64_bit_exact(n, numel):
+    """fp64 balanced big tiles (the default from one full round of 1024 tiles up)."""
+    from accdfl_amd import _lib
+    from accdfl_amd.core import wsum
+
+    peers = _random_peers(n, numel, "f64", seed=n * 37 + numel)
+    for i, v in enumerate([-0.0, float("inf"), float("-inf"), float("nan"), 1e-310, -1.7e308]):
+        peers[(3 * i) % n][(4099 * i + 2048 * 1024 * (i % 2)) % numel] = v
+    w = [float(x) for x in np.random.default_rng(n + 9).dirichlet(np.ones(n))]
+    want = c_wsum([_bits(p, "f64") for p in peers], w, "f64")
+    for cfg in (_lib.LaunchCfg(17, 0, 0, 0), None):
+        out = wsum.wsum([p.cuda() for p in peers], w, cfg=cfg)
+        torch.cuda.synchronize()
+        assert same_bits(_bits(out, "f64"), want, "f64"), (n, numel, cfg)
+
+
 @pytest.mark.parametrize("n", [3, 8, 16, 32])
 @pytest.mark.parametrize("numel", [5, 4096 * 16 * 3 + 7, 1104 * 4096 + 77])
 def test_bigtile_kernel_balanced_bit_exact(n, numel):
