@@ -11,6 +11,11 @@ One step = one launch of the libdlagg kernel over one rank's bucket.
 Algorithmic bytes per step per rank = (N + 1) * P * 4 (N peer reads + 1 output write).
 value = sum over ranks of bytes / max-over-ranks step time.
 
+Launch: under torch.distributed.run (WORLD_SIZE set) every process is one rank.  Without
+it, ``--gpus G`` (G > 1) makes this process start G ranks itself through
+torch.distributed.run before anything touches a GPU, and wait for them; every rank then
+checks that the process group really has G ranks.
+
 Extra objects on the JSON line:
   roofline      dominant kernel (the one dla_select_kernel names): achieved GB/s from HIP events on
                 the launch stream over the timed region vs 8 TB/s HBM peak; traffic =
@@ -27,13 +32,21 @@ Extra objects on the JSON line:
                 0..N-1 of one process (each bucket over its own PCIe link), strong scaling
   collectives   (N > 1) the RCCL legs: all-gather reassembly, exact peer-sharded
                 all-to-all path, reduce-scatter tolerance path
+  strong_scaling  ("scaling": "strong") FIXED models — the north-star 8 x 25 M fp32 model,
+                configs[3] / configs[3'] (64 peers) and configs[4] (128 peers, bf16) — each
+                split into N parameter buckets, one per rank: whole-model bytes / max-over-ranks
+                step time, inputs rotated so the working set exceeds the 256 MiB Infinity
+                Cache; the RCCL all-gather that reassembles the model is timed on its own
+  launch        backend, world size and who started the ranks (rank-count check)
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
 import statistics
+import subprocess
 import sys
 import time
 
@@ -90,6 +103,11 @@ def parse():
                     help="skip the RCCL legs (all-gather, peer-sharded all-to-all / reduce-scatter) at N > 1")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) for real runs; gloo only to rehearse "
                                                              "several ranks on one GPU")
+    ap.add_argument("--no-strong", action="store_true", help="skip the strong-scaling (fixed-model) lines")
+    ap.add_argument("--strong-steps", type=int, default=20)
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launch + rendezvous + rank-count check + bucket split only, no GPU work "
+                         "(what the CPU test of the multi-rank launch runs)")
     ap.add_argument("--sweep", action="store_true", help="interleaved A/B of launch variants, then exit")
     ap.add_argument("--host-breakdown", action="store_true", help="time the host-inclusive phases, then exit")
     ap.add_argument("--configs-only", action="store_true",
@@ -101,22 +119,59 @@ def parse():
     return ap.parse_args()
 
 
-def setup_dist(backend="nccl"):
+def spawn_ranks(args) -> int:
+    """``--gpus G`` without a torch.distributed.run wrapper: start G ranks (one process per
+    GPU) through torch.distributed.run and return its exit code.  Runs before this process
+    touches any GPU (no HIP call has been made yet), and starts the ranks as children."""
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=%d" % args.gpus,
+           "--master-addr=127.0.0.1", "--master-port=%d" % port, os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, BENCH_SELF_SPAWNED="1", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    env.setdefault("OMP_NUM_THREADS", str(max(1, (os.cpu_count() or 1) // args.gpus)))
+    return subprocess.call(cmd, env=env)
+
+
+def setup_dist(args):
     """Returns (rank, world, device, cpu_group): cpu_group is a gloo group for host-side
-    waits that must not park a kernel on any GPU (None at world 1)."""
+    waits that must not park a kernel on any GPU (None at world 1).  Checks that the
+    process group has exactly ``args.gpus`` ranks."""
+    backend = args.dist_backend
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    dev = torch.device("cuda", local % max(1, torch.cuda.device_count()))
-    torch.cuda.set_device(dev)
+    dev = None
+    if not args.dry_run:
+        dev = torch.device("cuda", local % max(1, torch.cuda.device_count()))
+        torch.cuda.set_device(dev)
     cpu_group = None
     if world > 1:
-        if backend == "nccl":
+        if backend == "nccl" and not args.dry_run:
             dist.init_process_group("nccl", device_id=dev)
         else:
-            dist.init_process_group(backend)
+            dist.init_process_group("gloo" if args.dry_run else backend)
         cpu_group = dist.new_group(backend="gloo")
+        world = dist.get_world_size()
+    if world != args.gpus:
+        raise SystemExit("bench.py: --gpus %d but the process group has %d rank(s)" % (args.gpus, world))
     return rank, world, dev, cpu_group
+
+
+def launch_info(world):
+    return {"backend": dist.get_backend() if world > 1 else "none (single process)", "world_size": world,
+            "started_by": ("bench.py --gpus (self-spawned torch.distributed.run)"
+                           if os.environ.get("BENCH_SELF_SPAWNED") else
+                           "torch.distributed.run" if "WORLD_SIZE" in os.environ else "single process")}
+
+
+def log(msg):
+    """Progress on stderr (one line per phase), so a long run visibly advances."""
+    if os.environ.get("RANK", "0") == "0":
+        print("[bench %.1fs] %s" % (time.perf_counter() - _T0, msg), file=sys.stderr, flush=True)
+
+
+_T0 = time.perf_counter()
 
 
 def barrier(world):
@@ -161,45 +216,72 @@ def time_kernel(fn, steps, warmup, world):
     return wall, ev_s
 
 
+def cpu_threads():
+    """(threads used for the CPU legs, how that count was found).  The process's CPU
+    affinity is what it may run on; on the GPU box the job's share is
+    also set as OMP_NUM_THREADS (the affinity there can list the whole machine)."""
+    aff = len(os.sched_getaffinity(0))
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    if omp and omp < aff:
+        return omp, "OMP_NUM_THREADS=%d (the job's CPU share; sched_getaffinity lists %d)" % (omp, aff)
+    return aff, "len(os.sched_getaffinity(0)) = %d" % aff
+
+
+def _cgroup_cpus():
+    """CPUs the cgroup quota allows (cpu.max), or None when unlimited / unreadable."""
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        return None
+
+
 def cpu_baseline(n, p, budget_s):
     """The reference op sequence (deepcopy -> mul_(0) -> add_(w*p)) on torch-CPU, timed on
-    a bounded sample of the same workload: repeated full NS reduces until ~budget_s."""
+    a bounded sample of the same workload: repeated full NS reduces until ~budget_s, at the
+    process's CPU share (cpu_threads), at every affinity CPU when that differs, and on one
+    thread.  ``value`` / ``cores`` is the fastest of these counts."""
     sys.path.insert(0, ROOT)
     from oracle.fedavg_oracle import fedavg_flat_torch  # timed CPU baseline (kind "port")
 
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
-    torch.set_num_threads(threads)
+    share, how = cpu_threads()
+    aff = len(os.sched_getaffinity(0))
     gen = torch.Generator().manual_seed(1000)
     peers = [torch.randn(p, generator=gen) * 0.05 for _ in range(n)]
     w = [float(x) for x in np.random.default_rng(0).dirichlet(np.ones(n))]
     out = torch.empty(p)
-    fedavg_flat_torch(peers, w, out)  # warm-up
-    times = []
-    start = time.perf_counter()
-    while (time.perf_counter() - start < budget_s and len(times) < 200) or len(times) < 3:
-        t0 = time.perf_counter()
-        fedavg_flat_torch(peers, w, out)
-        times.append(time.perf_counter() - t0)
-    med = statistics.median(times)
-    # the same op sequence on ONE thread (BASELINE.md asks for both figures)
-    torch.set_num_threads(1)
-    t1 = []
-    start = time.perf_counter()
-    while (time.perf_counter() - start < budget_s / 2 and len(t1) < 20) or len(t1) < 2:
-        t0 = time.perf_counter()
-        fedavg_flat_torch(peers, w, out)
-        t1.append(time.perf_counter() - t0)
-    torch.set_num_threads(threads)
-    med1 = statistics.median(t1)
+    byts = (n + 1) * p * 4
+    counts = [share] + ([aff] if aff != share else []) + [1]
+    per = {}
+    for th in counts:
+        torch.set_num_threads(th)
+        fedavg_flat_torch(peers, w, out)  # warm-up
+        times = []
+        start = time.perf_counter()
+        lim = budget_s if th != 1 else budget_s / 2
+        while (time.perf_counter() - start < lim and len(times) < 200) or len(times) < 2:
+            t0 = time.perf_counter()
+            fedavg_flat_torch(peers, w, out)
+            times.append(time.perf_counter() - t0)
+        med = statistics.median(times)
+        per[th] = (med, len(times), sum(times))
+        log("cpu baseline: %d threads, %.1f ms per reduce" % (th, med * 1e3))
+    torch.set_num_threads(share)
+    best = min((v[0], th) for th, v in per.items())[1]
+    med, cnt, tot = per[best]
     return {
-        "value": round((n + 1) * p * 4 / med / 1e9, 3),
+        "value": round(byts / med / 1e9, 3),
         "unit": "GB/s",
-        "cores": threads,
+        "cores": best,
         "kind": "port",
-        "sample": "%d full reduces of %d peers x %d fp32 (torch-CPU op sequence of fedavg.py:20-25), median "
-                  "%.1f ms, %.1f s total" % (len(times), n, p, med * 1e3, sum(times)),
-        "value_1thread": round((n + 1) * p * 4 / med1 / 1e9, 3),
-        "sample_1thread": "%d full reduces, median %.1f ms" % (len(t1), med1 * 1e3),
+        "sample": "%d full reduces of %d peers x %d fp32 (torch-CPU op sequence of fedavg.py:20-25) on %d "
+                  "threads, median %.1f ms, %.1f s total" % (cnt, n, p, best, med * 1e3, tot),
+        "threads_source": how,
+        "affinity_cpus": aff,
+        "cgroup_cpu_quota": _cgroup_cpus(),
+        "by_threads": {str(th): {"GB/s": round(byts / v[0] / 1e9, 3), "median_ms": round(v[0] * 1e3, 1),
+                                 "reduces": v[1]} for th, v in per.items()},
+        "value_1thread": round(byts / per[1][0] / 1e9, 3),
         "cpu": _cpu_model(),
     }
 
@@ -454,7 +536,7 @@ def _cpu_port_ms(n, share, dt, budget_s=1.5, max_elems=500_000_000):
     sys.path.insert(0, ROOT)
     from oracle.fedavg_oracle import fedavg_flat_torch  # timed CPU baseline (kind "port")
 
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    threads = cpu_threads()[0]
     torch.set_num_threads(threads)
     base = torch.randn(share, generator=torch.Generator().manual_seed(1000)) * 0.05
     peers = [(base * (1.0 + 0.01 * k)).to(dt) for k in range(n)]  # values do not change CPU time
@@ -529,6 +611,109 @@ def baseline_configs(device, steps=50, cpu=True):
                 res[name].update({"cpu_port_ms": round(ms, 3), "cpu_port_GB/s": round(byts / (ms / 1e3) / 1e9, 2),
                                   "cpu_threads": threads, "gpu_over_cpu": round(ms * 1e3 / (ev / steps * 1e6), 1)})
     return res
+
+
+# Fixed models for the strong-scaling lines: (peers, params of the whole model, dtype).
+STRONG = {
+    "north star, 8 peers x 25 M f32": (8, NS_PARAMS, "f32"),
+    "configs[3] CIFAR-10 GNLeNet, 64 peers": (64, 85_354, "f32"),
+    "configs[3'] CIFAR-10 ResNet-8, 64 peers": (64, 4_932_344, "f32"),
+    "configs[4] google_speech ResNet-34, 128 peers, bf16": (128, 21_296_355, "bf16"),
+}
+_MALL_BYTES = 256 << 20
+_ROTATE_BYTES = 1 << 30
+
+
+def strong_scaling(rank, world, device, steps, warmup):
+    """Each STRONG model split into ``world`` contiguous 256-B-aligned parameter buckets
+    (core/sharding.bucket_bounds, the bucket-sharded layout of SURVEY.md §8e); rank r reduces
+    bucket r of every peer.  Whole-model algorithmic bytes / max-over-ranks step time.  Each
+    rank cycles through enough copies of its bucket that the working set is >= 1 GiB, so a
+    small bucket cannot be served from the 256 MiB Infinity Cache step after step
+    ("cache_warm" repeats one copy, for comparison).  The all-gather that reassembles the
+    whole averaged model on every rank (RCCL) is timed separately, never inside the line."""
+    from accdfl_amd import _lib
+    from accdfl_amd.core import wsum
+    from accdfl_amd.core.sharding import BucketShardedFedAvg, bucket_bounds
+
+    res = {}
+    for name, (n, params, dts) in STRONG.items():
+        log("strong: " + name)
+        dt = torch.float32 if dts == "f32" else torch.bfloat16
+        es = 4 if dts == "f32" else 2
+        bounds = bucket_bounds(params, world, 256 // es)
+        s0, e0 = bounds[rank]
+        m = max(e0 - s0, 0)
+        pitch = max(128, (m + 127) // 128 * 128)
+        set_bytes = (n + 1) * pitch * es
+        copies = 1 if set_bytes >= _ROTATE_BYTES else min(64, -(-_ROTATE_BYTES // set_bytes))
+        w = [float(x) for x in np.random.default_rng(0).dirichlet(np.ones(n))]
+        slabs, outs, plans = [], [], []
+        for c in range(copies):
+            slabs.append(make_slab(n, pitch, dt, device, 1000 + 131 * c + 7 * rank))
+            outs.append(torch.empty(pitch, dtype=dt, device=device))
+            if m:
+                plans.append(_lib.Plan(wsum.dtype_code(dt), [slabs[c][k].data_ptr() for k in range(n)], w, m,
+                                       outs[c].data_ptr()))
+        sp = torch.cuda.current_stream().cuda_stream
+        ctr = [0]
+
+        def step_rot():
+            if plans:
+                plans[ctr[0] % len(plans)].launch(sp)
+            ctr[0] += 1
+
+        def step_warm():
+            if plans:
+                plans[0].launch(sp)
+
+        wall, ev = time_kernel(step_rot, steps, warmup, world)
+        wall_w, _ = time_kernel(step_warm, steps, warmup, world)
+        total = (n + 1) * params * es
+        row = {"peers": n, "params": params, "dtype": dts, "buckets": world,
+               "bucket_params_max": max(e - s for s, e in bounds),
+               "ms_per_step": round(wall / steps * 1e3, 5),
+               "value": round(total / (wall / steps) / 1e9, 2), "unit": "GB/s",
+               "kernel_us_max_rank": round(ev / steps * 1e6, 2),
+               "input_copies_rotated": copies,
+               "cache_warm_value": round(total / (wall_w / steps) / 1e9, 2),
+               "regime": "HBM" if (n + 1) * (bounds[0][1] - bounds[0][0]) * es > _MALL_BYTES
+               else "bucket fits the Infinity Cache; rotated copies keep it HBM-resident"}
+        if world > 1:
+            try:
+                cdev = device if dist.get_backend() == "nccl" else torch.device("cpu")  # gloo: host tensors
+                sh = BucketShardedFedAvg(params, dt, device=cdev)
+                bucket = torch.zeros(sh.bucket_len, dtype=dt, device=cdev)
+                full = torch.empty(params, dtype=dt, device=cdev)
+                wall_g, _ = time_kernel(lambda: sh.all_gather(bucket, full), 10, 2, world)
+                row["allgather_ms"] = round(wall_g / 10 * 1e3, 4)
+                row["with_allgather_value"] = round(total / (wall / steps + wall_g / 10) / 1e9, 2)
+                del bucket, full
+            except Exception as exc:  # never lose the line to the auxiliary leg
+                row["allgather_error"] = "%s: %s" % (type(exc).__name__, exc)
+        res[name] = row
+        del slabs, outs, plans
+        torch.cuda.empty_cache()
+    return res
+
+
+def dry_run(args, rank, world):
+    """No GPU: the launch, the rendezvous, the rank-count check and the bucket split the
+    strong-scaling lines use; rank 0 prints one JSON line (checked by the CPU tests)."""
+    from accdfl_amd.core.sharding import bucket_bounds
+
+    mine = {name: list(bucket_bounds(params, world, 256 // (4 if dts == "f32" else 2))[rank])
+            for name, (_, params, dts) in STRONG.items()}
+    got = [None] * world
+    if world > 1:
+        dist.all_gather_object(got, mine)
+    else:
+        got = [mine]
+    if rank == 0:
+        print(json.dumps({"dry_run": True, "n_gpus": world, "launch": launch_info(world),
+                          "buckets": {name: [g[name] for g in got] for name in STRONG}}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
 
 
 def small_configs(device, steps=200):
@@ -698,7 +883,12 @@ def measured_ceilings(device, nbytes=1 << 30):
 
 def main():
     args = parse()
-    rank, world, device, cpu_group = setup_dist(args.dist_backend)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args))  # nothing has touched a GPU in this process
+    rank, world, device, cpu_group = setup_dist(args)
+    if args.dry_run:
+        dry_run(args, rank, world)
+        return
     from accdfl_amd import _lib
     from accdfl_amd.core import wsum
 
@@ -730,6 +920,7 @@ def main():
     def step():
         _lib.wsum_ptrs(code, ptrs, w, p, out.data_ptr(), torch.cuda.current_stream().cuda_stream, cfg)
 
+    log("headline: %d peers x %d %s, %d ranks" % (n, p, args.dtype, world))
     wall, ev = time_kernel(step, args.steps, args.warmup, world)
     bytes_step = (n + 1) * p * es
     ms_per_step = wall / args.steps * 1e3
@@ -766,6 +957,7 @@ def main():
             "global_params": p * world,
             "parallelism": "bucket-sharded x%d (no data-path collective)" % world,
         },
+        "launch": launch_info(world),
         "roofline": {
             "bound": "hbm",
             "kernel": _lib.select_kernel(code, n, p) if cfg is None else "wsum_stream_kernel (forced launch cfg)",
@@ -778,9 +970,13 @@ def main():
             "us_per_launch": round(kern_s * 1e6, 2),
         },
     }
+    del slab
+    torch.cuda.empty_cache()
+    if not args.no_strong and args.dtype == "f32" and (n, p) == (NS_PEERS, NS_PARAMS):
+        log("strong-scaling lines")
+        result["strong_scaling"] = {"scaling": "strong",
+                                    "lines": strong_scaling(rank, world, device, args.strong_steps, 3)}
     if world > 1 and not args.no_collectives:
-        del slab
-        torch.cuda.empty_cache()
         try:  # same shapes on every rank: a failure raises on all of them, nothing waits
             result["collectives"] = collectives(n, args.coll_params or p, dt, es, world, device, None, w)
         except Exception as exc:  # never lose the headline line to an auxiliary leg
@@ -797,15 +993,16 @@ def main():
         dist.barrier(group=cpu_group)
     if rank == 0 and world == 1:
         if not args.no_small:
+            log("small / baseline configs")
             result["small_configs"] = small_configs(device)
             result["baseline_configs"] = baseline_configs(device)
-        del slab
-        torch.cuda.empty_cache()
         if not args.no_host_inclusive and args.dtype == "f32":
+            log("host-inclusive legs")
             result["host_inclusive"] = host_inclusive(n, p)
             result["wire_ingress"] = wire_ingress(p, device)
             result["host_inclusive_small"] = host_inclusive_small()
         if not args.no_cpu_baseline and args.dtype == "f32":
+            log("cpu baseline")
             result["cpu_baseline"] = cpu_baseline(n, p, args.cpu_seconds)
     if rank == 0:
         print(json.dumps(result), flush=True)

@@ -8,6 +8,7 @@ replaced; a silent fallback would report reference numbers as ours.)
 from __future__ import annotations
 
 import ctypes
+import hashlib
 import os
 import subprocess
 import threading
@@ -17,11 +18,12 @@ PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))  # decent
 REPO_ROOT = os.path.dirname(PKG_ROOT)
 CSRC = os.path.join(PKG_ROOT, "csrc", "dlagg.hip")
 INCLUDE = os.path.join(REPO_ROOT, "include")
+HEADER = os.path.join(INCLUDE, "dlagg.h")
 LIB_PATH = os.environ.get("DLAGG_LIB", os.path.join(PKG_ROOT, "lib", "libdlagg.so"))
 
 # dtype codes (include/dlagg.h)
 DLA_F32, DLA_BF16, DLA_F16, DLA_F64 = 0, 1, 2, 3
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 HIPCC_FLAGS = [
     "--offload-arch=gfx950",
@@ -35,6 +37,7 @@ HIPCC_FLAGS = [
 
 EXPORTED = (
     "dla_version",
+    "dla_build_id",
     "dla_last_error",
     "dla_max_peers_per_pass",
     "dla_select_kernel",
@@ -55,17 +58,46 @@ class DlaggError(RuntimeError):
     """A libdlagg call returned a non-zero status."""
 
 
+def source_build_id() -> str:
+    """Hash of the sources and flags libdlagg.so is built from (csrc/dlagg.hip,
+    include/dlagg.h, HIPCC_FLAGS).  build() compiles it into the library, and lib()
+    refuses a library whose dla_build_id() differs from the tree's."""
+    h = hashlib.sha256()
+    for path in (CSRC, HEADER):
+        with open(path, "rb") as f:
+            h.update(f.read())
+    h.update(" ".join(HIPCC_FLAGS).encode())
+    return h.hexdigest()[:20]
+
+
+_ID_PREFIX = b"dlagg-build-id:"
+
+
+def file_build_id(path: str) -> Optional[str]:
+    """The build id embedded in a built library file (read from its bytes, not loaded)."""
+    try:
+        with open(path, "rb") as f:
+            data = f.read()
+    except OSError:
+        return None
+    i = data.find(_ID_PREFIX)
+    if i < 0:
+        return None
+    j = data.find(b"\0", i)
+    return data[i + len(_ID_PREFIX):j].decode(errors="replace")
+
+
 def build(force: bool = False, verbose: bool = False) -> str:
-    """Compile csrc/dlagg.hip for gfx950 into lib/libdlagg.so (in-tree)."""
+    """Compile csrc/dlagg.hip for gfx950 into lib/libdlagg.so (in-tree), unless the
+    library there already carries this tree's build id."""
     out = os.path.join(PKG_ROOT, "lib", "libdlagg.so")
-    if not force and os.path.exists(out):
-        src_m = max(os.path.getmtime(CSRC), os.path.getmtime(os.path.join(INCLUDE, "dlagg.h")))
-        if os.path.getmtime(out) >= src_m:
-            return out
+    bid = source_build_id()
+    if not force and file_build_id(out) == bid:
+        return out
     os.makedirs(os.path.dirname(out), exist_ok=True)
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
     tmp = out + ".tmp"
-    cmd = [hipcc, *HIPCC_FLAGS, "-I", INCLUDE, "-o", tmp, CSRC]
+    cmd = [hipcc, *HIPCC_FLAGS, '-DDLA_BUILD_ID="%s"' % bid, "-I", INCLUDE, "-o", tmp, CSRC]
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)
@@ -97,6 +129,7 @@ class _Lib:
         so = self.so
         vp = ctypes.c_void_p
         so.dla_version.restype = ctypes.c_int
+        so.dla_build_id.restype = ctypes.c_char_p
         so.dla_last_error.restype = ctypes.c_char_p
         so.dla_max_peers_per_pass.restype = ctypes.c_int
         so.dla_select_kernel.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int64]
@@ -131,6 +164,13 @@ class _Lib:
         v = so.dla_version()
         if v != ABI_VERSION:
             raise RuntimeError("libdlagg ABI version %d, expected %d" % (v, ABI_VERSION))
+        self.build_id = so.dla_build_id().decode()
+        if os.path.exists(CSRC) and os.path.exists(HEADER):
+            want = source_build_id()
+            if self.build_id != want:
+                raise RuntimeError(
+                    "stale libdlagg.so at %s: built from sources %s, the tree's are %s — rebuild it "
+                    "(python -c 'import __graft_entry__ as g; g.build()')" % (path, self.build_id, want))
         self.max_peers_per_pass = so.dla_max_peers_per_pass()
 
     def check(self, rc: int, what: str):

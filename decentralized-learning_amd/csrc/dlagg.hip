@@ -42,7 +42,16 @@
 
 #include "dlagg.h"
 
+// Hash of this file, include/dlagg.h and the compile flags, set by the build
+// (accdfl_amd/_lib.py build()); the loader refuses a library whose id differs from the tree's.
+#ifndef DLA_BUILD_ID
+#define DLA_BUILD_ID "unversioned"
+#endif
+
 namespace {
+
+// Embedded as plain bytes too, so a build's id can be read from the file without loading it.
+__attribute__((used)) const char kBuildIdTag[] = "dlagg-build-id:" DLA_BUILD_ID;
 
 constexpr int kBlock = 256;           // multi-tensor / scalar kernels: 4 waves of 64 lanes
 constexpr int kGroup = 8;             // peers loaded together before folding
@@ -1048,8 +1057,10 @@ hipError_t launch_pass(const PeerTable<typename Ops<DT>::w_t, KMAX>& tab, int n,
     if (kind == 16 || kind == 17) return launch_bigtile<DT, KMAX>(tab, n, n_elems, out, s, kind == 17);
   }
   if constexpr (KMAX == 32 && !ACC_IN && DT == DLA_F32) {
+    // instantiated for exactly 16 and 32 peers; any other count of a forced 16/17 takes the stream
     const int kind = l.auto_kernel ? use_bigtile(n_elems / Ops<DT>::E, Ops<DT>::E, n) : l.variant;
-    if (kind == 16 || kind == 17) return launch_bigtile<DT, KMAX>(tab, n, n_elems, out, s, kind == 17);
+    if ((kind == 16 || kind == 17) && (n == 16 || n == 32))
+      return launch_bigtile<DT, KMAX>(tab, n, n_elems, out, s, kind == 17);
   }
   int block = l.block, chunks = l.chunks;
   if (!block || !chunks) {
@@ -1247,6 +1258,8 @@ struct dla_plan {
 extern "C" {
 
 int dla_version(void) { return DLA_ABI_VERSION; }
+
+const char* dla_build_id(void) { return kBuildIdTag + sizeof("dlagg-build-id:") - 1; }
 
 const char* dla_last_error(void) { return g_last_error.c_str(); }
 

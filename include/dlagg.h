@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define DLA_ABI_VERSION 4
+#define DLA_ABI_VERSION 5
 
 /* element dtypes of the peer buffers and of the output */
 #define DLA_F32 0
@@ -79,6 +79,11 @@ typedef struct dla_launch_cfg {
 
 /* ABI version (DLA_ABI_VERSION). */
 int dla_version(void);
+
+/* Build id: a hash of the sources and compile flags this library was built from
+ * (static string).  The Python loader refuses a library whose id differs from the
+ * tree's, so a stale prebuilt .so fails loudly instead of running old code.  ABI v5. */
+const char* dla_build_id(void);
 
 /* Message describing the last error on this thread ("" if none). */
 const char* dla_last_error(void);

@@ -1,0 +1,34 @@
+"""ctypes access to the C restatement of the reference reduce (oracle/fedavg_ref.c, test
+infrastructure only: the checker the GPU tests compare the HIP path against)."""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+_so = None
+
+
+def lib():
+    global _so
+    if _so is None:
+        so = os.path.join(ROOT, "oracle", "_build", "liboracle_fedavg.so")
+        if not os.path.exists(so):
+            subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
+        _so = ctypes.CDLL(so)
+    return _so
+
+
+def c_wsum(flat_peers, weights, dtype):
+    """fedavg.py:20-25 over flat peer arrays (f32/f64 values, bf16/f16 raw uint16 bits)."""
+    so = lib()
+    n = len(flat_peers)
+    fn = {"f32": so.oracle_wsum_f32, "f64": so.oracle_wsum_f64, "bf16": so.oracle_wsum_bf16,
+          "f16": so.oracle_wsum_f16}[dtype]
+    arrs = [np.ascontiguousarray(p) for p in flat_peers]
+    ptrs = (ctypes.c_void_p * n)(*[a.ctypes.data for a in arrs])
+    w = (ctypes.c_double * n)(*[float(x) for x in weights])
+    out = np.empty_like(arrs[0])
+    fn(ptrs, w, ctypes.c_int(n), ctypes.c_int64(out.size), ctypes.c_void_p(out.ctypes.data))
+    return out

@@ -39,12 +39,28 @@ def test_library_exports_every_declared_symbol(lib_path):
     assert set(_lib.EXPORTED) == set(_declared_symbols())
 
 
+def test_stale_library_is_refused(lib_path, tmp_path):
+    """A library whose embedded build id is not the tree's (built from other sources) fails
+    loudly at load instead of running old code."""
+    from accdfl_amd import _lib
+
+    data = bytearray(open(lib_path, "rb").read())
+    i = data.find(b"dlagg-build-id:") + len(b"dlagg-build-id:")
+    data[i] = ord("0") if data[i] != ord("0") else ord("1")
+    stale = tmp_path / "libdlagg_stale.so"
+    stale.write_bytes(bytes(data))
+    assert _lib.file_build_id(str(stale)) != _lib.source_build_id()
+    with pytest.raises(RuntimeError, match="stale libdlagg.so"):
+        _lib._Lib(str(stale))
+
+
 def test_library_version_and_argument_errors(lib_path):
     """Calls that fail validation never touch the GPU, so they run here."""
     from accdfl_amd import _lib
 
     L = _lib.lib()
-    assert L.so.dla_version() == 4
+    assert L.so.dla_version() == 5
+    assert L.build_id == _lib.source_build_id() == _lib.file_build_id(lib_path)
     assert L.max_peers_per_pass == 128
     # kernel selection by shape (host-only query): north star, configs[3] share, configs[4] share,
     # configs[2], GNLeNet 8 peers, fp64 north-star shape, few peers, invalid arguments
