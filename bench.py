@@ -251,7 +251,11 @@ def cpu_baseline(n, p, budget_s):
     w = [float(x) for x in np.random.default_rng(0).dirichlet(np.ones(n))]
     out = torch.empty(p)
     byts = (n + 1) * p * 4
-    counts = [share] + ([aff] if aff != share else []) + [1]
+    quota = _cgroup_cpus()
+    # every affinity CPU as well, unless the cgroup quota caps the job below that count (then
+    # oversubscribed threads only measure throttling: 2.4 s vs 0.15 s per reduce at 256 threads
+    # under a 16-CPU quota, profiles/r02a_bench.log)
+    counts = [share] + ([aff] if aff != share and (quota is None or quota >= aff) else []) + [1]
     per = {}
     for th in counts:
         torch.set_num_threads(th)
@@ -278,7 +282,7 @@ def cpu_baseline(n, p, budget_s):
                   "threads, median %.1f ms, %.1f s total" % (cnt, n, p, best, med * 1e3, tot),
         "threads_source": how,
         "affinity_cpus": aff,
-        "cgroup_cpu_quota": _cgroup_cpus(),
+        "cgroup_cpu_quota": quota,
         "by_threads": {str(th): {"GB/s": round(byts / v[0] / 1e9, 3), "median_ms": round(v[0] * 1e3, 1),
                                  "reduces": v[1]} for th, v in per.items()},
         "value_1thread": round(byts / per[1][0] / 1e9, 3),
