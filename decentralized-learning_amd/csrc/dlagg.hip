@@ -710,6 +710,106 @@ __global__ __launch_bounds__(64) void wsum_wide_kernel(
   }
 }
 
+// ------------------------------------------------ vector-per-lane ("wide-VW") kernel
+// The word-per-lane kernel with VW dwords per lane per load (8 or 16 bytes: dwordx2 / dwordx4):
+// G peers' loads in flight per lane, then the list-order fold of each dword (bf16 / f16: two
+// elements per dword through bf16_step2 / f16_step2; f32: one).  Same fold, same rounding
+// sequence as wsum_wide_kernel; 2-4x fewer load instructions per byte.
+template <int VW> struct VecOf;
+template <> struct VecOf<2> { using T = u32x2; };
+template <> struct VecOf<4> { using T = u32x4; };
+
+template <int DT>
+__device__ __attribute__((always_inline)) inline void fold_dword(typename Ops<DT>::acc_t* acc,
+                                                                 typename Ops<DT>::w_t wk, uint32_t word, bool first) {
+  using O = Ops<DT>;
+  if (first) {
+    typename O::acc_t x[O::WE];
+    O::unpack_w(word, x);
+#pragma unroll
+    for (int e = 0; e < O::WE; ++e) acc[e] = O::zero_mul(x[e]);  // fedavg.py:22
+  }
+  if constexpr (DT == DLA_BF16) {
+    bf16_step2(acc[0], acc[1], wk, word);  // fedavg.py:25, both elements
+  } else if constexpr (DT == DLA_F16) {
+    f16_step2(acc[0], acc[1], wk, word);
+  } else {
+    acc[0] = O::step(acc[0], wk, __uint_as_float(word));
+  }
+}
+
+__device__ inline void store_vec_sc1(u32x2* p, u32x2 v) {
+  asm volatile("global_store_dwordx2 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+}
+__device__ inline void store_vec_sc1(u32x4* p, u32x4 v) {
+  asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
+}
+
+template <int DT, int KMAX, int G, int VW, bool FULL, bool ACC_IN>
+__device__ __attribute__((always_inline)) inline void vec_round(
+    const PeerTable<typename Ops<DT>::w_t, KMAX>& tab, int k0, int m, bool first_round, int64_t i,
+    typename Ops<DT>::acc_t (&acc)[VW][Ops<DT>::WE]) {
+  using V = typename VecOf<VW>::T;
+  V v[G];
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    // partial round: slots past the last peer reload it (cached; branch-free issue)
+    const int k = FULL || g < m ? k0 + g : k0 + m - 1;
+    v[g] = __builtin_nontemporal_load(static_cast<const V*>(tab.p[k]) + i);
+  }
+  typename Ops<DT>::w_t wk[G];
+#pragma unroll
+  for (int g = 0; g < G; ++g) wk[g] = tab.w[k0 + g];
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    if (FULL || g < m) {
+#pragma unroll
+      for (int d = 0; d < VW; ++d) fold_dword<DT>(acc[d], wk[g], v[g][d], !ACC_IN && first_round && g == 0);
+    }
+  }
+}
+
+template <int DT, int KMAX, int G, int VW, bool ACC_IN>
+__global__ __launch_bounds__(64) void wsum_vec_kernel(
+    const PeerTable<typename Ops<DT>::w_t, KMAX> tab, int n_peers, int64_t n_vecs,
+    int64_t n_elems, void* __restrict__ out_v) {
+  static_assert(DT != DLA_F64, "dword folds: f32 / bf16 / f16");
+  using O = Ops<DT>;
+  using acc_t = typename O::acc_t;
+  using V = typename VecOf<VW>::T;
+  constexpr int WE = O::WE;               // elements per dword
+  const int64_t main_grid = (n_vecs + 63) / 64;
+  if (blockIdx.x >= main_grid) {  // the ragged-tail workgroup (< VW * WE elements)
+    fold_tail<DT, ACC_IN>(tab.p, tab.w, n_peers, n_vecs * VW * WE, n_elems, out_v);
+    return;
+  }
+  const int64_t j = static_cast<int64_t>(blockIdx.x) * 64 + threadIdx.x;
+  const bool live = j < n_vecs;
+  const int64_t i = live ? j : n_vecs - 1;  // clamped: loads stay unpredicated
+  V* out = static_cast<V*>(out_v);
+  acc_t acc[VW][WE];
+  if constexpr (ACC_IN) {
+    const V o = out[i];
+#pragma unroll
+    for (int d = 0; d < VW; ++d) O::unpack_w(o[d], acc[d]);
+  }
+#pragma unroll
+  for (int r = 0; r < (KMAX + G - 1) / G; ++r) {
+    const int k0 = r * G;
+    if (k0 >= n_peers) break;
+    if (k0 + G <= n_peers)  // full round: its own unpredicated path (as wsum_wide_kernel)
+      vec_round<DT, KMAX, G, VW, true, ACC_IN>(tab, k0, G, r == 0, i, acc);
+    else
+      vec_round<DT, KMAX, G, VW, false, ACC_IN>(tab, k0, n_peers - k0, r == 0, i, acc);
+  }
+  if (live) {
+    V o;
+#pragma unroll
+    for (int d = 0; d < VW; ++d) o[d] = O::pack_w(acc[d]);
+    store_vec_sc1(out + i, o);
+  }
+}
+
 // ------------------------------------------------ multi-tensor kernel
 // Up to MAXSEG parameter tensors ("segments") of one model in ONE launch
 // (fedavg.py:24 walks them one by one).  Workgroup b finds its segment from the
@@ -996,6 +1096,35 @@ hipError_t launch_wide(const PeerTable<typename Ops<DT>::w_t, KMAX>& tab, int n,
   return hipGetLastError();
 }
 
+// Variants 9-12: the vector-per-lane kernel (VW dwords per lane, G peers in flight per lane).
+template <int DT, int KMAX, bool ACC_IN>
+hipError_t launch_vec(const PeerTable<typename Ops<DT>::w_t, KMAX>& tab, int n, int64_t n_elems, void* out,
+                      hipStream_t s, int variant) {
+  if constexpr (DT == DLA_F64 || KMAX == 8) {
+    return hipErrorInvalidValue;
+  } else {
+    constexpr int WE = Ops<DT>::WE;
+#define DLA_VEC(G_, VW_)                                                                                   \
+  do {                                                                                                     \
+    constexpr int G = KMAX < (G_) ? KMAX : (G_);                                                           \
+    const int64_t n_vecs = n_elems / ((VW_) * WE);                                                         \
+    int64_t grid = (n_vecs + 63) / 64;                                                                     \
+    if (n_elems > n_vecs * (VW_) * WE) ++grid;                                                             \
+    if (grid < 1 || grid > 0x7fffffff) return hipErrorInvalidValue;                                        \
+    hipLaunchKernelGGL((wsum_vec_kernel<DT, KMAX, G, VW_, ACC_IN>), dim3(static_cast<unsigned>(grid)), dim3(64), \
+                       0, s, tab, n, n_vecs, n_elems, out);                                                \
+  } while (0)
+    switch (variant) {
+      case 9: DLA_VEC(32, 2); break;
+      case 10: DLA_VEC(16, 4); break;
+      case 11: DLA_VEC(32, 4); break;
+      default: DLA_VEC(16, 2); break;  // 12
+    }
+#undef DLA_VEC
+    return hipGetLastError();
+  }
+}
+
 template <int DT, int KMAX>
 hipError_t launch_bigtile(const PeerTable<typename Ops<DT>::w_t, KMAX>& tab, int n, int64_t n_elems, void* out,
                           hipStream_t s, bool balanced) {
@@ -1049,6 +1178,9 @@ hipError_t launch_pass(const PeerTable<typename Ops<DT>::w_t, KMAX>& tab, int n,
     hipLaunchKernelGGL((wsum_scalar_kernel<DT, KMAX, ACC_IN>), dim3(static_cast<unsigned>(blocks)),
                        dim3(kBlock), 0, s, tab, n, n_elems, out);
     return hipGetLastError();
+  }
+  if (l.variant >= 9 && l.variant <= 12) {
+    if constexpr (DT != DLA_F64 && KMAX != 8) return launch_vec<DT, KMAX, ACC_IN>(tab, n, n_elems, out, s, l.variant);
   }
   if (l.variant == 8 || (l.auto_kernel && use_wide(n_elems / Ops<DT>::E, n, Ops<DT>::E)))
     return launch_wide<DT, KMAX, ACC_IN>(tab, n, n_elems, out, s);
@@ -1223,9 +1355,10 @@ int wsum_impl(int dtype, const void* const* peers, const double* weights, int n_
                                      std::to_string(kMaxPeersPerPass));
   }
   const Launch l = resolve(cfg);
-  if (l.variant != 1 && l.variant != 2 && l.variant != 4 && l.variant != 8 && l.variant != 16 && l.variant != 17)
+  if (l.variant != 1 && l.variant != 2 && l.variant != 4 && !(l.variant >= 8 && l.variant <= 12) && l.variant != 16 &&
+      l.variant != 17)
     return fail(DLA_E_CONFIG,
-                "dla_wsum: unsupported variant " + std::to_string(l.variant) + " (1, 2, 4, 8, 16 or 17)");
+                "dla_wsum: unsupported variant " + std::to_string(l.variant) + " (1, 2, 4, 8-12, 16 or 17)");
   if (l.chunks != 0 && l.chunks != 1 && l.chunks != 2 && l.chunks != 4)
     return fail(DLA_E_CONFIG, "dla_wsum: chunks must be 0 (auto), 1, 2 or 4");
   if (l.block != 0 && l.block != 64 && l.block != 256)

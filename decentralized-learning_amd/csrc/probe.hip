@@ -14,6 +14,7 @@
 namespace {
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
 template <int CH, bool NT>
 __global__ __launch_bounds__(256) void read_kernel(const u32x4* __restrict__ src, int64_t n_chunks,
@@ -239,6 +240,87 @@ __global__ __launch_bounds__(64) void policy_kernel(const u32x4* s0, const u32x4
 }
 #undef DLP_LD
 
+// Width-calibration read: each lane reads W bytes (4, 8 or 16) per load, 4 loads in flight per
+// lane, nt.  Over a buffer of known size this calibrates rocprofv3's FETCH_SIZE for the load
+// width the word-per-lane FedAvg kernels use (MI355X_MICROARCH.md: only 16-B reads are calibrated).
+template <typename V>
+__global__ __launch_bounds__(256) void read_w_kernel(const V* __restrict__ src, int64_t n, uint32_t* __restrict__ sink) {
+  const int64_t base = static_cast<int64_t>(blockIdx.x) * 1024 + threadIdx.x;
+  V v[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    int64_t i = base + c * 256;
+    i = i < n ? i : n - 1;
+    v[c] = __builtin_nontemporal_load(src + i);
+  }
+  uint32_t f = 0;
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const uint32_t* q = reinterpret_cast<const uint32_t*>(&v[c]);
+#pragma unroll
+    for (int d = 0; d < static_cast<int>(sizeof(V) / 4); ++d) f ^= q[d];
+  }
+  if (f == 0x9e3779b9u && threadIdx.x == 0) sink[blockIdx.x & 1023] = f;
+}
+
+// The many-peer access pattern of the word-per-lane FedAvg kernels without the arithmetic:
+// lane j of workgroup b reads vector (b * 64 + j) of each of n_src rows (W bytes per lane), G rows
+// at a time, XOR-folded; one W-byte output per lane written sc1 (write=1) or nothing.
+struct SrcTable { const void* p[128]; };
+template <typename V, int G, bool WRITE>
+__global__ __launch_bounds__(64) void mread_w_kernel(const SrcTable tab, int n_src, int64_t n, V* __restrict__ dst,
+                                                     uint32_t* __restrict__ sink) {
+  const int64_t j = static_cast<int64_t>(blockIdx.x) * 64 + threadIdx.x;
+  const int64_t i = j < n ? j : n - 1;
+  V acc;
+  __builtin_memset(&acc, 0, sizeof(V));
+  for (int k0 = 0; k0 < n_src; k0 += G) {
+    V v[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const int k = k0 + g < n_src ? k0 + g : n_src - 1;
+      v[g] = __builtin_nontemporal_load(static_cast<const V*>(tab.p[k]) + i);
+    }
+#pragma unroll
+    for (int g = 0; g < G; ++g) acc ^= v[g];
+  }
+  if constexpr (WRITE) {
+    if (j < n) dst[j] = acc;
+  } else {
+    const uint32_t* q = reinterpret_cast<const uint32_t*>(&acc);
+    if (q[0] == 0x9e3779b9u) sink[blockIdx.x & 1023] = q[0];
+  }
+}
+
+// As mread_w_kernel with the rounds over the 128-row table unrolled (compile-time table
+// indices, as wsum_vec_kernel): the FedAvg kernel's exact load / store schedule, XOR in place
+// of the fold.  Tile-interleaved layout when tile_vecs > 0: vector i of row k lives at
+// base_k + (i / tile_vecs) * stride_vecs + i % tile_vecs.
+template <typename V, int G, bool WRITE>
+__global__ __launch_bounds__(64) void mread_unrolled_kernel(const SrcTable tab, int64_t n, V* __restrict__ dst,
+                                                            uint32_t* __restrict__ sink, int64_t tile_vecs,
+                                                            int64_t stride_vecs) {
+  const int64_t j = static_cast<int64_t>(blockIdx.x) * 64 + threadIdx.x;
+  const int64_t i = j < n ? j : n - 1;
+  const int64_t a = tile_vecs > 0 ? (i / tile_vecs) * stride_vecs + i % tile_vecs : i;
+  V acc;
+  __builtin_memset(&acc, 0, sizeof(V));
+#pragma unroll
+  for (int r = 0; r < 128 / G; ++r) {
+    V v[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) v[g] = __builtin_nontemporal_load(static_cast<const V*>(tab.p[r * G + g]) + a);
+#pragma unroll
+    for (int g = 0; g < G; ++g) acc ^= v[g];
+  }
+  if constexpr (WRITE) {
+    if (j < n) dst[j] = acc;
+  } else {
+    const uint32_t* q = reinterpret_cast<const uint32_t*>(&acc);
+    if (q[0] == 0x9e3779b9u) sink[blockIdx.x & 1023] = q[0];
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -373,6 +455,81 @@ int dlp_mread8(const void* const* srcs, int64_t bytes_each, void* dst, void* sin
   else if (chunks == 4) { if (write) DLP_L(4, true); else DLP_L(4, false); }
   else return -1;
 #undef DLP_L
+  return static_cast<int>(hipGetLastError());
+}
+
+// Read `bytes` with `width` (4, 8 or 16) bytes per lane per load (FETCH_SIZE width calibration).
+int dlp_read_width(const void* src, int64_t bytes, void* sink, int width, void* stream) {
+  if (!src || !sink || bytes < 16) return -1;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const int64_t n = bytes / width;
+  const dim3 g(static_cast<unsigned>((n + 1023) / 1024)), b(256);
+  uint32_t* sk = static_cast<uint32_t*>(sink);
+  switch (width) {
+    case 4: hipLaunchKernelGGL((read_w_kernel<uint32_t>), g, b, 0, s, static_cast<const uint32_t*>(src), n, sk); break;
+    case 8: hipLaunchKernelGGL((read_w_kernel<u32x2>), g, b, 0, s, static_cast<const u32x2*>(src), n, sk); break;
+    case 16: hipLaunchKernelGGL((read_w_kernel<u32x4>), g, b, 0, s, static_cast<const u32x4*>(src), n, sk); break;
+    default: return -1;
+  }
+  return static_cast<int>(hipGetLastError());
+}
+
+// n_src (<= 128) rows of bytes_each, read `width` bytes per lane, `group` rows in flight per
+// lane (16, 32 or 64 for width 4; 16 or 32 for 8; 8 or 16 for 16); write=1 also writes one row.
+int dlp_mread_width(const void* const* srcs, int n_src, int64_t bytes_each, void* dst, void* sink, int width,
+                    int group, int write, void* stream) {
+  if (!srcs || n_src < 1 || n_src > 128 || !sink || bytes_each < 16) return -1;
+  SrcTable t;
+  for (int k = 0; k < 128; ++k) t.p[k] = srcs[k < n_src ? k : n_src - 1];
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const int64_t n = bytes_each / width;
+  const dim3 g(static_cast<unsigned>((n + 63) / 64)), b(64);
+  uint32_t* sk = static_cast<uint32_t*>(sink);
+#define DLP_MW(V, G)                                                                                       \
+  do {                                                                                                     \
+    if (write)                                                                                             \
+      hipLaunchKernelGGL((mread_w_kernel<V, G, true>), g, b, 0, s, t, n_src, n, static_cast<V*>(dst), sk); \
+    else                                                                                                   \
+      hipLaunchKernelGGL((mread_w_kernel<V, G, false>), g, b, 0, s, t, n_src, n, static_cast<V*>(dst), sk); \
+  } while (0)
+  if (width == 4 && group == 16) DLP_MW(uint32_t, 16);
+  else if (width == 4 && group == 32) DLP_MW(uint32_t, 32);
+  else if (width == 4 && group == 64) DLP_MW(uint32_t, 64);
+  else if (width == 8 && group == 16) DLP_MW(u32x2, 16);
+  else if (width == 8 && group == 32) DLP_MW(u32x2, 32);
+  else if (width == 16 && group == 8) DLP_MW(u32x4, 8);
+  else if (width == 16 && group == 16) DLP_MW(u32x4, 16);
+  else return -1;
+#undef DLP_MW
+  return static_cast<int>(hipGetLastError());
+}
+
+// The unrolled 128-row read (mread_unrolled_kernel): width 8 with group 16 or 32, width 16 with
+// group 16; tile_bytes > 0 reads the tile-interleaved layout (row k's tile t at
+// base + (t * 128 + k) * tile_bytes, srcs[k] = base + k * tile_bytes).
+int dlp_mread_unrolled(const void* const* srcs, int64_t bytes_each, void* dst, void* sink, int width, int group,
+                       int write, int64_t tile_bytes, void* stream) {
+  if (!srcs || !sink || bytes_each < 16) return -1;
+  SrcTable t;
+  for (int k = 0; k < 128; ++k) t.p[k] = srcs[k];
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const int64_t n = bytes_each / width;
+  const int64_t tv = tile_bytes > 0 ? tile_bytes / width : 0, sv = tv * 128;
+  const dim3 g(static_cast<unsigned>((n + 63) / 64)), b(64);
+  uint32_t* sk = static_cast<uint32_t*>(sink);
+#define DLP_MU(V, G)                                                                                          \
+  do {                                                                                                        \
+    if (write)                                                                                                \
+      hipLaunchKernelGGL((mread_unrolled_kernel<V, G, true>), g, b, 0, s, t, n, static_cast<V*>(dst), sk, tv, sv); \
+    else                                                                                                      \
+      hipLaunchKernelGGL((mread_unrolled_kernel<V, G, false>), g, b, 0, s, t, n, static_cast<V*>(dst), sk, tv, sv); \
+  } while (0)
+  if (width == 8 && group == 16) DLP_MU(u32x2, 16);
+  else if (width == 8 && group == 32) DLP_MU(u32x2, 32);
+  else if (width == 16 && group == 16) DLP_MU(u32x4, 16);
+  else if (width == 4 && group == 64) DLP_MU(uint32_t, 64);
+  else return -1;
+#undef DLP_MU
   return static_cast<int>(hipGetLastError());
 }
 

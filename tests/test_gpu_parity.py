@@ -124,9 +124,9 @@ def test_every_launch_variant_is_bit_exact(dtype):
 @pytest.mark.parametrize("n", [1, 9, 33, 64, 129, 200])
 @pytest.mark.parametrize("numel", [1, 2, 63, 21_339, 100_007])
 def test_wide_kernel_bit_exact(dtype, n, numel):
-    """Word-per-lane kernel (variant 8; auto-picked for small shares over > 8 peers) and the
-    16-byte stream's lane-parallel ragged tail (up to 7 tail elements for 16-bit dtypes),
-    every dtype, single and multi-pass peer counts."""
+    """Word-per-lane kernel (variant 8; auto-picked for small shares over > 8 peers), its
+    8- and 16-byte-per-lane forms (variants 9-12), and the 16-byte stream's lane-parallel ragged
+    tail (up to 7 tail elements for 16-bit dtypes), every dtype, single and multi-pass peer counts."""
     from accdfl_amd import _lib
     from accdfl_amd.core import wsum
 
@@ -137,7 +137,9 @@ def test_wide_kernel_bit_exact(dtype, n, numel):
     w = [float(x) for x in np.random.default_rng(n).dirichlet(np.ones(n))]
     want = c_wsum([_bits(p, dtype) for p in peers], w, dtype)
     dev = [p.cuda() for p in peers]
-    for cfg in (_lib.LaunchCfg(8, 0, 0, 0), None, _lib.LaunchCfg(4, 1, 0, 64), _lib.LaunchCfg(4, 4, 0, 256)):
+    cfgs = [_lib.LaunchCfg(8, 0, 0, 0), None, _lib.LaunchCfg(4, 1, 0, 64), _lib.LaunchCfg(4, 4, 0, 256)]
+    cfgs += [_lib.LaunchCfg(v, 0, 0, 0) for v in (9, 10, 11, 12)]  # vector-per-lane (dwordx2 / dwordx4)
+    for cfg in cfgs:
         out = wsum.wsum(dev, w, cfg=cfg)
         torch.cuda.synchronize()
         assert same_bits(_bits(out, dtype), want, dtype), (dtype, n, numel, cfg)
@@ -181,6 +183,23 @@ def test_bigtile_kernel_many_peers_bit_exact(n, numel):
     out = wsum.wsum([p.cuda() for p in peers], w, cfg=_lib.LaunchCfg(16, 0, 0, 0))
     torch.cuda.synchronize()
     assert same_bits(_bits(out, "f32"), want, "f32"), (n, numel)
+
+
+@pytest.mark.parametrize("n", [12, 20])
+def test_forced_bigtile_with_unsupported_peer_count_falls_back(n):
+    """Variant 16/17 forced on an fp32 pass of a peer count the big tile is not built for (the
+    32-entry table holds only 16 and 32): the launch takes the stream instead of failing."""
+    from accdfl_amd import _lib
+    from accdfl_amd.core import wsum
+
+    numel = 4096 * 16 * 2 + 5
+    peers = _random_peers(n, numel, "f32", seed=n)
+    w = [float(x) for x in np.random.default_rng(n).dirichlet(np.ones(n))]
+    want = c_wsum([_bits(p, "f32") for p in peers], w, "f32")
+    for v in (16, 17):
+        out = wsum.wsum([p.cuda() for p in peers], w, cfg=_lib.LaunchCfg(v, 0, 0, 0))
+        torch.cuda.synchronize()
+        assert same_bits(_bits(out, "f32"), want, "f32"), (n, v)
 
 
 @pytest.mark.parametrize("n", [4, 8])
