@@ -51,6 +51,9 @@ EXPORTED = (
     "dla_plan_destroy",
     "dla_mean",
     "dla_host_copy_batch",
+    "dla_wsum_sharded",
+    "dla_shard_range",
+    "dla_shutdown",
 )
 
 
@@ -159,6 +162,14 @@ class _Lib:
         so.dla_host_copy_batch.argtypes = [ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(ctypes.c_int64),
                                            ctypes.c_int]
         so.dla_host_copy_batch.restype = ctypes.c_int
+        so.dla_wsum_sharded.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(vp),
+                                         ctypes.POINTER(ctypes.c_double), ctypes.c_int, ctypes.c_int64,
+                                         ctypes.POINTER(vp), ctypes.c_int, ctypes.POINTER(vp)]
+        so.dla_wsum_sharded.restype = ctypes.c_int
+        so.dla_shard_range.argtypes = [ctypes.c_int, ctypes.c_int64, ctypes.c_int, ctypes.c_int,
+                                       ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]
+        so.dla_shard_range.restype = ctypes.c_int
+        so.dla_shutdown.restype = ctypes.c_int
         so.dla_plan_destroy.argtypes = [vp]
         so.dla_plan_destroy.restype = None
         v = so.dla_version()
@@ -272,6 +283,34 @@ def host_copy_batch(dst_ptrs: Sequence[int], src_ptrs: Sequence[int], nbytes: Se
                                   (ctypes.c_int64 * m)(*nbytes), m)
     if rc != 0:
         L.check(rc, "dla_host_copy_batch")
+
+
+def wsum_sharded_ptrs(dtype_code: int, dev_ids: Sequence[int], peer_ptrs: Sequence[int], weights: Sequence[float],
+                      n_elems: int, out_ptrs: Sequence[int], gather: int, stream_ptrs: Sequence[int]) -> None:
+    """dla_wsum_sharded: bucket s of every peer reduced on dev_ids[s] into out_ptrs[s]."""
+    L = lib()
+    g = len(dev_ids)
+    if len(out_ptrs) != g or len(stream_ptrs) != g:
+        raise ValueError("one out pointer and one stream per shard")
+    rc = L.so.dla_wsum_sharded(dtype_code, g, (ctypes.c_int * g)(*dev_ids), _ptr_array(peer_ptrs),
+                               _dbl_array(weights), len(peer_ptrs), n_elems, _ptr_array(out_ptrs), gather,
+                               _ptr_array(stream_ptrs))
+    L.check(rc, "dla_wsum_sharded")
+
+
+def shard_range(dtype_code: int, n_elems: int, n_shards: int, shard: int):
+    """dla_shard_range: (start, end) of a shard's bucket."""
+    L = lib()
+    a, b = ctypes.c_int64(), ctypes.c_int64()
+    L.check(L.so.dla_shard_range(dtype_code, n_elems, n_shards, shard, ctypes.byref(a), ctypes.byref(b)),
+            "dla_shard_range")
+    return a.value, b.value
+
+
+def shutdown() -> None:
+    """dla_shutdown: release the sharded reduce's events and the peer access it enabled."""
+    L = lib()
+    L.check(L.so.dla_shutdown(), "dla_shutdown")
 
 
 class Plan:

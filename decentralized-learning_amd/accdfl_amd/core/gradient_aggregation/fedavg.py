@@ -407,6 +407,29 @@ def _reduce_device_resident(dtype, center: List[torch.Tensor], peers: List[List[
         c.copy_(t)
 
 
+def _reduce_multi_device(center: List[torch.Tensor], peers: List[List[torch.Tensor]], weights,
+                         devices: "List[torch.device] | None" = None):
+    """One dtype group, every tensor on a GPU but not all on one (e.g. models trained on
+    different GPUs of the aggregating node): each parameter is reduced in place of the
+    result's tensor by dla_wsum_sharded, its buckets spread over the GPUs holding the peers
+    (the result's GPU first) and each bucket read over xGMI where it lives elsewhere — no
+    staging copy of any peer.  Parameters under 8 MB per GPU use fewer buckets (one: a single
+    reduce on the result's GPU).  ``devices`` overrides the bucket placement (tests)."""
+    for i, c in enumerate(center):
+        terms = [pl[i].detach() if pl[i].is_contiguous() else pl[i].detach().contiguous() for pl in peers]
+        if devices is None:
+            others = sorted({t.device.index for t in terms} - {c.device.index})
+            devs = [c.device] + [torch.device("cuda", d) for d in others]
+        else:
+            devs = list(devices)
+        g = max(1, min(len(devs), c.numel() * c.element_size() // _MIN_SHARD_BYTES))
+        out = c if c.is_contiguous() else torch.empty(c.shape, dtype=c.dtype, device=c.device)
+        _wsum.wsum_sharded([t.reshape(-1) for t in terms], weights, devs[:g] if devices is None else devs,
+                           out=out.view(-1))
+        if out is not c:
+            c.copy_(out)
+
+
 def _reduce_param(device, center: torch.Tensor, terms: List[torch.Tensor], weights: List[float]):
     """A single parameter with its own contributor set (zip truncation)."""
     dev_terms = [t.detach().to(device).contiguous() for t in terms]
@@ -445,6 +468,8 @@ def reduce_parameters(center_params: List[torch.Tensor], peer_params: List[List[
         resident = all(t.device == device for t in center) and all(t.device == device for pl in peers for t in pl)
         if resident:
             _reduce_device_resident(dtype, center, peers, weights)
+        elif all(t.device.type == "cuda" for t in center) and all(t.device.type == "cuda" for pl in peers for t in pl):
+            _reduce_multi_device(center, peers, weights)
         else:
             _reduce_host_staged(_devices_for(device), dtype, center, peers, weights)
     for i in partial:

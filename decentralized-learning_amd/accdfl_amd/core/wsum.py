@@ -133,3 +133,63 @@ def wsum_multi(peer_params: Sequence[Sequence[torch.Tensor]], weights: Sequence[
             ptrs.append(p.data_ptr())
     _lib.wsum_multi_ptrs(code, ptrs, [o.data_ptr() for o in outs], [o.numel() for o in outs], weights,
                          _stream_ptr(device, stream))
+
+
+def wsum_sharded(peers: Sequence[torch.Tensor], weights: Sequence[float], devices: Sequence[torch.device],
+                 out: Optional[torch.Tensor] = None, mode: str = "direct") -> torch.Tensor:
+    """FedAvg of flat peers that may live on several GPUs of this process, bucket-sharded over
+    ``devices`` (dla_wsum_sharded): shard s reduces bucket s of every peer on
+    devices[s], reading the peers held by other GPUs over xGMI.  The result is bit-identical to
+    ``wsum`` (each element keeps its list-order fold) and lands in ``out`` on devices[0].
+
+    mode "direct": every shard writes its bucket straight into ``out`` (remote stores for the
+    shards on other GPUs); "gather": every shard writes a buffer on its own GPU, then the buckets
+    are copied into ``out`` peer-to-peer (gather=2).  Stream-ordered like any torch op: the
+    shards wait for the peers' producers and ``out``'s device waits for every shard."""
+    n = len(peers)
+    if n < 1:
+        raise IndexError("list index out of range")
+    if len(weights) != n:
+        raise AssertionError("len(weights) != len(peers)")
+    devs = [torch.device(d) if not isinstance(d, torch.device) else d for d in devices]
+    if not devs or any(d.type != "cuda" for d in devs):
+        raise ValueError("wsum_sharded needs one or more HIP devices")
+    require_device(devs[0])
+    p0 = peers[0]
+    code = dtype_code(p0.dtype)
+    numel = p0.numel()
+    for k, p in enumerate(peers):
+        if p.device.type != "cuda" or not p.is_contiguous() or p.dtype != p0.dtype or p.numel() != numel:
+            raise ValueError("peer %d must be a contiguous device tensor of %s x %d" % (k, p0.dtype, numel))
+    if out is None:
+        out = torch.empty(numel, dtype=p0.dtype, device=devs[0])
+    if out.device != devs[0] or not out.is_contiguous() or out.numel() != numel or out.dtype != p0.dtype:
+        raise ValueError("out must be a contiguous %s x %d tensor on %s" % (p0.dtype, numel, devs[0]))
+    # the shards' streams wait for whatever produced the peers
+    peer_devs = sorted({p.device.index for p in peers})
+    shard_streams = [torch.cuda.current_stream(d) for d in devs]
+    for pd in peer_devs:
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(pd))
+        for st in shard_streams:
+            st.wait_event(ev)
+    if mode == "direct":
+        outs, gather, keep = [out.data_ptr()] * len(devs), 0, []
+    elif mode == "gather":
+        keep = [out] + [torch.empty(numel, dtype=p0.dtype, device=d) for d in devs[1:]]
+        outs, gather = [t.data_ptr() for t in keep], 2
+    else:
+        raise ValueError("mode must be 'direct' or 'gather'")
+    _lib.wsum_sharded_ptrs(code, [d.index for d in devs], [p.data_ptr() for p in peers], weights, numel, outs,
+                           gather, [int(st.cuda_stream) for st in shard_streams])
+    # out's device waits for every shard's writes (direct) / its own copies (gather: already ordered)
+    o_stream = shard_streams[0]
+    for st in shard_streams[1:]:
+        if st.cuda_stream != o_stream.cuda_stream:
+            ev = torch.cuda.Event()
+            ev.record(st)
+            o_stream.wait_event(ev)
+    for t, st in zip(keep[1:], shard_streams[1:]):
+        t.record_stream(st)
+        t.record_stream(o_stream)
+    return out

@@ -36,8 +36,11 @@
 
 #include <cstdint>
 #include <cstring>
+#include <mutex>
 #include <new>
+#include <set>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "dlagg.h"
@@ -1376,6 +1379,170 @@ int wsum_impl(int dtype, const void* const* peers, const double* weights, int n_
   return DLA_OK;
 }
 
+// ------------------------------------------------ bucket-sharded reduce over the GPUs of one process
+// the flat parameter vector splits into contiguous 256-B-aligned buckets, one per
+// shard; shard s reduces its bucket of EVERY peer on its own GPU (peers on other GPUs are read
+// over xGMI peer-to-peer), so every element keeps its list-order fold and the result is
+// bit-identical to the one-GPU reduce.  Process-wide state (the only state the library keeps):
+// the peer-access pairs it enabled and a pool of synchronisation events, both released by
+// dla_shutdown().
+std::mutex g_shard_mu;
+std::set<std::pair<int, int>> g_peer_enabled;  // (accessing device, owning device) pairs enabled here
+std::vector<std::pair<int, hipEvent_t>> g_event_pool;  // (device, event) not in use
+
+int64_t shard_bucket_elems(int es, int64_t n_elems, int n_shards) {
+  const int64_t align = 256 / es;
+  int64_t per = (n_elems + n_shards - 1) / n_shards;
+  return (per + align - 1) / align * align;
+}
+
+class DeviceGuard {
+ public:
+  DeviceGuard() { ok_ = hipGetDevice(&prev_) == hipSuccess; }
+  ~DeviceGuard() {
+    if (ok_) (void)hipSetDevice(prev_);
+  }
+
+ private:
+  int prev_ = 0;
+  bool ok_ = false;
+};
+
+// Device that owns a device pointer (-1 if it is not device memory).
+int owner_device(const void* p) {
+  hipPointerAttribute_t a;
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return -1;
+  }
+  if (a.type != hipMemoryTypeDevice) return -1;
+  return a.device;
+}
+
+// Let `dev` read / write memory owned by `owner` (caller holds g_shard_mu; device set to dev).
+hipError_t ensure_peer_access(int dev, int owner) {
+  if (dev == owner || owner < 0 || g_peer_enabled.count({dev, owner})) return hipSuccess;
+  int can = 0;
+  hipError_t e = hipDeviceCanAccessPeer(&can, dev, owner);
+  if (e != hipSuccess) return e;
+  if (!can) return hipErrorPeerAccessUnsupported;
+  e = hipDeviceEnablePeerAccess(owner, 0);
+  if (e == hipErrorPeerAccessAlreadyEnabled) {
+    (void)hipGetLastError();
+    return hipSuccess;  // enabled by someone else (e.g. torch): not ours to disable
+  }
+  if (e == hipSuccess) g_peer_enabled.insert({dev, owner});
+  return e;
+}
+
+hipError_t take_event(int dev, hipEvent_t* ev) {  // caller holds g_shard_mu; device set to dev
+  for (size_t i = 0; i < g_event_pool.size(); ++i) {
+    if (g_event_pool[i].first == dev) {
+      *ev = g_event_pool[i].second;
+      g_event_pool.erase(g_event_pool.begin() + static_cast<std::ptrdiff_t>(i));
+      return hipSuccess;
+    }
+  }
+  return hipEventCreateWithFlags(ev, hipEventDisableTiming);
+}
+
+int wsum_sharded_impl(int dtype, int n_shards, const int* dev_ids, const void* const* peers, const double* weights,
+                      int n_peers, int64_t n_elems, void* const* outs, int gather, void* const* streams) {
+  g_last_error.clear();
+  const int es = elem_size(dtype);
+  if (es == 0) return fail(DLA_E_INVALID, "dla_wsum_sharded: unknown dtype " + std::to_string(dtype));
+  if (n_shards < 1 || !dev_ids || !outs || !streams)
+    return fail(DLA_E_INVALID, "dla_wsum_sharded: need n_shards >= 1 and dev_ids / outs / streams arrays");
+  if (n_peers < 1 || !peers || !weights)
+    return fail(DLA_E_INVALID, "dla_wsum_sharded: n_peers must be >= 1 (fedavg.py:20 indexes models[0])");
+  if (n_elems < 0) return fail(DLA_E_INVALID, "dla_wsum_sharded: n_elems < 0");
+  if (gather < 0 || gather > 2) return fail(DLA_E_INVALID, "dla_wsum_sharded: gather must be 0, 1 or 2");
+  if (n_elems == 0) return DLA_OK;
+  int n_dev = 0;
+  if (hipGetDeviceCount(&n_dev) != hipSuccess) return fail(DLA_E_INVALID, "dla_wsum_sharded: no HIP device");
+  for (int s = 0; s < n_shards; ++s) {
+    if (dev_ids[s] < 0 || dev_ids[s] >= n_dev)
+      return fail(DLA_E_INVALID, "dla_wsum_sharded: bad device id for shard " + std::to_string(s));
+    if (!outs[s]) return fail(DLA_E_INVALID, "dla_wsum_sharded: null out for shard " + std::to_string(s));
+  }
+  for (int k = 0; k < n_peers; ++k)
+    if (!peers[k]) return fail(DLA_E_INVALID, "dla_wsum_sharded: null peer pointer " + std::to_string(k));
+  const int64_t per = shard_bucket_elems(es, n_elems, n_shards);
+  std::lock_guard<std::mutex> lock(g_shard_mu);
+  DeviceGuard guard;
+  // peer access: every shard's GPU reads every peer and writes its own output(s)
+  std::vector<int> owners(static_cast<size_t>(n_peers));
+  for (int k = 0; k < n_peers; ++k) owners[k] = owner_device(peers[k]);
+  std::vector<int> out_owner(static_cast<size_t>(n_shards));
+  for (int s = 0; s < n_shards; ++s) out_owner[s] = owner_device(outs[s]);
+  for (int s = 0; s < n_shards; ++s) {
+    const int dev = dev_ids[s];
+    hipError_t e = hipSetDevice(dev);
+    for (int k = 0; e == hipSuccess && k < n_peers; ++k) e = ensure_peer_access(dev, owners[k]);
+    if (e == hipSuccess) e = ensure_peer_access(dev, out_owner[s]);
+    if (e != hipSuccess)
+      return fail(static_cast<int>(e), std::string("dla_wsum_sharded: peer access for shard ") + std::to_string(s) +
+                                           ": " + hipGetErrorString(e));
+  }
+  // the reduce of every bucket, each on its own GPU and stream
+  const Launch l = resolve(nullptr);
+  std::vector<const void*> shifted(static_cast<size_t>(n_peers));
+  for (int s = 0; s < n_shards; ++s) {
+    const int64_t b = per * s < n_elems ? per * s : n_elems;
+    const int64_t e_ = per * (s + 1) < n_elems ? per * (s + 1) : n_elems;
+    if (b >= e_) continue;
+    for (int k = 0; k < n_peers; ++k) shifted[k] = static_cast<const char*>(peers[k]) + b * es;
+    void* o = static_cast<char*>(outs[s]) + b * es;
+    if (n_peers > kMaxPeersPerPass)  // multi-pass: out carries the running sum (as dla_wsum)
+      for (int k = 1; k < n_peers; ++k)
+        if (shifted[k] == o)
+          return fail(DLA_E_ALIAS, "dla_wsum_sharded: out of shard " + std::to_string(s) + " aliases peer " +
+                                       std::to_string(k));
+    hipError_t e = hipSetDevice(dev_ids[s]);
+    if (e == hipSuccess) {
+      hipStream_t st = static_cast<hipStream_t>(streams[s]);
+      switch (dtype) {
+        case DLA_F32: e = run<DLA_F32>(shifted.data(), weights, n_peers, e_ - b, o, st, l); break;
+        case DLA_BF16: e = run<DLA_BF16>(shifted.data(), weights, n_peers, e_ - b, o, st, l); break;
+        case DLA_F16: e = run<DLA_F16>(shifted.data(), weights, n_peers, e_ - b, o, st, l); break;
+        default: e = run<DLA_F64>(shifted.data(), weights, n_peers, e_ - b, o, st, l); break;
+      }
+    }
+    if (e != hipSuccess)
+      return fail(static_cast<int>(e), std::string("dla_wsum_sharded: shard ") + std::to_string(s) + ": " +
+                                           hipGetErrorString(e));
+  }
+  if (gather == 0) return DLA_OK;
+  // gather: bucket s (on outs[s]) -> outs[d] for every other destination d (1) or d = 0 only (2),
+  // enqueued on the destination's stream after an event recorded behind shard s's reduce
+  std::vector<hipEvent_t> done(static_cast<size_t>(n_shards), nullptr);
+  hipError_t e = hipSuccess;
+  for (int s = 0; e == hipSuccess && s < n_shards; ++s) {
+    e = hipSetDevice(dev_ids[s]);
+    if (e == hipSuccess) e = take_event(dev_ids[s], &done[s]);
+    if (e == hipSuccess) e = hipEventRecord(done[s], static_cast<hipStream_t>(streams[s]));
+  }
+  const int n_dst = gather == 1 ? n_shards : 1;
+  for (int d = 0; e == hipSuccess && d < n_dst; ++d) {
+    e = hipSetDevice(dev_ids[d]);
+    hipStream_t sd = static_cast<hipStream_t>(streams[d]);
+    for (int s = 0; e == hipSuccess && s < n_shards; ++s) {
+      const int64_t b = per * s < n_elems ? per * s : n_elems;
+      const int64_t e_ = per * (s + 1) < n_elems ? per * (s + 1) : n_elems;
+      if (s == d || b >= e_ || outs[s] == outs[d]) continue;  // same buffer: the bucket is already there
+      e = hipStreamWaitEvent(sd, done[s], 0);
+      if (e == hipSuccess)
+        e = hipMemcpyPeerAsync(static_cast<char*>(outs[d]) + b * es, dev_ids[d],
+                               static_cast<const char*>(outs[s]) + b * es, dev_ids[s],
+                               static_cast<size_t>((e_ - b) * es), sd);
+    }
+  }
+  for (int s = 0; s < n_shards; ++s)  // an event may be re-recorded once every wait on it is enqueued
+    if (done[s]) g_event_pool.push_back({dev_ids[s], done[s]});
+  if (e != hipSuccess) return fail(static_cast<int>(e), std::string("dla_wsum_sharded: gather: ") + hipGetErrorString(e));
+  return DLA_OK;
+}
+
 }  // namespace
 
 struct dla_plan {
@@ -1543,6 +1710,38 @@ int dla_host_copy_batch(void* const* dsts, const void* const* srcs, const int64_
   }
   for (int i = 0; i < n; ++i)
     if (bytes[i] > 0) std::memcpy(dsts[i], srcs[i], static_cast<size_t>(bytes[i]));
+  return DLA_OK;
+}
+
+int dla_shard_range(int dtype, int64_t n_elems, int n_shards, int shard, int64_t* start, int64_t* end) {
+  g_last_error.clear();
+  const int es = elem_size(dtype);
+  if (es == 0 || n_elems < 0 || n_shards < 1 || shard < 0 || shard >= n_shards || !start || !end)
+    return fail(DLA_E_INVALID, "dla_shard_range: bad arguments");
+  const int64_t per = shard_bucket_elems(es, n_elems, n_shards);
+  *start = per * shard < n_elems ? per * shard : n_elems;
+  *end = per * (shard + 1) < n_elems ? per * (shard + 1) : n_elems;
+  return DLA_OK;
+}
+
+int dla_wsum_sharded(int dtype, int n_shards, const int* dev_ids, const void* const* peers, const double* weights,
+                     int n_peers, int64_t n_elems, void* const* outs, int gather, void* const* streams) {
+  return wsum_sharded_impl(dtype, n_shards, dev_ids, peers, weights, n_peers, n_elems, outs, gather, streams);
+}
+
+int dla_shutdown(void) {
+  g_last_error.clear();
+  std::lock_guard<std::mutex> lock(g_shard_mu);
+  DeviceGuard guard;
+  for (auto& de : g_event_pool) {
+    if (hipSetDevice(de.first) == hipSuccess) (void)hipEventDestroy(de.second);
+  }
+  g_event_pool.clear();
+  for (const auto& pr : g_peer_enabled) {
+    if (hipSetDevice(pr.first) == hipSuccess) (void)hipDeviceDisablePeerAccess(pr.second);
+  }
+  g_peer_enabled.clear();
+  (void)hipGetLastError();
   return DLA_OK;
 }
 

@@ -134,6 +134,35 @@ int dla_max_peers_per_pass(void);
  * benchmarks that must name the dominant kernel.  ABI v4. */
 const char* dla_select_kernel(int dtype, int n_peers, int64_t n_elems);
 
+/* Bucket-sharded reduce over several GPUs of ONE process (replaces the
+ * single-device fedavg.py:20-25 loop for models that live on several GPUs of the aggregating
+ * node, e.g. the per-node models of the simulator, simulations/learning_simulation.py:335).
+ *   dev_ids  n_shards HIP device ids; shard s runs on dev_ids[s] (ids may repeat)
+ *   peers    n_peers DEVICE pointers, each to n_elems elements of dtype, on ANY device of the
+ *            process: a shard reads the peers on other GPUs over xGMI (peer access is enabled
+ *            on first use and kept until dla_shutdown)
+ *   outs     n_shards DEVICE pointers, outs[s] to n_elems elements; shard s writes its bucket
+ *            [start_s, end_s) (dla_shard_range) at the same offset of outs[s] (outs may all be
+ *            one buffer: every shard then writes its bucket into it directly)
+ *   gather   0: each outs[s] holds its own bucket only; 1: all-gather, every outs[s] receives
+ *            every bucket (peer-to-peer copies over xGMI); 2: outs[0] receives every bucket
+ *   streams  n_shards hipStream_t, streams[s] on dev_ids[s] (NULL = that device's null stream);
+ *            nothing is synchronised: the peers must be ready when the streams reach this work,
+ *            and with gather the copies into outs[d] are ordered on streams[d] behind the
+ *            reduces they copy (library events)
+ * Buckets are contiguous, every start a multiple of 256 bytes: B = ceil(n_elems / n_shards)
+ * rounded up to 256 / sizeof(dtype) elements, shard s = [min(s*B, n), min((s+1)*B, n)).  Every
+ * element keeps its list-order fold, so the result is bit-identical to dla_wsum.  ABI v5. */
+int dla_wsum_sharded(int dtype, int n_shards, const int* dev_ids, const void* const* peers, const double* weights,
+                     int n_peers, int64_t n_elems, void* const* outs, int gather, void* const* streams);
+
+/* The bucket [*start, *end) of `shard` in dla_wsum_sharded's split.  ABI v5. */
+int dla_shard_range(int dtype, int64_t n_elems, int n_shards, int shard, int64_t* start, int64_t* end);
+
+/* Releases what dla_wsum_sharded keeps across calls (its synchronisation events, and the
+ * peer-access pairs it enabled).  Call only when no sharded work is in flight.  ABI v5. */
+int dla_shutdown(void);
+
 /* Prepared reduce: validates and stores the peer/out pointers once, so a round
  * that reduces the same device buffers again (a PeerSlab every round, a benchmark
  * loop) pays only the launch.  Same semantics as dla_wsum. */

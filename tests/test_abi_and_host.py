@@ -192,3 +192,19 @@ def test_bucket_bounds():
             for s, e in b:
                 assert s % 64 == 0 or s == n
                 assert s <= e
+
+
+def test_shard_range_matches_bucket_bounds(lib_path):
+    """dla_shard_range (host-only) splits exactly like core/sharding.bucket_bounds: contiguous
+    buckets whose starts are multiples of 256 bytes, covering every element once."""
+    from accdfl_amd import _lib
+    from accdfl_amd.core.sharding import bucket_bounds
+
+    for code, es in ((_lib.DLA_F32, 4), (_lib.DLA_BF16, 2), (_lib.DLA_F64, 8)):
+        for n in (0, 1, 63, 85_354, 21_296_355, 25_000_000):
+            for g in (1, 2, 3, 4, 8):
+                got = [_lib.shard_range(code, n, g, s) for s in range(g)]
+                assert got == bucket_bounds(n, g, 256 // es)
+                assert all(a * es % 256 == 0 for a, b in got if a < b)
+    with pytest.raises(_lib.DlaggError):
+        _lib.shard_range(_lib.DLA_F32, 10, 2, 2)
