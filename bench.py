@@ -116,6 +116,8 @@ def parse():
     ap.add_argument("--no-ceilings", action="store_true", help="skip the probe ceilings in --sweep")
     ap.add_argument("--libs", default="", help="comma list of libdlagg builds to A/B in --sweep (same process)")
     ap.add_argument("--pads", default="", help="comma list of extra row-pitch bytes to A/B in --sweep")
+    ap.add_argument("--tile-bytes", default="", help="comma list of tile sizes: A/B the tile-interleaved slab "
+                                                       "(dla_wsum_slab_tiled) against the row-major default in --sweep")
     return ap.parse_args()
 
 
@@ -772,6 +774,31 @@ def sweep(args, device):
                 torch.cuda.empty_cache()  # fresh physical pages for the next allocation
         for t, pad in sorted((statistics.median(v), k) for k, v in res.items()):
             print(json.dumps({"pad_bytes": pad, "us": round(t * 1e6, 2), "GB/s": round(byts / t / 1e9, 1)}))
+        return
+    if args.tile_bytes:
+        byts = (args.peers + 1) * args.params * es
+        tiles = [int(x) for x in args.tile_bytes.split(",")]
+        slabs = {}
+        for tb in tiles:
+            te = tb // es
+            n_t = -(-args.params // te)
+            slabs[tb] = make_slab(n_t * args.peers, te, dt, device, 2000)  # [n_tiles * N, T] = [n_tiles][N][T]
+        res = {}
+        variants = [int(x) for x in (args.sweep_cfgs.split(",") if args.sweep_cfgs else ["9", "12", "10"])]
+        for rnd in range(5):
+            fn = lambda: _lib.wsum_ptrs(code, ptrs, w, args.params, out.data_ptr(), sp)  # noqa: E731
+            _, ev = time_kernel(fn, 50, 5, 1)
+            res.setdefault(("row-major default", 0), []).append(ev / 50)
+            for tb in tiles:
+                for v in variants:
+                    cfg = _lib.LaunchCfg(v, 0, 0, 0)
+                    fn = lambda: _lib.wsum_slab_tiled_ptr(code, slabs[tb].data_ptr(), tb // es, args.peers, w,  # noqa
+                                                          args.params, out.data_ptr(), sp, cfg)
+                    _, ev = time_kernel(fn, 50, 5, 1)
+                    res.setdefault(("tiled %d B" % tb, v), []).append(ev / 50)
+        for t, k in sorted((statistics.median(v), k) for k, v in res.items()):
+            print(json.dumps({"layout": k[0], "variant": k[1], "us": round(t * 1e6, 2),
+                              "GB/s": round(byts / t / 1e9, 1), "min_us": round(min(res[k]) * 1e6, 2)}))
         return
     if args.libs:
         import ctypes

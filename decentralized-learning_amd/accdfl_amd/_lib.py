@@ -54,6 +54,7 @@ EXPORTED = (
     "dla_wsum_sharded",
     "dla_shard_range",
     "dla_shutdown",
+    "dla_wsum_slab_tiled",
 )
 
 
@@ -170,6 +171,10 @@ class _Lib:
                                        ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]
         so.dla_shard_range.restype = ctypes.c_int
         so.dla_shutdown.restype = ctypes.c_int
+        so.dla_wsum_slab_tiled.argtypes = [ctypes.c_int, vp, ctypes.c_int64, ctypes.c_int64,
+                                           ctypes.POINTER(ctypes.c_double), ctypes.c_int, ctypes.c_int64, vp, vp,
+                                           ctypes.POINTER(LaunchCfg)]
+        so.dla_wsum_slab_tiled.restype = ctypes.c_int
         so.dla_plan_destroy.argtypes = [vp]
         so.dla_plan_destroy.restype = None
         v = so.dla_version()
@@ -296,6 +301,15 @@ def wsum_sharded_ptrs(dtype_code: int, dev_ids: Sequence[int], peer_ptrs: Sequen
                                _dbl_array(weights), len(peer_ptrs), n_elems, _ptr_array(out_ptrs), gather,
                                _ptr_array(stream_ptrs))
     L.check(rc, "dla_wsum_sharded")
+
+
+def wsum_slab_tiled_ptr(dtype_code: int, base_ptr: int, tile_elems: int, slab_rows: int, weights: Sequence[float],
+                        n_elems: int, out_ptr: int, stream_ptr: int, cfg: Optional[LaunchCfg] = None) -> None:
+    """dla_wsum_slab_tiled: FedAvg of rows 0..len(weights)-1 of a tile-interleaved slab."""
+    L = lib()
+    rc = L.so.dla_wsum_slab_tiled(dtype_code, base_ptr, tile_elems, slab_rows, _dbl_array(weights), len(weights),
+                                  n_elems, out_ptr, stream_ptr, ctypes.byref(cfg) if cfg is not None else None)
+    L.check(rc, "dla_wsum_slab_tiled")
 
 
 def shard_range(dtype_code: int, n_elems: int, n_shards: int, shard: int):

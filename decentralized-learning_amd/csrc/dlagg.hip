@@ -437,10 +437,12 @@ __device__ __attribute__((always_inline)) inline void fold_tile(
 // memory latencies in sequence (12 of the 13 us of a 64-peer x 21 339-element f32 reduce);
 // broadcasting every value to every lane instead makes the fold a serial VALU chain of
 // n_peers x 7 steps (28 us for one bf16 tail element over 128 peers).
+// tile_shift >= 0: the peers are in the tile-interleaved slab layout (dla_wsum_slab_tiled), element j
+// of a peer at p[k] + (j >> tile_shift) * tile_stride + (j & (2^tile_shift - 1)).
 template <int DT, bool ACC_IN>
 __device__ __attribute__((always_inline)) inline void fold_tail(
     const void* const* __restrict__ p, const typename Ops<DT>::w_t* __restrict__ w, int n_peers,
-    int64_t first, int64_t n_elems, void* __restrict__ out_v) {
+    int64_t first, int64_t n_elems, void* __restrict__ out_v, int tile_shift = -1, int64_t tile_stride = 0) {
   using O = Ops<DT>;
   using acc_t = typename O::acc_t;
   using elem_t = typename O::elem_t;
@@ -458,7 +460,10 @@ __device__ __attribute__((always_inline)) inline void fold_tail(
     const elem_t* src = static_cast<const elem_t*>(p[k]);
     elem_t v[kMaxTail];
 #pragma unroll
-    for (int t = 0; t < kMaxTail; ++t) v[t] = src[first + (t < n_tail ? t : n_tail - 1)];
+    for (int t = 0; t < kMaxTail; ++t) {
+      const int64_t jj = first + (t < n_tail ? t : n_tail - 1);
+      v[t] = src[tile_shift < 0 ? jj : (jj >> tile_shift) * tile_stride + (jj & ((int64_t{1} << tile_shift) - 1))];
+    }
 #pragma unroll
     for (int t = 0; t < kMaxTail; ++t) stage[t][lane] = v[t];
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -750,7 +755,7 @@ __device__ inline void store_vec_sc1(u32x4* p, u32x4 v) {
 
 template <int DT, int KMAX, int G, int VW, bool FULL, bool ACC_IN>
 __device__ __attribute__((always_inline)) inline void vec_round(
-    const PeerTable<typename Ops<DT>::w_t, KMAX>& tab, int k0, int m, bool first_round, int64_t i,
+    const PeerTable<typename Ops<DT>::w_t, KMAX>& tab, int k0, int m, bool first_round, int64_t a,
     typename Ops<DT>::acc_t (&acc)[VW][Ops<DT>::WE]) {
   using V = typename VecOf<VW>::T;
   V v[G];
@@ -758,7 +763,7 @@ __device__ __attribute__((always_inline)) inline void vec_round(
   for (int g = 0; g < G; ++g) {
     // partial round: slots past the last peer reload it (cached; branch-free issue)
     const int k = FULL || g < m ? k0 + g : k0 + m - 1;
-    v[g] = __builtin_nontemporal_load(static_cast<const V*>(tab.p[k]) + i);
+    v[g] = __builtin_nontemporal_load(static_cast<const V*>(tab.p[k]) + a);
   }
   typename Ops<DT>::w_t wk[G];
 #pragma unroll
@@ -772,10 +777,13 @@ __device__ __attribute__((always_inline)) inline void vec_round(
   }
 }
 
-template <int DT, int KMAX, int G, int VW, bool ACC_IN>
+// TILED: the peers are rows of a tile-interleaved slab (dla_wsum_slab_tiled): vector i of a peer at
+// p[k] + (i >> tshift_v) * tstride_v + (i & (2^tshift_v - 1)); the output stays contiguous.
+template <int DT, int KMAX, int G, int VW, bool ACC_IN, bool TILED = false>
 __global__ __launch_bounds__(64) void wsum_vec_kernel(
     const PeerTable<typename Ops<DT>::w_t, KMAX> tab, int n_peers, int64_t n_vecs,
-    int64_t n_elems, void* __restrict__ out_v) {
+    int64_t n_elems, void* __restrict__ out_v, int tshift_v = 0, int64_t tstride_v = 0, int tshift_e = -1,
+    int64_t tstride_e = 0) {
   static_assert(DT != DLA_F64, "dword folds: f32 / bf16 / f16");
   using O = Ops<DT>;
   using acc_t = typename O::acc_t;
@@ -783,12 +791,14 @@ __global__ __launch_bounds__(64) void wsum_vec_kernel(
   constexpr int WE = O::WE;               // elements per dword
   const int64_t main_grid = (n_vecs + 63) / 64;
   if (blockIdx.x >= main_grid) {  // the ragged-tail workgroup (< VW * WE elements)
-    fold_tail<DT, ACC_IN>(tab.p, tab.w, n_peers, n_vecs * VW * WE, n_elems, out_v);
+    fold_tail<DT, ACC_IN>(tab.p, tab.w, n_peers, n_vecs * VW * WE, n_elems, out_v, TILED ? tshift_e : -1,
+                          tstride_e);
     return;
   }
   const int64_t j = static_cast<int64_t>(blockIdx.x) * 64 + threadIdx.x;
   const bool live = j < n_vecs;
   const int64_t i = live ? j : n_vecs - 1;  // clamped: loads stay unpredicated
+  const int64_t a = TILED ? (i >> tshift_v) * tstride_v + (i & ((int64_t{1} << tshift_v) - 1)) : i;
   V* out = static_cast<V*>(out_v);
   acc_t acc[VW][WE];
   if constexpr (ACC_IN) {
@@ -801,9 +811,9 @@ __global__ __launch_bounds__(64) void wsum_vec_kernel(
     const int k0 = r * G;
     if (k0 >= n_peers) break;
     if (k0 + G <= n_peers)  // full round: its own unpredicated path (as wsum_wide_kernel)
-      vec_round<DT, KMAX, G, VW, true, ACC_IN>(tab, k0, G, r == 0, i, acc);
+      vec_round<DT, KMAX, G, VW, true, ACC_IN>(tab, k0, G, r == 0, a, acc);
     else
-      vec_round<DT, KMAX, G, VW, false, ACC_IN>(tab, k0, n_peers - k0, r == 0, i, acc);
+      vec_round<DT, KMAX, G, VW, false, ACC_IN>(tab, k0, n_peers - k0, r == 0, a, acc);
   }
   if (live) {
     V o;
@@ -1126,6 +1136,70 @@ hipError_t launch_vec(const PeerTable<typename Ops<DT>::w_t, KMAX>& tab, int n, 
 #undef DLA_VEC
     return hipGetLastError();
   }
+}
+
+// The tile-interleaved slab (dla_wsum_slab_tiled) through the vector-per-lane kernel: variant 12 =
+// dwordx2 x 16 peers in flight, 10 = dwordx4 x 16, otherwise (default, 9) dwordx2 x 32.
+template <int DT, int KMAX, bool ACC_IN>
+hipError_t launch_vec_tiled(const PeerTable<typename Ops<DT>::w_t, KMAX>& tab, int n, int64_t n_elems, void* out,
+                            hipStream_t s, int variant, int tshift_e, int64_t tstride_e) {
+  if constexpr (DT == DLA_F64) {
+    return hipErrorInvalidValue;
+  } else {
+    constexpr int WE = Ops<DT>::WE;
+#define DLA_VECT(G_, VW_)                                                                                     \
+  do {                                                                                                        \
+    constexpr int G = KMAX < (G_) ? KMAX : (G_);                                                              \
+    constexpr int per_vec = (VW_) * WE;                                                                       \
+    int vs = 0;                                                                                               \
+    while ((1 << vs) < per_vec) ++vs;                                                                         \
+    if (tshift_e < vs) return hipErrorInvalidValue;                                                           \
+    const int64_t n_vecs = n_elems / per_vec;                                                                 \
+    int64_t grid = (n_vecs + 63) / 64;                                                                        \
+    if (n_elems > n_vecs * per_vec) ++grid;                                                                   \
+    if (grid < 1 || grid > 0x7fffffff) return hipErrorInvalidValue;                                           \
+    hipLaunchKernelGGL((wsum_vec_kernel<DT, KMAX, G, VW_, ACC_IN, true>), dim3(static_cast<unsigned>(grid)),   \
+                       dim3(64), 0, s, tab, n, n_vecs, n_elems, out, tshift_e - vs, tstride_e / per_vec, tshift_e, \
+                       tstride_e);                                                                            \
+  } while (0)
+    switch (variant) {
+      case 12: DLA_VECT(16, 2); break;
+      case 10: DLA_VECT(16, 4); break;
+      default: DLA_VECT(32, 2); break;
+    }
+#undef DLA_VECT
+    return hipGetLastError();
+  }
+}
+
+template <int DT>
+hipError_t run_tiled(const void* base, int64_t tile_elems, int tshift, int64_t stride_elems, const double* weights,
+                     int n, int64_t n_elems, void* out, hipStream_t s, int variant) {
+  constexpr int es = sizeof(typename Ops<DT>::elem_t);
+  for (int k0 = 0; k0 < n; k0 += kMaxPeersPerPass) {
+    const int m = n - k0 < kMaxPeersPerPass ? n - k0 : kMaxPeersPerPass;
+    hipError_t e;
+#define DLA_TILED_PASS(KM)                                                                                   \
+  do {                                                                                                       \
+    PeerTable<typename Ops<DT>::w_t, KM> tab;                                                                \
+    std::memset(&tab, 0, sizeof(tab));                                                                       \
+    for (int k = 0; k < m; ++k) {                                                                            \
+      tab.p[k] = static_cast<const char*>(base) + (k0 + k) * tile_elems * es;                                \
+      tab.w[k] = static_cast<typename Ops<DT>::w_t>(weights[k0 + k]);                                        \
+    }                                                                                                        \
+    e = k0 > 0 ? launch_vec_tiled<DT, KM, true>(tab, m, n_elems, out, s, variant, tshift, stride_elems)       \
+               : launch_vec_tiled<DT, KM, false>(tab, m, n_elems, out, s, variant, tshift, stride_elems);     \
+  } while (0)
+    if (m <= 8)
+      DLA_TILED_PASS(8);
+    else if (m <= 32)
+      DLA_TILED_PASS(32);
+    else
+      DLA_TILED_PASS(kMaxPeersPerPass);
+#undef DLA_TILED_PASS
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
 }
 
 template <int DT, int KMAX>
@@ -1742,6 +1816,37 @@ int dla_shutdown(void) {
   }
   g_peer_enabled.clear();
   (void)hipGetLastError();
+  return DLA_OK;
+}
+
+int dla_wsum_slab_tiled(int dtype, const void* base, int64_t tile_elems, int64_t slab_rows, const double* weights,
+                        int n_peers, int64_t n_elems, void* out, void* stream, const dla_launch_cfg_t* cfg) {
+  g_last_error.clear();
+  const int es = elem_size(dtype);
+  if (es == 0 || dtype == DLA_F64)
+    return fail(DLA_E_INVALID, "dla_wsum_slab_tiled: dtype must be F32, BF16 or F16");
+  if (!base || !weights || n_peers < 1 || n_peers > slab_rows || n_elems < 0)
+    return fail(DLA_E_INVALID, "dla_wsum_slab_tiled: need base, weights and 1 <= n_peers <= slab_rows");
+  if (tile_elems < 1 || (tile_elems & (tile_elems - 1)) || tile_elems * es < 16)
+    return fail(DLA_E_INVALID, "dla_wsum_slab_tiled: tile_elems must be a power of two of >= 16 bytes");
+  if ((reinterpret_cast<uintptr_t>(base) & 15u) || (reinterpret_cast<uintptr_t>(out) & 15u))
+    return fail(DLA_E_INVALID, "dla_wsum_slab_tiled: base and out must be 16-byte aligned");
+  if (n_elems == 0) return DLA_OK;
+  if (!out) return fail(DLA_E_INVALID, "dla_wsum_slab_tiled: null out");
+  int tshift = 0;
+  while ((int64_t{1} << tshift) < tile_elems) ++tshift;
+  const int variant = cfg && cfg->variant ? cfg->variant : 9;
+  if (variant != 9 && variant != 10 && variant != 12)
+    return fail(DLA_E_CONFIG, "dla_wsum_slab_tiled: variant must be 0 (= 9), 9, 10 or 12");
+  const int64_t stride = slab_rows * tile_elems;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  hipError_t e;
+  switch (dtype) {
+    case DLA_F32: e = run_tiled<DLA_F32>(base, tile_elems, tshift, stride, weights, n_peers, n_elems, out, s, variant); break;
+    case DLA_BF16: e = run_tiled<DLA_BF16>(base, tile_elems, tshift, stride, weights, n_peers, n_elems, out, s, variant); break;
+    default: e = run_tiled<DLA_F16>(base, tile_elems, tshift, stride, weights, n_peers, n_elems, out, s, variant); break;
+  }
+  if (e != hipSuccess) return fail(static_cast<int>(e), std::string("dla_wsum_slab_tiled: ") + hipGetErrorString(e));
   return DLA_OK;
 }
 

@@ -106,6 +106,17 @@ int dla_wsum_ex(int dtype, const void* const* peers, const double* weights, int 
 int dla_wsum_slab(int dtype, const void* base, int64_t pitch_elems, const double* weights,
                   int n_peers, int64_t n_elems, void* out, void* stream);
 
+/* Peers stored in the TILE-INTERLEAVED slab layout (the many-peer PeerSlab layout):
+ * the slab is [n_tiles][slab_rows][tile_elems]; element j of peer (row) k lives at
+ *     base + ((j / tile_elems) * slab_rows + k) * tile_elems + j % tile_elems
+ * so the rows' tiles at one offset sit side by side and a many-peer reduce streams one region
+ * of HBM instead of n_peers distant ones.  Peers 0..n_peers-1 (n_peers <= slab_rows) are
+ * reduced in row order into the contiguous `out` (n_elems elements).  tile_elems: a power of
+ * two of >= 16 bytes; base and out 16-byte aligned; F32, BF16 or F16.  cfg (may be NULL):
+ * variant 9 (default), 10 or 12 picks the vector-per-lane kernel form.  ABI v5. */
+int dla_wsum_slab_tiled(int dtype, const void* base, int64_t tile_elems, int64_t slab_rows, const double* weights,
+                        int n_peers, int64_t n_elems, void* out, void* stream, const dla_launch_cfg_t* cfg);
+
 /* Replaces the per-parameter inner loop of fedavg.py:24-25 for T parameter
  * tensors at once (one model = T tensors, parameters() order).
  *   peer_ptrs host array [n_tensors * n_peers]: peer_ptrs[t * n_peers + k] is

@@ -544,3 +544,41 @@ def fedavg_param_lists_f32(models, w):
     from oracle.fedavg_oracle import fedavg_param_lists
 
     return fedavg_param_lists([[p.detach().cpu().numpy() for p in m.parameters()] for m in models], w, "f32")
+
+
+def _tiled_slab(peers, tile_elems, dtype):
+    """[n_tiles][N][tile] slab holding the peers in the tile-interleaved layout (padding zero)."""
+    n, numel = len(peers), peers[0].numel()
+    n_t = -(-numel // tile_elems)
+    slab = torch.zeros((n_t, n, tile_elems), dtype=TDT[dtype])
+    for k, p in enumerate(peers):
+        pad = torch.zeros(n_t * tile_elems, dtype=TDT[dtype])
+        pad[:numel] = p
+        slab[:, k, :] = pad.view(n_t, tile_elems)
+    return slab.cuda()
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16", "f16"])
+@pytest.mark.parametrize("n", [1, 8, 33, 130])
+@pytest.mark.parametrize("numel", [5, 4097, 300_007])
+@pytest.mark.parametrize("tile_bytes", [16, 1024, 4096])
+def test_tiled_slab_bit_exact(dtype, n, numel, tile_bytes):
+    """dla_wsum_slab_tiled (tile-interleaved PeerSlab layout): every kernel form, ragged tails
+    (tiled addressing in the tail workgroup too), multi-pass peer counts, IEEE specials."""
+    from accdfl_amd import _lib
+    from accdfl_amd.core import wsum
+
+    es = 4 if dtype == "f32" else 2
+    peers = _random_peers(n, numel, dtype, seed=n * 3 + numel)
+    for i, v in enumerate([-0.0, float("inf"), float("-inf"), float("nan"), 1e-40, -3e38]):
+        peers[(3 * i) % n][(11 * i) % numel] = v
+    w = [float(x) for x in np.random.default_rng(n + 7).dirichlet(np.ones(n))]
+    want = c_wsum([_bits(p, dtype) for p in peers], w, dtype)
+    te = tile_bytes // es
+    slab = _tiled_slab(peers, te, dtype)
+    for v in (0, 9, 10, 12):
+        out = torch.empty(numel, dtype=TDT[dtype], device="cuda")
+        _lib.wsum_slab_tiled_ptr(wsum.dtype_code(TDT[dtype]), slab.data_ptr(), te, n, w, numel, out.data_ptr(),
+                                 torch.cuda.current_stream().cuda_stream, _lib.LaunchCfg(v, 0, 0, 0))
+        torch.cuda.synchronize()
+        assert same_bits(_bits(out, dtype), want, dtype), (dtype, n, numel, tile_bytes, v)
