@@ -17,8 +17,10 @@
 Deliberate differences (documented in DESIGN.md): parameters whose shapes or dtypes
 differ between models raise RuntimeError instead of broadcasting / promoting.
 
-Deliberate differences also include: the result's CPU parameters are allocated in
-pinned host memory (``is_pinned()`` is True) so the reduce's D2H lands in them.
+The result's CPU parameters are ordinary pageable tensors as in the reference; during a
+large round they are page-locked in place for the D2H and unlocked before the call returns
+(``core/host_memory.py``: ACCDFL_AMD_RESULT_MEMORY=registered, the default; "pinned" keeps
+them page-locked for good, "pageable" never locks them).
 
 Where the arithmetic runs: always on the HIP device (libdlagg.so).  Models already
 on the device are reduced in place of their parameters with no copies; CPU models
@@ -38,6 +40,7 @@ import torch
 from torch import nn
 
 from accdfl_amd import _lib
+from accdfl_amd.core import host_memory as _host_memory
 from accdfl_amd.core import wsum as _wsum
 from accdfl_amd.core.gradient_aggregation import GradientAggregation
 
@@ -360,35 +363,43 @@ def _reduce_host_staged(devices: List[torch.device], dtype, center: List[torch.T
             st.ensure(n, _round_up(max(e - s, 1), align))
             st.copy_stream.wait_stream(torch.cuda.current_stream(dev))  # previous users of d_in are done
             stages.append(st)
-        # D2H straight into the result's parameters when they are pinned and dense (see
-        # _center_copy); otherwise through one pinned buffer.
-        direct = all(c.is_pinned() and c.is_contiguous() for c in center)
+        # D2H straight into the result's parameters when they are dense: page-locked (mode
+        # "pinned"), page-locked for this call (mode "registered", below) or staged by the
+        # runtime (mode "pageable"); non-dense results go through one pinned buffer.
+        direct = all(c.is_contiguous() for c in center)
         h_out = None if direct else torch.empty(total, dtype=dtype, pin_memory=True)
         jobs = [(st, dev, s, e) for st, dev, (s, e) in zip(stages, devices, bounds) if s < e]
-        if _SHARD_THREADS:
-            from concurrent.futures import ThreadPoolExecutor
-
-            def bucket(job):
-                st, dev, s, e = job
-                with torch.no_grad():  # grad mode is per thread; the result's parameters are leaves
-                    _bucket_pipelined(st, dev, flats, numels, s, e, weights, center, h_out, align)
-
-            if len(jobs) == 1:
-                bucket(jobs[0])
-            else:
-                with ThreadPoolExecutor(max_workers=len(jobs)) as pool:
-                    list(pool.map(bucket, jobs))  # re-raises the first failure
-        else:
-            for k in range(n):  # peer-major: every GPU's DMA starts as early as possible
-                for st, dev, s, e in jobs:
-                    _stage_rows(st, dev, k, flats[k], numels, s, e)
-            for st, dev, s, e in jobs:
-                _reduce_rows(st, dev, weights, center, numels, s, e, h_out)
-            for dev in devices:
-                torch.cuda.current_stream(dev).synchronize()
+        with _host_memory.registered(center if direct else []):
+            _run_bucket_jobs(jobs, devices, flats, numels, weights, center, h_out, align, n)
         if not direct:
             for c, o in zip(center, torch.split(h_out, numels)):
                 c.copy_(o.view_as(c))
+
+
+def _run_bucket_jobs(jobs, devices, flats, numels, weights, center, h_out, align, n):
+    """Every bucket's H2D -> reduce -> D2H, one thread per GPU (pipelined) or peer-major from
+    this thread (packed); returns when every D2H has landed."""
+    if _SHARD_THREADS:
+        from concurrent.futures import ThreadPoolExecutor
+
+        def bucket(job):
+            st, dev, s, e = job
+            with torch.no_grad():  # grad mode is per thread; the result's parameters are leaves
+                _bucket_pipelined(st, dev, flats, numels, s, e, weights, center, h_out, align)
+
+        if len(jobs) == 1:
+            bucket(jobs[0])
+        else:
+            with ThreadPoolExecutor(max_workers=len(jobs)) as pool:
+                list(pool.map(bucket, jobs))  # re-raises the first failure
+    else:
+        for k in range(n):  # peer-major: every GPU's DMA starts as early as possible
+            for st, dev, s, e in jobs:
+                _stage_rows(st, dev, k, flats[k], numels, s, e)
+        for st, dev, s, e in jobs:
+            _reduce_rows(st, dev, weights, center, numels, s, e, h_out)
+        for dev in devices:
+            torch.cuda.current_stream(dev).synchronize()
 
 
 def _reduce_device_resident(dtype, center: List[torch.Tensor], peers: List[List[torch.Tensor]], weights):
@@ -482,9 +493,9 @@ def _center_copy(model0: nn.Module, pin: bool = True) -> nn.Module:
     uninitialised tensors of the same shape, strides, dtype, device and
     ``requires_grad``: the reduce overwrites every one of them, so copying models[0]'s
     values first (and page-faulting P fresh elements: 16 ms of a 35 ms host-inclusive
-    8 x 25 M reduce) is wasted.  CPU parameters are allocated pinned so the result's
-    D2H copy lands in them directly.  Buffers and every other attribute are deep-copied
-    exactly as in the reference."""
+    8 x 25 M reduce) is wasted.  With ``pin`` the CPU parameters are allocated page-locked
+    (result-memory mode "pinned", core/host_memory.py).  Buffers and every other attribute
+    are deep-copied exactly as in the reference."""
     memo = {}
     pin = pin and torch.cuda.is_available()
     for p in model0.parameters():
@@ -514,7 +525,7 @@ class FedAvg(GradientAggregation):
                     return small
             params0 = list(models[0].parameters())
             nbytes = sum(p.numel() * p.element_size() for p in params0) * len(models)
-            center_model = _center_copy(models[0], pin=nbytes >= _SMALL_ROUND_BYTES)
+            center_model = _center_copy(models[0], pin=nbytes >= _SMALL_ROUND_BYTES and _host_memory.pin_results())
             reduce_parameters(list(center_model.parameters()), [list(m.parameters()) for m in models],
                               list(weights))
             return center_model

@@ -23,6 +23,7 @@ import torch
 from torch import nn
 
 from accdfl_amd import _lib
+from accdfl_amd.core import host_memory as _host_memory
 from accdfl_amd.core import wsum as _wsum
 
 _ALIGN_BYTES = 256
@@ -219,10 +220,15 @@ class PeerSlab:
             for p, v in zip(params, self.unflatten(flat)):
                 p.copy_(v)
             return
-        if all(p.is_pinned() and p.is_contiguous() for p in params):
-            for p, v in zip(params, torch.split(flat, self.numels)):
-                p.view(-1).copy_(v, non_blocking=True)  # D2H straight into the result
-            torch.cuda.current_stream(self.device).synchronize()
+        large = self.total * self.buf.element_size() >= 8 * _host_memory.REGISTER_MIN_BYTES
+        if all(p.is_contiguous() and p.device.type == "cpu" for p in params) and (
+                all(p.is_pinned() for p in params) or (large and _host_memory.result_memory() != "pinned")):
+            # D2H straight into the result: page-locked tensors, or (large models) tensors
+            # page-locked for this call only (core/host_memory.py) / staged by the runtime
+            with _host_memory.registered(params):
+                for p, v in zip(params, torch.split(flat, self.numels)):
+                    p.view(-1).copy_(v, non_blocking=True)
+                torch.cuda.current_stream(self.device).synchronize()
             return
         if all(p.is_contiguous() and p.device.type == "cpu" for p in params):  # small rounds: one D2H,
             if self._h_out is None or self._h_out.numel() < self.total:      # one native host scatter

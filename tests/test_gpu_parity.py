@@ -412,6 +412,48 @@ def test_device_model_manager_falls_back_on_mixed_layouts():
         assert same_bits(p.detach().numpy(), q, "f32")
 
 
+def test_device_model_manager_never_averages_stale_rows():
+    """The slab is used only while its rows are the registry's current entries, unchanged: a
+    registry replaced directly (accdfl/dl/community.py:98-104 assigns it) or a model written in
+    place after it arrived is averaged from the registry as the reference reads it at
+    aggregate time."""
+    from types import SimpleNamespace
+
+    from torch import nn
+
+    from accdfl_amd.core.gradient_aggregation import GradientAggregationMethod
+    from accdfl_amd.core.model_manager import DeviceModelManager
+    from oracle.fedavg_oracle import fedavg_param_lists
+
+    torch.manual_seed(5)
+    settings = SimpleNamespace(gradient_aggregation=GradientAggregationMethod.FEDAVG)
+    first = [nn.Linear(7, 4) for _ in range(3)]
+    second = [nn.Linear(7, 4) for _ in range(3)]
+    w = [0.5, 0.3, 0.2]
+
+    def want(models):
+        return fedavg_param_lists([[p.detach().numpy() for p in m.parameters()] for m in models], w, "f32")
+
+    mm = DeviceModelManager(None, settings, capacity=4)
+    for k, m in enumerate(first):
+        mm.process_incoming_trained_model(b"p%d" % k, m)
+    assert mm._uniform()
+    # the DL round: the registry is assigned directly, same peer count, slab rows now stale
+    mm.incoming_trained_models = {b"q%d" % k: m for k, m in enumerate(second)}
+    assert not mm._uniform()
+    for p, q in zip(mm.aggregate_trained_models(w).parameters(), want(second)):
+        assert same_bits(p.detach().numpy(), q, "f32")
+    # a model written in place after it arrived
+    mm = DeviceModelManager(None, settings, capacity=4)
+    for k, m in enumerate(first):
+        mm.process_incoming_trained_model(b"p%d" % k, m)
+    with torch.no_grad():
+        first[1].weight.mul_(3.0)
+    assert not mm._uniform()
+    for p, q in zip(mm.aggregate_trained_models(w).parameters(), want(first)):
+        assert same_bits(p.detach().numpy(), q, "f32")
+
+
 @pytest.mark.parametrize("threads", [True, False])
 @pytest.mark.parametrize("dtype", ["f32", "bf16"])
 def test_host_path_sharded_over_devices(dtype, threads):
@@ -582,3 +624,48 @@ def test_tiled_slab_bit_exact(dtype, n, numel, tile_bytes):
                                  torch.cuda.current_stream().cuda_stream, _lib.LaunchCfg(v, 0, 0, 0))
         torch.cuda.synchronize()
         assert same_bits(_bits(out, dtype), want, dtype), (dtype, n, numel, tile_bytes, v)
+
+
+@pytest.mark.parametrize("mode", ["registered", "pageable", "pinned"])
+def test_result_memory_modes(mode):
+    """Large rounds (>= 64 MB) in each result-memory mode (core/host_memory.py): bit-exact, and
+    the kept results are page-locked only in mode "pinned" — the default ("registered") locks
+    the result's tensors for the D2H and unlocks them before returning, so page-locked memory
+    does not grow with the number of results a caller keeps."""
+    from torch import nn
+
+    from accdfl_amd.core import host_memory
+    from accdfl_amd.core.gradient_aggregation.fedavg import FedAvg
+    from accdfl_amd.core.model_manager import DeviceModelManager
+    from accdfl_amd.core.gradient_aggregation import GradientAggregationMethod
+    from types import SimpleNamespace
+
+    n, big, small = 4, 5_000_003, 1000
+    g = torch.Generator().manual_seed(42)
+    models = []
+    for _ in range(n):
+        m = nn.Module()
+        m.a = nn.Parameter(torch.randn(big, generator=g) * 0.05)
+        m.b = nn.Parameter(torch.randn(small, generator=g) * 0.05)
+        models.append(m)
+    w = [float(x) for x in np.random.default_rng(4).dirichlet(np.ones(n))]
+    want = c_wsum([torch.cat([m.a.detach(), m.b.detach()]).numpy() for m in models], w, "f32")
+    prev = host_memory.result_memory()
+    host_memory.set_result_memory(mode)
+    try:
+        kept = []
+        for _ in range(3):
+            out = FedAvg.aggregate(models, w)
+            kept.append(out)
+            got = torch.cat([out.a.detach(), out.b.detach()]).numpy()
+            assert same_bits(got, want, "f32")
+            assert out.a.is_pinned() == (mode == "pinned")
+        mm = DeviceModelManager(None, SimpleNamespace(gradient_aggregation=GradientAggregationMethod.FEDAVG), 0,
+                                capacity=n)
+        for k, m in enumerate(models):
+            mm.process_incoming_trained_model(b"p%d" % k, m)
+        out = mm.aggregate_trained_models(w)
+        assert same_bits(torch.cat([out.a.detach(), out.b.detach()]).numpy(), want, "f32")
+        assert out.a.is_pinned() == (mode == "pinned")
+    finally:
+        host_memory.set_result_memory(prev)
