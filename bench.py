@@ -24,8 +24,6 @@ Extra objects on the JSON line:
                 "port") on this host's cores, rank 0 at N=1 only, bounded sample
   host_inclusive  FedAvg.aggregate on CPU modules (the reference call sites'
                 situation): pack + H2D + reduce + D2H, rank 0 at N=1 only
-  small_configs device-resident rates of the BASELINE configs 1-2 model sizes
-                (cache-resident / launch-bound; informational)
   baseline_configs  every BASELINE config at its per-GPU share (prepared launch), with
                 the torch-CPU op sequence timed on the same share beside it
   host_inclusive_sharded  (N > 1, rank 0) the CPU-module path bucket-sharded over GPUs
@@ -63,11 +61,6 @@ NS_PEERS = 8
 NS_PARAMS = 25_000_000
 PMC_FILE = os.path.join(ROOT, "profiles", "pmc_traffic.json")
 
-SMALL = {  # BASELINE configs[1] / configs[2] parameter counts
-    "cifar10_gnlenet_n8": (8, 85_354),
-    "femnist_cnn_n32": (32, 1_690_046),
-}
-
 # Every BASELINE.json config as the share ONE GPU reduces: name ->
 # (peers, params of the whole model, dtype, GPUs the config names).  A G-GPU config's
 # per-GPU share is its parameter bucket: params / G of every peer.
@@ -104,6 +97,9 @@ def parse():
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) for real runs; gloo only to rehearse "
                                                              "several ranks on one GPU")
     ap.add_argument("--no-strong", action="store_true", help="skip the strong-scaling (fixed-model) lines")
+    ap.add_argument("--layout", default="slab", choices=["slab", "rows"],
+                    help="HBM layout of the headline's peers: the PeerSlab tile-interleaved slab (default) or "
+                         "one buffer per peer")
     ap.add_argument("--strong-steps", type=int, default=20)
     ap.add_argument("--dry-run", action="store_true",
                     help="launch + rendezvous + rank-count check + bucket split only, no GPU work "
@@ -133,6 +129,10 @@ def spawn_ranks(args) -> int:
     env = dict(os.environ, BENCH_SELF_SPAWNED="1", HSA_ENABLE_IPC_MODE_LEGACY="0")
     env.setdefault("OMP_NUM_THREADS", str(max(1, (os.cpu_count() or 1) // args.gpus)))
     return subprocess.call(cmd, env=env)
+
+
+def args_cfg(args):
+    return (args.variant, args.chunks, args.grid, args.block)
 
 
 def setup_dist(args):
@@ -188,6 +188,44 @@ def make_slab(n, p, dtype, device, seed_base):
         g = torch.Generator(device=device).manual_seed(seed_base + k)
         slab[k].normal_(0.0, 0.05, generator=g)
     return slab
+
+
+class SlabInput:
+    """n peers x p elements resident in HBM as PeerSlab holds them (core/peer_slab.py) and a
+    prepared reduce of them into ``out``: layout "slab" = the tile-interleaved slab
+    [n_tiles, n, tile] (fp32 / bf16 / f16; dla_wsum_slab_tiled), "rows" = one row per peer
+    (separate peer buffers, what FedAvg.aggregate on device modules reduces; dla_wsum)."""
+
+    def __init__(self, n, p, dt, device, seed_base, weights, layout="slab"):
+        from accdfl_amd import _lib
+        from accdfl_amd.core import wsum
+
+        code = wsum.dtype_code(dt)
+        pitch = max(128, (p + 127) // 128 * 128)
+        rows = make_slab(n, pitch, dt, device, seed_base)
+        self.out = torch.empty(pitch, dtype=dt, device=device)
+        self.layout = layout if dt != torch.float64 else "rows"
+        if self.layout == "slab":
+            self.tile = _lib.slab_tile_elems(code, n, p)
+            n_t = max(1, -(-p // self.tile))
+            self.buf = torch.empty((n_t, n, self.tile), dtype=dt, device=device)
+            full = p // self.tile
+            for k in range(n):
+                if full:
+                    self.buf[:full, k, :].copy_(rows[k, : full * self.tile].view(full, self.tile))
+                if p > full * self.tile:
+                    self.buf[full, k, : p - full * self.tile].copy_(rows[k, full * self.tile: p])
+            del rows
+            self.plan = _lib.TiledPlan(code, self.buf.data_ptr(), self.tile, n, weights, p, self.out.data_ptr())
+            self.kernel = "wsum_vec_kernel (tile-interleaved slab, %d-B tiles)" % (self.tile * self.buf.element_size())
+        else:
+            self.buf = rows
+            self.tile = 0
+            self.plan = _lib.Plan(code, [rows[k].data_ptr() for k in range(n)], weights, p, self.out.data_ptr())
+            self.kernel = _lib.select_kernel(code, n, p)
+
+    def launch(self, stream_ptr):
+        self.plan.launch(stream_ptr)
 
 
 def time_kernel(fn, steps, warmup, world):
@@ -585,8 +623,8 @@ def time_graph(launch, per_graph=20, reps=10):
 
 
 def baseline_configs(device, steps=50, cpu=True):
-    """Device-resident reduce rate of each BASELINE config's per-GPU share, through a
-    prepared dla_plan (bytes = (N + 1) * share * sizeof), beside the reference op sequence
+    """Device-resident reduce rate of each BASELINE config's per-GPU share staged as PeerSlab
+    holds it (SlabInput, a prepared launch; bytes = (N + 1) * share * sizeof), beside the reference op sequence
     on the host's cores for the same share (flat, one tensor per peer: a lower bound on
     the reference's per-tensor loop, which pays T dispatches per peer)."""
     from accdfl_amd import _lib
@@ -596,20 +634,17 @@ def baseline_configs(device, steps=50, cpu=True):
         dt = torch.float32 if dts == "f32" else torch.bfloat16
         es = 4 if dts == "f32" else 2
         share = -(-params // gpus)
-        pitch = (share + 127) // 128 * 128
-        slab = make_slab(n, pitch, dt, device, 1000)
-        out = torch.empty(share, dtype=dt, device=device)
-        plan = _lib.Plan(_lib.DLA_F32 if dts == "f32" else _lib.DLA_BF16, [slab[k].data_ptr() for k in range(n)],
-                         [float(1.0 / n)] * n, share, out.data_ptr())
+        inp = SlabInput(n, share, dt, device, 1000, [float(1.0 / n)] * n)
         sp = torch.cuda.current_stream().cuda_stream
-        _, ev = time_kernel(lambda: plan.launch(sp), steps, 10, 1)
-        tg = time_graph(plan.launch)
+        _, ev = time_kernel(lambda: inp.launch(sp), steps, 10, 1)
+        tg = time_graph(inp.launch)
         byts = (n + 1) * share * es
         res[name] = {"peers": n, "params_per_gpu": share, "dtype": dts, "us_per_reduce": round(ev / steps * 1e6, 2),
                      "GB/s": round(byts / (ev / steps) / 1e9, 1), "bytes": byts,
                      "us_per_reduce_graph": round(tg * 1e6, 2), "GB/s_graph": round(byts / tg / 1e9, 1),
-                     "regime": "HBM" if byts > 256 << 20 else "Infinity-Cache / launch-latency"}
-        del slab, out, plan
+                     "regime": "HBM" if byts > 256 << 20 else "Infinity-Cache / launch-latency",
+                     "kernel": inp.kernel}
+        del inp
         torch.cuda.empty_cache()
         if cpu:
             ms, threads = _cpu_port_ms(n, share, dt)
@@ -654,24 +689,18 @@ def strong_scaling(rank, world, device, steps, warmup):
         set_bytes = (n + 1) * pitch * es
         copies = 1 if set_bytes >= _ROTATE_BYTES else min(64, -(-_ROTATE_BYTES // set_bytes))
         w = [float(x) for x in np.random.default_rng(0).dirichlet(np.ones(n))]
-        slabs, outs, plans = [], [], []
-        for c in range(copies):
-            slabs.append(make_slab(n, pitch, dt, device, 1000 + 131 * c + 7 * rank))
-            outs.append(torch.empty(pitch, dtype=dt, device=device))
-            if m:
-                plans.append(_lib.Plan(wsum.dtype_code(dt), [slabs[c][k].data_ptr() for k in range(n)], w, m,
-                                       outs[c].data_ptr()))
+        inputs = [SlabInput(n, m, dt, device, 1000 + 131 * c + 7 * rank, w) for c in range(copies)] if m else []
         sp = torch.cuda.current_stream().cuda_stream
         ctr = [0]
 
         def step_rot():
-            if plans:
-                plans[ctr[0] % len(plans)].launch(sp)
+            if inputs:
+                inputs[ctr[0] % len(inputs)].launch(sp)
             ctr[0] += 1
 
         def step_warm():
-            if plans:
-                plans[0].launch(sp)
+            if inputs:
+                inputs[0].launch(sp)
 
         wall, ev = time_kernel(step_rot, steps, warmup, world)
         wall_w, _ = time_kernel(step_warm, steps, warmup, world)
@@ -684,7 +713,8 @@ def strong_scaling(rank, world, device, steps, warmup):
                "input_copies_rotated": copies,
                "cache_warm_value": round(total / (wall_w / steps) / 1e9, 2),
                "regime": "HBM" if (n + 1) * (bounds[0][1] - bounds[0][0]) * es > _MALL_BYTES
-               else "bucket fits the Infinity Cache; rotated copies keep it HBM-resident"}
+               else "bucket fits the Infinity Cache; rotated copies keep it HBM-resident",
+               "kernel": inputs[0].kernel if inputs else None}
         if world > 1:
             try:
                 cdev = device if dist.get_backend() == "nccl" else torch.device("cpu")  # gloo: host tensors
@@ -698,7 +728,7 @@ def strong_scaling(rank, world, device, steps, warmup):
             except Exception as exc:  # never lose the line to the auxiliary leg
                 row["allgather_error"] = "%s: %s" % (type(exc).__name__, exc)
         res[name] = row
-        del slabs, outs, plans
+        del inputs
         torch.cuda.empty_cache()
     return res
 
@@ -720,25 +750,6 @@ def dry_run(args, rank, world):
                           "buckets": {name: [g[name] for g in got] for name in STRONG}}), flush=True)
     if world > 1:
         dist.destroy_process_group()
-
-
-def small_configs(device, steps=200):
-    """Device-resident reduces at the BASELINE configs' own model sizes, launched through a
-    prepared dla_plan (what a PeerSlab round pays)."""
-    from accdfl_amd import _lib
-
-    res = {}
-    for name, (n, p) in SMALL.items():
-        slab = make_slab(n, (p + 63) // 64 * 64, torch.float32, device, 1000)
-        w = [float(1.0 / n)] * n
-        out = torch.empty(p, dtype=torch.float32, device=device)
-        plan = _lib.Plan(_lib.DLA_F32, [slab[k].data_ptr() for k in range(n)], w, p, out.data_ptr())
-        sp = torch.cuda.current_stream().cuda_stream
-        wall, ev = time_kernel(lambda: plan.launch(sp), steps, 20, 1)
-        res[name] = {"GB/s": round((n + 1) * p * 4 / (ev / steps) / 1e9, 1), "us_per_reduce": round(ev / steps * 1e6, 2),
-                     "bytes": (n + 1) * p * 4, "note": "fits the 256 MiB Infinity Cache; launch/latency-bound"}
-        del slab
-    return res
 
 
 def sweep(args, device):
@@ -937,19 +948,22 @@ def main():
     dt = {"f32": torch.float32, "bf16": torch.bfloat16, "f16": torch.float16}[args.dtype]
     es = 4 if args.dtype == "f32" else 2
     n, p = args.peers, args.params
-    # this rank's bucket of every peer: rows of one [n, pitch] slab (16-B aligned rows)
-    pitch = (p + 63) // 64 * 64
-    slab = make_slab(n, pitch, dt, device, 1000 + 97 * rank)
-    out = torch.empty(p, dtype=dt, device=device)
+    # this rank's bucket of every peer, resident in HBM as PeerSlab stages it: the
+    # tile-interleaved slab (core/peer_slab.py; --layout rows: one buffer per peer)
     w = [float(x) for x in np.random.default_rng(0).dirichlet(np.ones(n))]
     cfg = None
     if args.variant or args.chunks or args.grid or args.block:
         cfg = _lib.LaunchCfg(args.variant, args.chunks, args.grid, args.block)
-    ptrs = [slab[k].data_ptr() for k in range(n)]
     code = wsum.dtype_code(dt)
+    inp = SlabInput(n, p, dt, device, 1000 + 97 * rank, w, layout="rows" if cfg is not None else args.layout)
+    if cfg is not None:
+        ptrs = [inp.buf[k].data_ptr() for k in range(n)]
 
-    def step():
-        _lib.wsum_ptrs(code, ptrs, w, p, out.data_ptr(), torch.cuda.current_stream().cuda_stream, cfg)
+        def step():
+            _lib.wsum_ptrs(code, ptrs, w, p, inp.out.data_ptr(), torch.cuda.current_stream().cuda_stream, cfg)
+    else:
+        def step():
+            inp.launch(torch.cuda.current_stream().cuda_stream)
 
     log("headline: %d peers x %d %s, %d ranks" % (n, p, args.dtype, world))
     wall, ev = time_kernel(step, args.steps, args.warmup, world)
@@ -962,7 +976,8 @@ def main():
     if os.path.exists(PMC_FILE):
         try:
             pm = json.load(open(PMC_FILE))
-            if pm.get("workload") == "ns" and pm.get("peers") == n and pm.get("params") == p:
+            if (pm.get("workload") == "ns" and pm.get("peers") == n and pm.get("params") == p
+                    and pm.get("layout", "rows") == inp.layout and cfg is None):
                 traffic = pm.get("hbm_bytes_per_launch")
         except (OSError, ValueError):
             traffic = None
@@ -987,11 +1002,13 @@ def main():
             "params_per_gpu": p,
             "global_params": p * world,
             "parallelism": "bucket-sharded x%d (no data-path collective)" % world,
+            "hbm_layout": ("PeerSlab tile-interleaved slab [n_tiles][%d peers][%d-element tiles]" % (n, inp.tile)
+                           if inp.layout == "slab" else "one buffer per peer"),
         },
         "launch": launch_info(world),
         "roofline": {
             "bound": "hbm",
-            "kernel": _lib.select_kernel(code, n, p) if cfg is None else "wsum_stream_kernel (forced launch cfg)",
+            "kernel": inp.kernel if cfg is None else "forced launch cfg %s" % (tuple(args_cfg(args)),),
             "achieved": round(achieved, 1),
             "peak": HBM_PEAK_GBPS,
             "unit": "GB/s",
@@ -1001,8 +1018,17 @@ def main():
             "us_per_launch": round(kern_s * 1e6, 2),
         },
     }
-    del slab
+    del inp
     torch.cuda.empty_cache()
+    if cfg is None and args.layout == "slab":
+        # the same peers as separate buffers (what FedAvg.aggregate on device modules reduces)
+        rows = SlabInput(n, p, dt, device, 1000 + 97 * rank, w, layout="rows")
+        _, ev_r = time_kernel(lambda: rows.launch(torch.cuda.current_stream().cuda_stream), args.steps,
+                              args.warmup, world)
+        result["separate_buffers"] = {"kernel": rows.kernel, "us_per_launch": round(ev_r / args.steps * 1e6, 2),
+                                      "GB/s": round(bytes_step / (ev_r / args.steps) / 1e9, 1)}
+        del rows
+        torch.cuda.empty_cache()
     if not args.no_strong and args.dtype == "f32" and (n, p) == (NS_PEERS, NS_PARAMS):
         log("strong-scaling lines")
         result["strong_scaling"] = {"scaling": "strong",
@@ -1024,8 +1050,7 @@ def main():
         dist.barrier(group=cpu_group)
     if rank == 0 and world == 1:
         if not args.no_small:
-            log("small / baseline configs")
-            result["small_configs"] = small_configs(device)
+            log("baseline configs")
             result["baseline_configs"] = baseline_configs(device)
         if not args.no_host_inclusive and args.dtype == "f32":
             log("host-inclusive legs")

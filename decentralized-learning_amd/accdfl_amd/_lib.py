@@ -55,6 +55,7 @@ EXPORTED = (
     "dla_shard_range",
     "dla_shutdown",
     "dla_wsum_slab_tiled",
+    "dla_slab_tile_elems",
 )
 
 
@@ -175,6 +176,8 @@ class _Lib:
                                            ctypes.POINTER(ctypes.c_double), ctypes.c_int, ctypes.c_int64, vp, vp,
                                            ctypes.POINTER(LaunchCfg)]
         so.dla_wsum_slab_tiled.restype = ctypes.c_int
+        so.dla_slab_tile_elems.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int64]
+        so.dla_slab_tile_elems.restype = ctypes.c_int64
         so.dla_plan_destroy.argtypes = [vp]
         so.dla_plan_destroy.restype = None
         v = so.dla_version()
@@ -312,6 +315,11 @@ def wsum_slab_tiled_ptr(dtype_code: int, base_ptr: int, tile_elems: int, slab_ro
     L.check(rc, "dla_wsum_slab_tiled")
 
 
+def slab_tile_elems(dtype_code: int, slab_rows: int, n_elems: int) -> int:
+    """dla_slab_tile_elems: the recommended tile of a tile-interleaved slab."""
+    return int(lib().so.dla_slab_tile_elems(dtype_code, slab_rows, n_elems))
+
+
 def shard_range(dtype_code: int, n_elems: int, n_shards: int, shard: int):
     """dla_shard_range: (start, end) of a shard's bucket."""
     L = lib()
@@ -357,3 +365,29 @@ class Plan:
         if h is not None and h.value:
             self._so.dla_plan_destroy(h)
             self._h = None
+
+
+class TiledPlan:
+    """A prepared dla_wsum_slab_tiled call: the argument arrays are built once, so a round
+    that reduces the same tiled slab again pays only the call (the tiled counterpart of Plan)."""
+
+    def __init__(self, dtype_code: int, base_ptr: int, tile_elems: int, slab_rows: int, weights: Sequence[float],
+                 n_elems: int, out_ptr: int, cfg: Optional[LaunchCfg] = None):
+        L = lib()
+        self._so = L.so
+        self._check = L.check
+        self.n_peers = len(weights)
+        self._args = [dtype_code, base_ptr, tile_elems, slab_rows, _dbl_array(weights), self.n_peers, n_elems,
+                      out_ptr]
+        self._cfg = ctypes.byref(cfg) if cfg is not None else None
+        self._keep = cfg
+
+    def set_weights(self, weights: Sequence[float]) -> None:
+        if len(weights) != self.n_peers:
+            raise AssertionError("len(weights) != n_peers")
+        self._args[4] = _dbl_array(weights)
+
+    def launch(self, stream_ptr: int) -> None:
+        rc = self._so.dla_wsum_slab_tiled(*self._args, stream_ptr, self._cfg)
+        if rc != 0:
+            self._check(rc, "dla_wsum_slab_tiled")

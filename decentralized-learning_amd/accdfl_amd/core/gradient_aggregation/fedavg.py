@@ -17,10 +17,9 @@
 Deliberate differences (documented in DESIGN.md): parameters whose shapes or dtypes
 differ between models raise RuntimeError instead of broadcasting / promoting.
 
-The result's CPU parameters are ordinary pageable tensors as in the reference; during a
-large round they are page-locked in place for the D2H and unlocked before the call returns
-(``core/host_memory.py``: ACCDFL_AMD_RESULT_MEMORY=registered, the default; "pinned" keeps
-them page-locked for good, "pageable" never locks them).
+The result's CPU parameters are ordinary pageable tensors as in the reference
+(``core/host_memory.py``: ACCDFL_AMD_RESULT_MEMORY=pageable, the default; "pinned" allocates
+a large round's result page-locked, which is faster but keeps it page-locked for good).
 
 Where the arithmetic runs: always on the HIP device (libdlagg.so).  Models already
 on the device are reduced in place of their parameters with no copies; CPU models
@@ -364,13 +363,12 @@ def _reduce_host_staged(devices: List[torch.device], dtype, center: List[torch.T
             st.copy_stream.wait_stream(torch.cuda.current_stream(dev))  # previous users of d_in are done
             stages.append(st)
         # D2H straight into the result's parameters when they are dense: page-locked (mode
-        # "pinned"), page-locked for this call (mode "registered", below) or staged by the
-        # runtime (mode "pageable"); non-dense results go through one pinned buffer.
+        # "pinned") or staged by the runtime (mode "pageable"); non-dense results go through
+        # one pinned buffer.
         direct = all(c.is_contiguous() for c in center)
         h_out = None if direct else torch.empty(total, dtype=dtype, pin_memory=True)
         jobs = [(st, dev, s, e) for st, dev, (s, e) in zip(stages, devices, bounds) if s < e]
-        with _host_memory.registered(center if direct else []):
-            _run_bucket_jobs(jobs, devices, flats, numels, weights, center, h_out, align, n)
+        _run_bucket_jobs(jobs, devices, flats, numels, weights, center, h_out, align, n)
         if not direct:
             for c, o in zip(center, torch.split(h_out, numels)):
                 c.copy_(o.view_as(c))

@@ -4,16 +4,22 @@ The reference keeps received models as CPU ``nn.Module``s in an insertion-ordere
 dict (accdfl/core/model_manager.py:39-47) and only touches their bytes when the
 round's aggregation runs (fedavg.py:23-25).  On MI355X the better moment to move a
 model's bytes is when it ARRIVES: ``stage()`` flattens the model's parameters
-(``parameters()`` order — the order fedavg.py:24 zips them in) into a pinned bounce
-buffer and enqueues the H2D copy on a dedicated copy stream, so transfers overlap
-the wait for the other peers.  ``reduce()`` is then one device-resident launch of
-the libdlagg kernel over rows 0..n-1 (arrival order = summation order).
+(``parameters()`` order — the order fedavg.py:24 zips them in) and enqueues the H2D copy
+on a dedicated copy stream, so transfers overlap the wait for the other peers.
+``reduce()`` is then one device-resident launch of the libdlagg kernel over rows 0..n-1
+(arrival order = summation order).
 
-HBM layout: ``buf`` is a row-major [capacity, pitch] slab of the parameter dtype;
-``pitch`` is the flat parameter count rounded up to 256 bytes so every row starts
-16-byte aligned (the kernel's dwordx4 path).  A 25 M-parameter fp32 model is a
-100 MB row; 288 GB of HBM holds ~2800 of them, so capacity is never the constraint
-at accdfl's sample sizes.
+HBM layout.  fp32 / bf16 / f16 slabs are TILE-INTERLEAVED:
+``buf`` is [n_tiles, capacity, tile] — row k's elements [t*tile, (t+1)*tile) sit at
+``buf[t, k]``, so the tiles of every peer at one offset are adjacent and the reduce
+(dla_wsum_slab_tiled) streams one region of HBM at a time instead of ``capacity`` regions
+100 MB apart: 8 x 25 M fp32 130.2 us against 135.6 for separate rows, 128 x 21.3 M bf16
+792 against 869 (profiles/r02d_ab_tiled.log).  ``tile`` is dla_slab_tile_elems (1-16 KiB).
+A row is staged contiguously on the device first and scattered into its tiles by one
+device copy (HBM speed, on the copy stream).  fp64 slabs keep one row per peer
+([capacity, pitch], pitch = the parameter count rounded up to 256 bytes).  A 25 M-parameter
+fp32 model is a 100 MB row; 288 GB of HBM holds ~2800 of them, so capacity is never the
+constraint at accdfl's sample sizes.
 """
 from __future__ import annotations
 
@@ -23,7 +29,6 @@ import torch
 from torch import nn
 
 from accdfl_amd import _lib
-from accdfl_amd.core import host_memory as _host_memory
 from accdfl_amd.core import wsum as _wsum
 
 _ALIGN_BYTES = 256
@@ -32,9 +37,9 @@ _ALIGN_BYTES = 256
 class PeerSlab:
 
     def __init__(self, shapes: Sequence[Sequence[int]], dtype: torch.dtype, capacity: int = 8,
-                 device: Optional[torch.device] = None):
+                 device: Optional[torch.device] = None, layout: str = "auto"):
         self.device = _wsum.require_device(device)
-        _wsum.dtype_code(dtype)
+        self.code = _wsum.dtype_code(dtype)
         self.dtype = dtype
         self.shapes = [tuple(int(d) for d in s) for s in shapes]
         self.numels = [int(torch.Size(s).numel()) for s in self.shapes]
@@ -42,16 +47,40 @@ class PeerSlab:
         esize = torch.empty((), dtype=dtype).element_size()
         align = _ALIGN_BYTES // esize
         self.pitch = max(align, (self.total + align - 1) // align * align)
+        if layout == "auto":
+            layout = "rows" if dtype == torch.float64 else "tiled"
+        if layout not in ("tiled", "rows") or (layout == "tiled" and dtype == torch.float64):
+            raise ValueError("PeerSlab layout must be 'tiled' (fp32/bf16/f16) or 'rows'")
+        self.layout = layout
         self.capacity = max(1, int(capacity))
-        self.buf = torch.empty((self.capacity, self.pitch), dtype=dtype, device=self.device)
+        self.tile = 0
+        self.buf = self._alloc(self.capacity)
         self.n = 0
         self.copy_stream = torch.cuda.Stream(self.device)
         self._bounce = [None, None]
         self._bounce_ev = [None, None]
+        self._row_stage = None      # contiguous device row a tiled stage lands in before its scatter
         self._h_out = None
         self._flat = None          # device result of reduce_into (reused every round)
         self._plan = None          # prepared launch over (rows 0..n-1, _flat)
         self._plan_key = None
+
+    def _alloc(self, capacity: int) -> torch.Tensor:
+        if self.layout == "rows":
+            return torch.empty((capacity, self.pitch), dtype=self.dtype, device=self.device)
+        self.tile = max(1, _lib.slab_tile_elems(self.code, capacity, self.total))
+        n_tiles = max(1, -(-self.total // self.tile))
+        return torch.empty((n_tiles, capacity, self.tile), dtype=self.dtype, device=self.device)
+
+    def _tiles_of(self, buf: torch.Tensor, k: int) -> torch.Tensor:
+        """Row k of a tiled slab as a [n_tiles, tile] view."""
+        return buf[:, k, :]
+
+    def row(self, k: int) -> torch.Tensor:
+        """Row k's ``total`` elements as a contiguous device tensor (a copy for tiled slabs)."""
+        if self.layout == "rows":
+            return self.buf[k, : self.total]
+        return self._tiles_of(self.buf, k).reshape(-1)[: self.total]
 
     # ------------------------------------------------------------------ creation
     @classmethod
@@ -73,15 +102,33 @@ class PeerSlab:
     # ------------------------------------------------------------------- staging
     def _grow(self, rows: int):
         cap = max(rows, 2 * self.capacity)
-        new = torch.empty((cap, self.pitch), dtype=self.dtype, device=self.device)
         cur = torch.cuda.current_stream(self.device)
         self.copy_stream.wait_stream(cur)
         with torch.cuda.stream(self.copy_stream):
+            old, old_tile = self.buf, self.tile
+            new = self._alloc(cap)  # a tiled slab may change its tile with the row count
             if self.n:
-                new[: self.n].copy_(self.buf[: self.n])
-        self.buf.record_stream(self.copy_stream)
+                if self.layout == "rows":
+                    new[: self.n].copy_(old[: self.n])
+                elif self.tile == old_tile:
+                    new[:, : self.n, :].copy_(old[:, : self.n, :])
+                else:
+                    for k in range(self.n):
+                        flat = self._tiles_of(old, k).reshape(-1)[: self.total]
+                        self._scatter(new, k, flat)
+        old.record_stream(self.copy_stream)
         self.buf = new
         self.capacity = cap
+
+    def _scatter(self, buf: torch.Tensor, k: int, flat: torch.Tensor):
+        """Contiguous row (``total`` elements, on the device) -> row k's tiles (copy stream)."""
+        full = self.total // self.tile
+        tiles = self._tiles_of(buf, k)
+        if full:
+            tiles[:full].copy_(flat[: full * self.tile].view(full, self.tile))
+        rest = self.total - full * self.tile
+        if rest:
+            tiles[full, :rest].copy_(flat[full * self.tile:])
 
     def _bounce_buffer(self, slot: int) -> torch.Tensor:
         ev = self._bounce_ev[slot]
@@ -118,6 +165,12 @@ class PeerSlab:
             self._grow(row + 1)
         cur = torch.cuda.current_stream(self.device)
         self.copy_stream.wait_stream(cur)
+        if self.layout == "rows":
+            dst_row = self.buf[row]
+        else:
+            if self._row_stage is None:
+                self._row_stage = torch.empty(self.pitch, dtype=self.dtype, device=self.device)
+            dst_row = self._row_stage
         if all(t.device.type == "cpu" for t in flat):
             esize = self.buf.element_size()
             slot = row & 1
@@ -131,7 +184,7 @@ class PeerSlab:
                     if not small and run_start is not None:  # flush the run of small tensors
                         _lib.host_copy_batch(*pending)
                         pending = ([], [], [])
-                        self.buf[row, run_start:off].copy_(bounce[run_start:off], non_blocking=True)
+                        dst_row[run_start:off].copy_(bounce[run_start:off], non_blocking=True)
                         run_start = None
                     if t is None:
                         break
@@ -144,20 +197,23 @@ class PeerSlab:
                         pending[1].append(t.data_ptr())
                         pending[2].append(t.numel() * esize)
                     else:
-                        self.buf[row, off:off + t.numel()].copy_(t)  # pageable H2D, no host copy
+                        dst_row[off:off + t.numel()].copy_(t)  # pageable H2D, no host copy
                     off += t.numel()
                 if bounce is not None:
                     ev = torch.cuda.Event()
                     ev.record(self.copy_stream)
                     self._bounce_ev[slot] = ev
         else:
-            dst = self.buf[row, : self.total]
+            dst = dst_row[: self.total]
             with torch.cuda.stream(self.copy_stream):
                 src = [t.to(self.device, non_blocking=True) for t in flat]
                 if len(src) == 1:
                     dst.copy_(src[0])
                 else:
                     torch.cat(src, out=dst)
+        if self.layout == "tiled":
+            with torch.cuda.stream(self.copy_stream):  # behind this row's H2D, before the next stage
+                self._scatter(self.buf, row, self._row_stage[: self.total])
         self.n = row + 1
         return row
 
@@ -177,7 +233,16 @@ class PeerSlab:
             raise IndexError("list index out of range")
         cur = torch.cuda.current_stream(self.device)
         cur.wait_stream(self.copy_stream)
-        return _wsum.wsum_rows(self.buf, weights, self.total, out=out)
+        if self.layout == "rows":
+            return _wsum.wsum_rows(self.buf, weights, self.total, out=out)
+        if out is None:
+            out = torch.empty(self.total, dtype=self.dtype, device=self.device)
+        if out.device != self.device or out.dtype != self.dtype or out.numel() < self.total or not out.is_contiguous():
+            raise ValueError("out must be a contiguous %s tensor of >= %d elements on %s"
+                             % (self.dtype, self.total, self.device))
+        _lib.wsum_slab_tiled_ptr(self.code, self.buf.data_ptr(), self.tile, self.capacity, weights, self.total,
+                                 out.data_ptr(), int(cur.cuda_stream))
+        return out
 
     def _offsets(self) -> List[int]:
         offs, o = [], 0
@@ -201,6 +266,8 @@ class PeerSlab:
             raise IndexError("list index out of range")
         if self._flat is None:
             self._flat = torch.empty(self.pitch, dtype=self.dtype, device=self.device)
+        if self.layout == "tiled":
+            return self.reduce(weights, out=self._flat)[: self.total]
         key = (n, self.buf.data_ptr(), self._flat.data_ptr())
         if self._plan_key != key:
             ptrs = [self.buf[k].data_ptr() for k in range(n)]
@@ -220,15 +287,14 @@ class PeerSlab:
             for p, v in zip(params, self.unflatten(flat)):
                 p.copy_(v)
             return
-        large = self.total * self.buf.element_size() >= 8 * _host_memory.REGISTER_MIN_BYTES
+        large = self.total * self.buf.element_size() >= 8 << 20
         if all(p.is_contiguous() and p.device.type == "cpu" for p in params) and (
-                all(p.is_pinned() for p in params) or (large and _host_memory.result_memory() != "pinned")):
-            # D2H straight into the result: page-locked tensors, or (large models) tensors
-            # page-locked for this call only (core/host_memory.py) / staged by the runtime
-            with _host_memory.registered(params):
-                for p, v in zip(params, torch.split(flat, self.numels)):
-                    p.view(-1).copy_(v, non_blocking=True)
-                torch.cuda.current_stream(self.device).synchronize()
+                all(p.is_pinned() for p in params) or large):
+            # D2H straight into the result: page-locked tensors (result-memory mode "pinned") or,
+            # for large models, pageable ones through the runtime's staging (core/host_memory.py)
+            for p, v in zip(params, torch.split(flat, self.numels)):
+                p.view(-1).copy_(v, non_blocking=True)
+            torch.cuda.current_stream(self.device).synchronize()
             return
         if all(p.is_contiguous() and p.device.type == "cpu" for p in params):  # small rounds: one D2H,
             if self._h_out is None or self._h_out.numel() < self.total:      # one native host scatter

@@ -978,6 +978,15 @@ void shape_for(int64_t n_chunks, int n_peers, int elems_per_chunk, int* block, i
 //    per-GPU share: 115.1 -> 111.4 us; 128 x 665 511 bf16: 35.4 -> 32.3 us).
 // f32 shares of >= 128 K chunks keep the stream (32 x 1 690 046: 34.5 vs 35.8 us; 64 x 1 233 086:
 // 48.2 vs 52.4 us).  Interleaved A/B on MI355X: profiles/r01_ab_wide*.log.
+// Passes of more than 8 peers in fp32 / bf16 / f16 take the vector-per-lane kernel (8 bytes per
+// lane per load): 32 peers in flight per lane for passes of >= 32 peers (variant 9), else 16
+// (variant 12: a 32-slot round would reload the last peer into every unused slot).  Interleaved
+// A/B on MI355X against the word-per-lane kernel / 16-byte stream this replaces (us,
+// profiles/r02b_ab_vec.log): 128 x 2 662 045 bf16 106.2 vs 109.9, 128 x 21.3 M bf16 840.5 vs
+// 857.6, 128 x 665 511 bf16 27.6 vs 30.4, 16 x 21.3 M bf16 112.4 vs 118.9, 32 x 1 690 046 f32
+// 33.4 vs 34.4, 64 x 1 233 086 f32 48.4 vs 48.4, 128 x 85 354 f32 10.9 vs 11.1.
+int vec_variant(int n_peers) { return n_peers >= 32 ? 9 : 12; }
+
 constexpr int64_t kWideMaxChunks = 64 * 1024;
 bool use_wide(int64_t n_chunks, int n_peers, int elems_per_chunk) {
   if (n_peers <= kGroup) return false;
@@ -1258,6 +1267,12 @@ hipError_t launch_pass(const PeerTable<typename Ops<DT>::w_t, KMAX>& tab, int n,
   }
   if (l.variant >= 9 && l.variant <= 12) {
     if constexpr (DT != DLA_F64 && KMAX != 8) return launch_vec<DT, KMAX, ACC_IN>(tab, n, n_elems, out, s, l.variant);
+  }
+  if constexpr (DT != DLA_F64 && KMAX != 8) {
+    // more than 8 peers: the vector-per-lane kernel, unless an fp32 big tile applies (below)
+    const bool big = DT == DLA_F32 && !ACC_IN && (n == 16 || n == 32) &&
+                     use_bigtile(n_elems / Ops<DT>::E, Ops<DT>::E, n) != 0;
+    if (l.auto_kernel && !big) return launch_vec<DT, KMAX, ACC_IN>(tab, n, n_elems, out, s, vec_variant(n));
   }
   if (l.variant == 8 || (l.auto_kernel && use_wide(n_elems / Ops<DT>::E, n, Ops<DT>::E)))
     return launch_wide<DT, KMAX, ACC_IN>(tab, n, n_elems, out, s);
@@ -1644,6 +1659,9 @@ const char* dla_select_kernel(int dtype, int n_peers, int64_t n_elems) {
   if (es == 0 || n_peers < 1 || n_elems < 0) return "";
   const int e = 16 / es;  // elements per 16-byte chunk
   const int first_pass = n_peers < kMaxPeersPerPass ? n_peers : kMaxPeersPerPass;
+  if (dtype != DLA_F64 && first_pass > 8 &&
+      !(dtype == DLA_F32 && (first_pass == 16 || first_pass == 32) && use_bigtile(n_elems / e, e, n_peers)))
+    return "wsum_vec_kernel";
   if (use_wide(n_elems / e, first_pass, e)) return "wsum_wide_kernel";
   if ((dtype == DLA_F32 || dtype == DLA_F64) && use_bigtile(n_elems / e, e, n_peers))
     return "wsum_bigtile_kernel";
@@ -1835,7 +1853,8 @@ int dla_wsum_slab_tiled(int dtype, const void* base, int64_t tile_elems, int64_t
   if (!out) return fail(DLA_E_INVALID, "dla_wsum_slab_tiled: null out");
   int tshift = 0;
   while ((int64_t{1} << tshift) < tile_elems) ++tshift;
-  const int variant = cfg && cfg->variant ? cfg->variant : 9;
+  const int variant = cfg && cfg->variant ? cfg->variant : vec_variant(n_peers < kMaxPeersPerPass ? n_peers
+                                                                                                 : kMaxPeersPerPass);
   if (variant != 9 && variant != 10 && variant != 12)
     return fail(DLA_E_CONFIG, "dla_wsum_slab_tiled: variant must be 0 (= 9), 9, 10 or 12");
   const int64_t stride = slab_rows * tile_elems;
@@ -1848,6 +1867,22 @@ int dla_wsum_slab_tiled(int dtype, const void* base, int64_t tile_elems, int64_t
   }
   if (e != hipSuccess) return fail(static_cast<int>(e), std::string("dla_wsum_slab_tiled: ") + hipGetErrorString(e));
   return DLA_OK;
+}
+
+int64_t dla_slab_tile_elems(int dtype, int slab_rows, int64_t n_elems) {
+  const int es = elem_size(dtype);
+  if (es == 0 || slab_rows < 1 || n_elems < 0) return 0;
+  // Interleaved A/B over tile sizes 1, 4 and 16 KiB (profiles/r02d_ab_tiled.log): 16 KiB for up to
+  // 16 rows (8 x 25 M f32 130.2 / 131.1 / 132.1 us for 16 / 4 / 1 KiB; 16 x 21.3 M bf16 106.3 /
+  // 108.3 / 109.2), 1 KiB for rows under 1 MiB (128 x 85 354 f32 9.5 / 10.9 / 9.8), else 4 KiB
+  // (128 x 21.3 M bf16 792 / 796 / 831; 64 x 1.23 M f32 47.5 / 55.2 / 48.5; within 2 % of the
+  // best elsewhere: 128 x 2.66 M bf16 103.6 vs 102.7, 32 x 1.69 M f32 33.5 vs 32.8).
+  int64_t bytes = 4096;
+  if (n_elems * es < (int64_t{1} << 20))
+    bytes = 1024;
+  else if (slab_rows <= 16)
+    bytes = 16384;
+  return bytes / es;
 }
 
 }  // extern "C"

@@ -58,15 +58,20 @@ extern "C" {
 
 /* Launch tuning knobs for dla_wsum_ex (0 = library default for each field). */
 typedef struct dla_launch_cfg {
-  int variant;      /* 0 = by shape: 4; 8 for a small share over more than 8 peers
-                       (and 16-bit dtypes over more than 32 peers); 16 for fp32 shares
-                       over 8, 16 or 32 peers beyond 256 MiB whose big tiles fill >= 80 %
-                       of their last round of 1024 resident waves, and fp64 over 4..8;
-                       cache policy of the 16-byte register stream:
+  int variant;      /* 0 = by shape: passes of more than 8 fp32 / bf16 / f16 peers take 9
+                       (>= 32 peers) or 12; fp32 shares over 8, 16 or 32 peers beyond
+                       256 MiB whose big tiles fill >= 80 % of their last round of 1024
+                       resident waves take 16 (17 from one full round up), fp64 over 4..8
+                       likewise; fp64 small shares over more than 8 peers 8; otherwise 4.
+                       Cache policy of the 16-byte register stream:
                        1 = plain loads / plain stores   2 = nt loads / plain stores
                        4 = nt loads / sc1 stores (write-through, line not kept in L2)
                        8 = word-per-lane kernel (nt loads, sc1 stores, up to 64 peers
                            in flight per lane; chunks/block/grid are ignored)
+                       9 = vector-per-lane kernel: 8 bytes per lane per load, 32 peers in
+                           flight per lane (passes of more than 8 peers; fp64 and smaller
+                           passes take 4); 10 = 16 bytes x 16 peers; 11 = 16 bytes x 32;
+                           12 = 8 bytes x 16
                       16 = peer-major big-tile kernel (fp32 <= 8, 16 or 32 peers, fp64 <= 8:
                            16 KiB of output per wave, one peer's 16 KiB streamed at a
                            time; chunks/block/grid are ignored; other dtypes take 4)
@@ -117,6 +122,10 @@ int dla_wsum_slab(int dtype, const void* base, int64_t pitch_elems, const double
 int dla_wsum_slab_tiled(int dtype, const void* base, int64_t tile_elems, int64_t slab_rows, const double* weights,
                         int n_peers, int64_t n_elems, void* out, void* stream, const dla_launch_cfg_t* cfg);
 
+/* The tile (in elements) the library recommends for a tile-interleaved slab of slab_rows rows of
+ * n_elems elements (what PeerSlab uses); 0 for invalid arguments.  ABI v5. */
+int64_t dla_slab_tile_elems(int dtype, int slab_rows, int64_t n_elems);
+
 /* Replaces the per-parameter inner loop of fedavg.py:24-25 for T parameter
  * tensors at once (one model = T tensors, parameters() order).
  *   peer_ptrs host array [n_tensors * n_peers]: peer_ptrs[t * n_peers + k] is
@@ -140,8 +149,8 @@ int dla_mean(int dtype, const void* const* peers, int n_peers, int64_t n_elems, 
 int dla_max_peers_per_pass(void);
 
 /* Name of the kernel family dla_wsum picks (default launch, 16-byte aligned buffers) for
- * this dtype, peer count and size: "wsum_bigtile_kernel", "wsum_wide_kernel" or
- * "wsum_stream_kernel" (static string; "" for invalid arguments).  For profilers and
+ * this dtype, peer count and size: "wsum_bigtile_kernel", "wsum_vec_kernel", "wsum_wide_kernel"
+ * or "wsum_stream_kernel" (static string; "" for invalid arguments).  For profilers and
  * benchmarks that must name the dominant kernel.  ABI v4. */
 const char* dla_select_kernel(int dtype, int n_peers, int64_t n_elems);
 

@@ -27,7 +27,7 @@ def main():
     w = [1.0 / n] * n
     res = {}
     for rnd in range(3):
-        for mode in ("registered", "pinned", "pageable"):
+        for mode in ("pinned", "pageable"):
             host_memory.set_result_memory(mode)
             FedAvg.aggregate(models, w)
             ts = []

@@ -106,22 +106,21 @@ algo = (n_peers + 1) * params * esize
 ns_workload = (n_peers, params, dtype_name) == (8, 25_000_000, "f32")
 summary["algorithmic_bytes_per_launch"] = algo
 if fetch_kb is not None and write_kb is not None:
-    # gfx950: FETCH_SIZE counts half of a wide coalesced stream's bytes -> x2 (MI355X guide, HBM
-    # section), calibrated there for 16-B-per-lane loads (bigtile, stream kernels).  The wide
-    # kernel loads one dword per lane (256 B per wave instruction), a width the guide leaves
-    # uncalibrated; measured here (r01s6_c4: 128 x 2.66 M bf16) its raw FETCH_SIZE is 0.5002 of
-    # the peer bytes a correct result must read at least once, so the same 1/2 tally applies.
+    # gfx950: FETCH_SIZE counts half of a streaming read's bytes -> x2.  The guide calibrates
+    # 16-B-per-lane loads; r02 calibrated 4-, 8- and 16-B loads on a known 1 GiB read
+    # (profiles/r02b_fetch_calibration.json: 0.50001 for each width), so the x2 holds for the
+    # dword (wsum_wide_kernel) and dwordx2 (wsum_vec_kernel) loads as measured, not assumed.
     corr = 2
-    summary["fetch_correction"] = 2 if bench_kernel != "wsum_wide_kernel" else \
-        "2 (dword loads: calibrated against the peer bytes read, raw FETCH_SIZE = 0.5002 of them)"
+    summary["fetch_correction"] = "2 (calibrated for 4/8/16-B loads: profiles/r02b_fetch_calibration.json)"
     hbm = corr * fetch_kb * 1024 + write_kb * 1024
     summary["hbm_bytes_per_launch"] = hbm
     summary["hbm_over_algorithmic"] = hbm / algo
     # bench.py reads profiles/pmc_traffic.json for the north-star line only; other shapes get
     # their own <round>_pmc_traffic.json
     pmc_name = "pmc_traffic.json" if ns_workload else "%s_pmc_traffic.json" % rnd
-    json.dump({"workload": "ns" if ns_workload else "other", "dtype": dtype_name, "peers": n_peers, "params": params, "hbm_bytes_per_launch": int(hbm),
-               "fetch_kb_raw": fetch_kb, "write_kb": write_kb, "correction": "FETCH_SIZE x2 (gfx950 coalesced streams)",
+    layout = args[args.index("--layout") + 1] if "--layout" in args else "slab"
+    json.dump({"workload": "ns" if ns_workload else "other", "layout": layout, "dtype": dtype_name, "peers": n_peers, "params": params, "hbm_bytes_per_launch": int(hbm),
+               "fetch_kb_raw": fetch_kb, "write_kb": write_kb, "correction": "FETCH_SIZE x2 (gfx950; calibrated for 4/8/16-B loads)",
                "source": "profiles/%s_summary.json" % rnd}, open(os.path.join(HERE, pmc_name), "w"), indent=1)
 if "avg_ns" in summary:
     summary["achieved_GBps_from_trace"] = algo / summary["avg_ns"]

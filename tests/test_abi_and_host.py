@@ -14,7 +14,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def _declared_symbols():
     text = open(os.path.join(ROOT, "include", "dlagg.h")).read()
-    return sorted(set(re.findall(r"^\s*(?:int|void|const char\*)\s+(dla_\w+)\s*\(", text, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|int64_t|void|const char\*)\s+(dla_\w+)\s*\(", text, re.M)))
 
 
 @pytest.fixture(scope="module")
@@ -65,9 +65,10 @@ def test_library_version_and_argument_errors(lib_path):
     # kernel selection by shape (host-only query): north star, configs[3] share, configs[4] share,
     # configs[2], GNLeNet 8 peers, fp64 north-star shape, few peers, invalid arguments
     assert _lib.select_kernel(0, 8, 25_000_000) == "wsum_bigtile_kernel"
-    assert _lib.select_kernel(0, 64, 21_339) == "wsum_wide_kernel"
-    assert _lib.select_kernel(1, 128, 2_662_045) == "wsum_wide_kernel"
-    assert _lib.select_kernel(0, 32, 1_690_046) == "wsum_stream_kernel"
+    assert _lib.select_kernel(0, 64, 21_339) == "wsum_vec_kernel"
+    assert _lib.select_kernel(1, 128, 2_662_045) == "wsum_vec_kernel"
+    assert _lib.select_kernel(0, 32, 1_690_046) == "wsum_vec_kernel"
+    assert _lib.select_kernel(3, 64, 21_339) == "wsum_wide_kernel"
     assert _lib.select_kernel(0, 8, 85_354) == "wsum_stream_kernel"
     assert _lib.select_kernel(3, 8, 12_500_000) == "wsum_bigtile_kernel"
     assert _lib.select_kernel(0, 4, 25_000_000) == "wsum_stream_kernel"
@@ -78,12 +79,17 @@ def test_library_version_and_argument_errors(lib_path):
     assert _lib.select_kernel(0, 16, 21_296_355) == "wsum_bigtile_kernel"
     assert _lib.select_kernel(0, 8, 21_300_000) == "wsum_bigtile_kernel"
     assert _lib.select_kernel(0, 8, 3_400_000) == "wsum_stream_kernel"
-    assert _lib.select_kernel(0, 32, 3_000_000) == "wsum_stream_kernel"  # 0.72 of one round
+    assert _lib.select_kernel(0, 32, 3_000_000) == "wsum_vec_kernel"  # 0.72 of one round
     assert _lib.select_kernel(0, 32, 4_110_000) == "wsum_bigtile_kernel"
     assert _lib.select_kernel(0, 32, 8_200_000) == "wsum_bigtile_kernel"
-    assert _lib.select_kernel(0, 24, 8_200_000) == "wsum_stream_kernel"
+    assert _lib.select_kernel(0, 24, 8_200_000) == "wsum_vec_kernel"
     assert _lib.select_kernel(1, 8, 50_000_000) == "wsum_stream_kernel"
     assert _lib.select_kernel(9, 8, 100) == "" and _lib.select_kernel(0, 0, 100) == ""
+    # tile of the tile-interleaved PeerSlab (dla_slab_tile_elems, host-only)
+    assert _lib.slab_tile_elems(0, 8, 25_000_000) * 4 == 16384
+    assert _lib.slab_tile_elems(1, 128, 2_662_045) * 2 == 4096
+    assert _lib.slab_tile_elems(0, 128, 85_354) * 4 == 1024 and _lib.slab_tile_elems(0, 8, 1000) * 4 == 1024
+    assert _lib.slab_tile_elems(9, 8, 100) == 0
     # n_peers = 0 -> DLA_E_INVALID with a message
     rc = L.so.dla_wsum(0, None, None, 0, 10, None, None)
     assert rc == -1 and b"n_peers" in L.so.dla_last_error()
