@@ -17,9 +17,10 @@
 Deliberate differences (documented in DESIGN.md): parameters whose shapes or dtypes
 differ between models raise RuntimeError instead of broadcasting / promoting.
 
-The result's CPU parameters are ordinary pageable tensors as in the reference
-(``core/host_memory.py``: ACCDFL_AMD_RESULT_MEMORY=pageable, the default; "pinned" allocates
-a large round's result page-locked, which is faster but keeps it page-locked for good).
+The result's CPU parameters are ordinary pageable tensors as in the reference; those of a
+large round come from a pool of already-faulted pageable blocks (``core/host_memory.py``:
+ACCDFL_AMD_RESULT_MEMORY=pooled, the default; "pinned" allocates them page-locked, which
+keeps them page-locked for good; "pageable" allocates them fresh).
 
 Where the arithmetic runs: always on the HIP device (libdlagg.so).  Models already
 on the device are reduced in place of their parameters with no copies; CPU models
@@ -246,7 +247,7 @@ def _small_round(models: List[nn.Module], weights) -> "nn.Module | None":
     with _staging_lock:
         st, compute = _start_host_small(device, dtype, peers, weights, total,
                                         _round_up(total, _ALIGN_BYTES // esize))
-        center = _center_copy(models[0], pin=False)  # overlaps the H2D / reduce / D2H
+        center = _center_copy(models[0], large=False)  # overlaps the H2D / reduce / D2H
         params = list(center.parameters())
         if len(params) != len(numels) or not all(c.is_contiguous() for c in params):
             compute.synchronize()
@@ -362,9 +363,8 @@ def _reduce_host_staged(devices: List[torch.device], dtype, center: List[torch.T
             st.ensure(n, _round_up(max(e - s, 1), align))
             st.copy_stream.wait_stream(torch.cuda.current_stream(dev))  # previous users of d_in are done
             stages.append(st)
-        # D2H straight into the result's parameters when they are dense: page-locked (mode
-        # "pinned") or staged by the runtime (mode "pageable"); non-dense results go through
-        # one pinned buffer.
+        # D2H straight into the result's parameters when they are dense (pageable ones through the
+        # runtime's staging, page-locked ones directly); non-dense results go through one pinned buffer.
         direct = all(c.is_contiguous() for c in center)
         h_out = None if direct else torch.empty(total, dtype=dtype, pin_memory=True)
         jobs = [(st, dev, s, e) for st, dev, (s, e) in zip(stages, devices, bounds) if s < e]
@@ -486,21 +486,23 @@ def reduce_parameters(center_params: List[torch.Tensor], peer_params: List[List[
         _reduce_param(device, center_params[i], [peer_params[k][i] for k in ks], [weights[k] for k in ks])
 
 
-def _center_copy(model0: nn.Module, pin: bool = True) -> nn.Module:
+def _center_copy(model0: nn.Module, large: bool = True) -> nn.Module:
     """``copy.deepcopy(models[0])`` (fedavg.py:20) whose parameters are fresh,
     uninitialised tensors of the same shape, strides, dtype, device and
     ``requires_grad``: the reduce overwrites every one of them, so copying models[0]'s
     values first (and page-faulting P fresh elements: 16 ms of a 35 ms host-inclusive
-    8 x 25 M reduce) is wasted.  With ``pin`` the CPU parameters are allocated page-locked
-    (result-memory mode "pinned", core/host_memory.py).  Buffers and every other attribute
-    are deep-copied exactly as in the reference."""
+    8 x 25 M reduce) is wasted.  For a ``large`` round the contiguous CPU parameters come
+    from core/host_memory.result_tensor (pre-faulted pooled pageable memory by default).
+    Buffers and every other attribute are deep-copied exactly as in the reference."""
     memo = {}
-    pin = pin and torch.cuda.is_available()
     for p in model0.parameters():
         if id(p) in memo or type(p) is not nn.Parameter:
             continue  # Parameter subclasses keep the stock deepcopy
         if p.device.type == "cpu":
-            data = torch.empty_strided(p.size(), p.stride(), dtype=p.dtype, pin_memory=pin)
+            if large and p.is_contiguous():
+                data = _host_memory.result_tensor(p.shape, p.dtype)
+            else:
+                data = torch.empty_strided(p.size(), p.stride(), dtype=p.dtype)
         else:
             data = torch.empty_strided(p.size(), p.stride(), dtype=p.dtype, device=p.device)
         memo[id(p)] = nn.Parameter(data, p.requires_grad)
@@ -523,7 +525,7 @@ class FedAvg(GradientAggregation):
                     return small
             params0 = list(models[0].parameters())
             nbytes = sum(p.numel() * p.element_size() for p in params0) * len(models)
-            center_model = _center_copy(models[0], pin=nbytes >= _SMALL_ROUND_BYTES and _host_memory.pin_results())
+            center_model = _center_copy(models[0], large=nbytes >= _SMALL_ROUND_BYTES)
             reduce_parameters(list(center_model.parameters()), [list(m.parameters()) for m in models],
                               list(weights))
             return center_model

@@ -2,31 +2,40 @@
 
 The reference returns ``deepcopy(models[0])`` with ordinary (pageable) CPU tensors
 (accdfl/core/gradient_aggregation/fedavg.py:20), and callers keep that model: the simulator
-holds one per node.  The reduce's D2H has to land in those tensors.  Two modes, chosen by
-``ACCDFL_AMD_RESULT_MEMORY`` or ``set_result_memory``:
+holds one per node.  The reduce's D2H has to land in those tensors, and on the MI355X hosts
+measured the cost of a fresh pageable result is not the copy but faulting its pages in: a
+100 MB D2H takes 1.8 ms into pageable memory already touched, 11.2 ms into fresh memory,
+and 1.8 ms into page-locked memory (profiles/r02f_result_memory.log).  Three modes, chosen
+by ``ACCDFL_AMD_RESULT_MEMORY`` or ``set_result_memory``:
 
-* ``pageable`` (default): the result's tensors are ordinary pageable memory, exactly like the
-  reference's; the D2H goes through the HIP runtime's own staging.  Nothing stays page-locked
-  however many results a caller keeps.
-* ``pinned``: the result's tensors of a large round are allocated page-locked
-  (``is_pinned()``) and the D2H writes them directly.  Faster (8 x 25 M fp32 host-inclusive
-  round 16.6-17.4 ms against 21.8-22.4), but they stay page-locked for the model's lifetime,
-  and torch's caching host allocator keeps freed blocks page-locked too, so page-locked host
+* ``pooled`` (default): the large result tensors (>= 1 MiB) are ordinary pageable memory
+  taken from a pool of already-faulted blocks (anonymous mmaps, transparent huge pages
+  requested).  A block returns to the pool when the last tensor using it is freed, and the
+  pool keeps at most ``POOL_FREE_BYTES`` of free blocks.  Nothing is page-locked.
+* ``pinned``: the result tensors of a large round are allocated page-locked
+  (``is_pinned()``).  As fast, but they stay page-locked for the model's lifetime and
+  torch's caching host allocator keeps freed blocks page-locked too, so page-locked host
   memory grows with the number of results kept.
-
-Locking the pageable result in place for the duration of the D2H (``hipHostRegister``) was
-measured too and bought nothing over ``pageable`` (21.8-22.1 ms): the cost of a fresh
-pageable result is faulting its pages in, which the reference's deepcopy pays as well
-(profiles/r02d_result_memory.log).
+* ``pageable``: fresh pageable tensors (``torch.empty``), every page faulted in by the D2H.
 """
 from __future__ import annotations
 
+import mmap
 import os
+import threading
+import weakref
+from typing import Dict, List
 
-MODES = ("pageable", "pinned")
-_mode = os.environ.get("ACCDFL_AMD_RESULT_MEMORY", "pageable")
+import numpy as np
+import torch
+
+MODES = ("pooled", "pinned", "pageable")
+_mode = os.environ.get("ACCDFL_AMD_RESULT_MEMORY", "pooled")
 if _mode not in MODES:
     raise ValueError("ACCDFL_AMD_RESULT_MEMORY must be one of %s" % (MODES,))
+
+POOL_MIN_BYTES = 1 << 20          # smaller tensors are plain torch.empty
+POOL_FREE_BYTES = int(os.environ.get("ACCDFL_AMD_POOL_FREE_BYTES", str(2 << 30)))
 
 
 def set_result_memory(mode: str) -> None:
@@ -43,3 +52,69 @@ def result_memory() -> str:
 def pin_results() -> bool:
     """Allocate a large round's result parameters page-locked (mode "pinned")."""
     return _mode == "pinned"
+
+
+_NP = {torch.float32: np.float32, torch.float64: np.float64, torch.float16: np.float16,
+       torch.bfloat16: np.int16, torch.int64: np.int64, torch.int32: np.int32}
+
+
+class _Pool:
+    """Free pre-faulted pageable blocks by size.  A tensor handed out views a numpy array over
+    a block; a finalizer on that array (it lives exactly as long as the tensor's storage)
+    puts the block back."""
+
+    def __init__(self):
+        self._free: Dict[int, List[mmap.mmap]] = {}
+        self._free_bytes = 0
+        self._lock = threading.Lock()
+
+    def _release(self, size: int, block: mmap.mmap):
+        with self._lock:
+            if self._free_bytes + size <= POOL_FREE_BYTES:
+                self._free.setdefault(size, []).append(block)
+                self._free_bytes += size
+        # otherwise the block is dropped: unmapped once the dying array lets go of it
+
+    def take(self, shape, dtype: torch.dtype) -> torch.Tensor:
+        numel = int(np.prod(shape)) if len(shape) else 1
+        esize = torch.empty((), dtype=dtype).element_size()
+        size = -(-numel * esize // mmap.PAGESIZE) * mmap.PAGESIZE
+        with self._lock:
+            blocks = self._free.get(size)
+            block = blocks.pop() if blocks else None
+            if block is not None:
+                self._free_bytes -= size
+        if block is None:
+            block = mmap.mmap(-1, size)
+            if hasattr(mmap, "MADV_HUGEPAGE"):
+                try:
+                    block.madvise(mmap.MADV_HUGEPAGE)
+                except OSError:
+                    pass
+        arr = np.frombuffer(block, dtype=_NP[dtype], count=numel)
+        weakref.finalize(arr, self._release, size, block)
+        t = torch.from_numpy(arr)
+        if dtype == torch.bfloat16:
+            t = t.view(torch.bfloat16)
+        return t.view(tuple(shape))
+
+    def free_bytes(self) -> int:
+        return self._free_bytes
+
+
+_pool = _Pool()
+
+
+def result_tensor(shape, dtype: torch.dtype) -> torch.Tensor:
+    """An uninitialised contiguous CPU tensor for a result parameter, per the mode."""
+    numel = int(np.prod(shape)) if len(shape) else 1
+    nbytes = numel * torch.empty((), dtype=dtype).element_size()
+    if _mode == "pooled" and nbytes >= POOL_MIN_BYTES and dtype in _NP:
+        return _pool.take(tuple(shape), dtype)
+    if _mode == "pinned" and torch.cuda.is_available():
+        return torch.empty(tuple(shape), dtype=dtype, pin_memory=True)
+    return torch.empty(tuple(shape), dtype=dtype)
+
+
+def pool_free_bytes() -> int:
+    return _pool.free_bytes()

@@ -51,7 +51,7 @@ def main():
     print(json.dumps(res), flush=True)
     agg = {}
     for rnd in range(3):
-        modes = ("pinned", "pageable") if rnd % 2 == 0 else ("pageable", "pinned")
+        modes = ("pooled", "pinned", "pageable") if rnd % 2 == 0 else ("pageable", "pinned", "pooled")
         for mode in modes:
             host_memory.set_result_memory(mode)
             agg.setdefault(mode, []).append(t_ms(lambda: FedAvg.aggregate(models, w)))

@@ -214,3 +214,40 @@ def test_shard_range_matches_bucket_bounds(lib_path):
                 assert all(a * es % 256 == 0 for a, b in got if a < b)
     with pytest.raises(_lib.DlaggError):
         _lib.shard_range(_lib.DLA_F32, 10, 2, 2)
+
+
+def test_result_memory_pool_reuses_blocks_only_after_release():
+    """core/host_memory's pooled pageable result tensors: a block comes back only when every
+    tensor on it is gone; live results never share memory; dtypes incl. bf16 keep their shape."""
+    import gc
+
+    from accdfl_amd.core import host_memory as hm
+
+    prev = hm.result_memory()
+    hm.set_result_memory("pooled")
+    try:
+        a = hm.result_tensor((1000, 700), torch.float32)
+        b = hm.result_tensor((1000, 700), torch.float32)
+        assert a.shape == (1000, 700) and a.dtype == torch.float32 and not a.is_pinned()
+        assert a.data_ptr() != b.data_ptr()
+        a.fill_(1.0)
+        b.fill_(2.0)
+        pa = a.data_ptr()
+        view = a[3:5]  # a view keeps the block alive
+        del a
+        gc.collect()
+        c = hm.result_tensor((1000, 700), torch.float32)
+        assert c.data_ptr() not in (pa, b.data_ptr())
+        del view
+        gc.collect()
+        assert hm.pool_free_bytes() >= 1000 * 700 * 4
+        d = hm.result_tensor((700, 1000), torch.float32)  # same size: the released block
+        assert d.data_ptr() == pa and float(b[0, 0]) == 2.0
+        e = hm.result_tensor((4096, 512), torch.bfloat16)
+        assert e.dtype == torch.bfloat16 and e.shape == (4096, 512)
+        e.fill_(1.5)
+        assert float(e.float().sum()) == 1.5 * 4096 * 512
+        small = hm.result_tensor((10,), torch.float32)  # below POOL_MIN_BYTES: plain torch memory
+        assert small.numel() == 10
+    finally:
+        hm.set_result_memory(prev)

@@ -626,11 +626,12 @@ def test_tiled_slab_bit_exact(dtype, n, numel, tile_bytes):
         assert same_bits(_bits(out, dtype), want, dtype), (dtype, n, numel, tile_bytes, v)
 
 
-@pytest.mark.parametrize("mode", ["pageable", "pinned"])
+@pytest.mark.parametrize("mode", ["pooled", "pageable", "pinned"])
 def test_result_memory_modes(mode):
     """Large rounds (>= 64 MB) in each result-memory mode (core/host_memory.py): bit-exact, and
-    the kept results are page-locked only in mode "pinned" — with the default ("pageable")
-    page-locked memory does not grow with the number of results a caller keeps."""
+    the kept results are page-locked only in mode "pinned" — with the default ("pooled")
+    page-locked memory does not grow with the number of results a caller keeps (ADVICE r01);
+    kept results never share a pooled block."""
     from torch import nn
 
     from accdfl_amd.core import host_memory
@@ -659,6 +660,10 @@ def test_result_memory_modes(mode):
             got = torch.cat([out.a.detach(), out.b.detach()]).numpy()
             assert same_bits(got, want, "f32")
             assert out.a.is_pinned() == (mode == "pinned")
+        assert len({o.a.data_ptr() for o in kept}) == len(kept)
+        for o, o2 in zip(kept, kept[1:]):  # results kept alive are independent
+            assert same_bits(torch.cat([o.a.detach(), o.b.detach()]).numpy(),
+                             torch.cat([o2.a.detach(), o2.b.detach()]).numpy(), "f32")
         mm = DeviceModelManager(None, SimpleNamespace(gradient_aggregation=GradientAggregationMethod.FEDAVG), 0,
                                 capacity=n)
         for k, m in enumerate(models):
