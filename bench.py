@@ -572,6 +572,114 @@ def wire_ingress(p, device, reps=5):
     return out
 
 
+EVA_BLOCK = 60_000  # accdfl/core/session_settings.py:76 (eva block_size)
+
+
+def dfl_messages(n, p, seed=300):
+    """n DFL 'trained_model' messages of a p-parameter fp32 model as EVA delivers them: the
+    blocks of serialize_model bytes + the pickled population view (accdfl/dfl/community.py:
+    478-509 builds them), with each message's model_data_len."""
+    import pickle
+
+    from torch import nn
+
+    from accdfl_amd.core import wire
+
+    msgs = []
+    for k in range(n):
+        m = nn.Module()
+        m.w = nn.Parameter(torch.randn(p, generator=torch.Generator().manual_seed(seed + k)) * 0.05)
+        mb = wire.serialize_model(m)
+        view = pickle.dumps({"peer%d" % j: j for j in range(16)})
+        msgs.append((wire.payload_blocks(mb + view, EVA_BLOCK), len(mb)))
+    return msgs
+
+
+def dfl_round(msgs, p, device, reps=3):
+    """§8 f1-f3 at north-star scale: one DFL aggregator round (accdfl/dfl/community.py:576-673)
+    end to end — every message's EVA blocks split at model_data_len and decoded into page-locked
+    ingress buffers -> HBM PeerSlab (no b''.join, no slice copy, no create_model /
+    load_state_dict), the uniform average (:673), and its serialize_model bytes (:556-567)."""
+    from torch import nn
+
+    from accdfl_amd.core import wire
+    from accdfl_amd.core.gradient_aggregation import GradientAggregationMethod
+    from accdfl_amd.core.model_manager import DeviceModelManager
+    from types import SimpleNamespace
+
+    n = len(msgs)
+    template = nn.Module()
+    template.w = nn.Parameter(torch.zeros(p))
+    mm = DeviceModelManager(None, SimpleNamespace(gradient_aggregation=GradientAggregationMethod.FEDAVG), 0,
+                            capacity=n, template=template, device=device)
+
+    def one():
+        mm.reset_incoming_trained_models()
+        t0 = time.perf_counter()
+        for k, (blocks, ml) in enumerate(msgs):
+            head, _ = wire.split_blocks(blocks, ml)
+            mm.process_incoming_serialized(b"peer%d" % k, head)
+        t1 = time.perf_counter()
+        out = mm.aggregate_trained_models()
+        t2 = time.perf_counter()
+        data = wire.serialize_model(out)
+        t3 = time.perf_counter()
+        assert len(data) > p * 4
+        return t1 - t0, t2 - t1, t3 - t2, t3 - t0
+
+    one()
+    runs = [one() for _ in range(reps)]
+    med = [statistics.median(r[i] for r in runs) for i in range(4)]
+    return {"peers": n, "params": p, "eva_block_bytes": EVA_BLOCK,
+            "ingress_ms": round(med[0] * 1e3, 2), "aggregate_ms": round(med[1] * 1e3, 2),
+            "egress_serialize_ms": round(med[2] * 1e3, 2), "round_ms": round(med[3] * 1e3, 2),
+            "round_GBps": round((n + 1) * p * 4 / med[3] / 1e9, 2),
+            "path": "EVA blocks -> split at model_data_len -> restricted decode into page-locked ingress buffers "
+                    "-> async H2D into the tile-interleaved PeerSlab -> reduce -> D2H into the pooled result -> "
+                    "serialize_model bytes"}
+
+
+def dfl_round_reference_style(msgs, p, reps=2):
+    """The same round the way the reference runs it, on this host's CPU: b''.join of the EVA
+    blocks (accdfl/util/eva/transfer/incoming.py:35), the model_data_len slice
+    (accdfl/dfl/community.py:587), pickle.loads + load_state_dict into a fresh model
+    (accdfl/core/models/__init__.py:13-16), the FedAvg op sequence (oracle port of fedavg.py:
+    13-26), serialize_model.  Timed CPU comparison only."""
+    import copy
+    import pickle
+
+    from torch import nn
+
+    sys.path.insert(0, ROOT)
+    from oracle.fedavg_oracle import fedavg_modules_torch  # timed CPU comparison (kind "port")
+    from accdfl_amd.core import wire
+
+    template = nn.Module()
+    template.w = nn.Parameter(torch.zeros(p))
+
+    def one():
+        t0 = time.perf_counter()
+        models = []
+        for blocks, ml in msgs:
+            data = b"".join(blocks)
+            model_bytes = data[:ml]
+            m = copy.deepcopy(template)
+            m.load_state_dict(pickle.loads(model_bytes))  # bytes this process made
+            models.append(m)
+        t1 = time.perf_counter()
+        out = fedavg_modules_torch(models, None)
+        t2 = time.perf_counter()
+        wire.serialize_model(out)
+        t3 = time.perf_counter()
+        return t1 - t0, t2 - t1, t3 - t2, t3 - t0
+
+    runs = [one() for _ in range(reps)]
+    med = [statistics.median(r[i] for r in runs) for i in range(4)]
+    return {"ingress_ms": round(med[0] * 1e3, 1), "aggregate_ms": round(med[1] * 1e3, 1),
+            "egress_serialize_ms": round(med[2] * 1e3, 1), "round_ms": round(med[3] * 1e3, 1),
+            "threads": torch.get_num_threads()}
+
+
 def _cpu_port_ms(n, share, dt, budget_s=1.5, max_elems=500_000_000):
     """The reference op sequence (oracle/fedavg_oracle.py, torch-CPU) on the same share,
     on this host's cores: median ms of a bounded sample, or None above max_elems."""
@@ -1057,9 +1165,17 @@ def main():
             result["host_inclusive"] = host_inclusive(n, p)
             result["wire_ingress"] = wire_ingress(p, device)
             result["host_inclusive_small"] = host_inclusive_small()
+            log("DFL round from EVA blocks")
+            msgs = dfl_messages(n, p)
+            result["dfl_round"] = dfl_round(msgs, p, device)
+            del msgs
         if not args.no_cpu_baseline and args.dtype == "f32":
             log("cpu baseline")
             result["cpu_baseline"] = cpu_baseline(n, p, args.cpu_seconds)
+            if not args.no_host_inclusive:
+                msgs = dfl_messages(n, p)
+                result["cpu_baseline"]["dfl_round_reference_style"] = dfl_round_reference_style(msgs, p)
+                del msgs
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

@@ -89,6 +89,10 @@ class DeviceModelManager(ModelManager):
         # fingerprint at staging time) — the slab is used only while these still describe the
         # registry exactly (see _uniform)
         self._staged: List[tuple] = []
+        # page-locked ingress buffers, one per registry position of a round (reused every round):
+        # models that arrive as EVA block lists are gathered here instead of b''.join'ed
+        self._ingress: List[Optional[torch.Tensor]] = []
+        self._ingress_ev: List[Optional[torch.cuda.Event]] = []
 
     @staticmethod
     def _fingerprint(model) -> tuple:
@@ -111,15 +115,48 @@ class DeviceModelManager(ModelManager):
         except TypeError:
             pass  # mixed-dtype model: the round falls back to FedAvg.aggregate (_uniform is False)
 
-    def process_incoming_serialized(self, peer_pk: bytes, data: bytes):
-        """A model straight from the wire (``serialize_model`` bytes, e.g. EVA's
-        ``TransferResult.data``): decoded without executing the payload and staged into
-        HBM; no ``create_model`` / ``load_state_dict`` (§8 f1)."""
+    def _ingress_alloc(self, pos: int, nbytes: int):
+        """Bump allocator over registry position ``pos``'s page-locked ingress buffer (grown to
+        ``nbytes``); waits until the H2D that last read that buffer has finished."""
+        while len(self._ingress) <= pos:
+            self._ingress.append(None)
+            self._ingress_ev.append(None)
+        ev = self._ingress_ev[pos]
+        if ev is not None:
+            ev.synchronize()
+        buf = self._ingress[pos]
+        if buf is None or buf.numel() < nbytes:
+            buf = self._ingress[pos] = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
+        off = [0]
+
+        def alloc(n: int) -> torch.Tensor:
+            a = off[0]
+            off[0] = a + (n + 255) // 256 * 256
+            if off[0] > buf.numel():
+                raise ValueError("ingress buffer overflow")
+            return buf[a:a + n]
+        return alloc
+
+    def process_incoming_serialized(self, peer_pk: bytes, data):
+        """A model straight from the wire (§8 f1), decoded without executing the payload and
+        staged into HBM, with no ``create_model`` / ``load_state_dict``.  ``data`` is the
+        ``serialize_model`` payload as bytes, a memoryview (e.g. the model part of a DFL message,
+        ``memoryview(result.data)[:model_data_len]``: no slice copy, accdfl/dfl/community.py:587)
+        or the block list of the EVA transfer before its ``b''.join``
+        (accdfl/util/eva/transfer/incoming.py:35; ``wire.split_blocks`` splits a DFL message's
+        blocks): its tensors are then gathered into a page-locked ingress buffer and sent to
+        HBM from there asynchronously.  The decoded tensors view ``data`` / that buffer, which
+        stays valid for this round (the buffer is reused one round later)."""
         if peer_pk in self.incoming_trained_models:
             return
         if self.template is None:
             raise ValueError("DeviceModelManager needs a template module to decode wire payloads")
-        sd = wire.loads_state_dict(data, copy=False)  # read-only views of `data`; staged, never written
+        pos = len(self.incoming_trained_models)
+        alloc = None
+        if isinstance(data, (list, tuple)):
+            n_tensors = len(self.template.state_dict())
+            alloc = self._ingress_alloc(pos, sum(len(b) for b in data) + 256 * (n_tensors + 1))
+        sd = wire.loads_state_dict(data, copy=False, alloc=alloc)  # views of `data` / the ingress buffer
         params = wire.parameter_tensors(sd, self.template)
         peer = WirePeer(sd)
         self.incoming_trained_models[peer_pk] = peer
@@ -128,6 +165,10 @@ class DeviceModelManager(ModelManager):
         if self.slab.matches(params) and len(self._staged) == self.slab.n:
             self.slab.stage(params)
             self._staged.append((peer_pk, peer, ()))
+        if alloc is not None:
+            ev = torch.cuda.Event()
+            ev.record(self.slab.copy_stream)
+            self._ingress_ev[pos] = ev
 
     def reset_incoming_trained_models(self):
         super().reset_incoming_trained_models()

@@ -197,7 +197,9 @@ class PeerSlab:
                         pending[1].append(t.data_ptr())
                         pending[2].append(t.numel() * esize)
                     else:
-                        dst_row[off:off + t.numel()].copy_(t)  # pageable H2D, no host copy
+                        # H2D straight from where the tensor lives: pageable (no host copy) or a
+                        # page-locked ingress buffer (async; the caller keeps it until copy_stream passes)
+                        dst_row[off:off + t.numel()].copy_(t, non_blocking=t.is_pinned())
                     off += t.numel()
                 if bounce is not None:
                     ev = torch.cuda.Event()

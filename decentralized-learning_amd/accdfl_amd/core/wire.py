@@ -21,7 +21,9 @@ from __future__ import annotations
 import collections
 import io
 import pickle
-from typing import Dict
+from typing import Callable, Dict, List, Optional, Sequence
+
+import numpy as np
 
 import torch
 from torch import nn
@@ -57,12 +59,64 @@ class _BlobUnpickler(pickle.Unpickler):
         return ("storage", _STORAGE_DTYPES[pid[1][1]], str(pid[2]), int(pid[4]))
 
 
-def _parse_storage_blob(blob) -> torch.TypedStorage:
+class _Span:
+    """A byte range of a block list (EVA's ``data_list``) that crosses block boundaries:
+    kept as pieces (memoryviews into the blocks), never joined unless asked."""
+    __slots__ = ("pieces", "n")
+
+    def __init__(self, pieces):
+        self.pieces = pieces
+        self.n = sum(len(p) for p in pieces)
+
+    def __len__(self):
+        return self.n
+
+    def sub(self, a: int, b: int) -> "list":
+        """The pieces covering [a, b) of this span."""
+        out, off = [], 0
+        for p in self.pieces:
+            s, e = max(a, off), min(b, off + len(p))
+            if s < e:
+                out.append(p[s - off:e - off])
+            off += len(p)
+            if off >= b:
+                break
+        return out
+
+    def read(self, a: int, b: int) -> bytes:
+        return b"".join(self.sub(a, b))
+
+
+def _gather(pieces, dst: torch.Tensor) -> None:
+    """Copy the pieces back to back into the host uint8 tensor ``dst`` (one native batched
+    memcpy: libdlagg's dla_host_copy_batch)."""
+    from accdfl_amd import _lib
+
+    dsts, srcs, sizes, keep, off = [], [], [], [], 0
+    base = dst.data_ptr()
+    for p in pieces:
+        a = np.frombuffer(p, dtype=np.uint8)
+        keep.append(a)
+        dsts.append(base + off)
+        srcs.append(a.ctypes.data)
+        sizes.append(len(p))
+        off += len(p)
+    _lib.host_copy_batch(dsts, srcs, sizes)
+
+
+def _parse_storage_blob(blob, alloc=None) -> torch.TypedStorage:
     """Zero-copy decode of ``TypedStorage.__reduce__``'s blob (legacy torch.save of one
     storage; torch/serialization.py _legacy_save): the element data is viewed in place.
-    ``blob`` may be bytes or a memoryview into the payload; only its small header is copied."""
-    blob = memoryview(blob)
-    f = io.BytesIO(bytes(blob[:65536]))  # the four header pickles are a few hundred bytes
+    ``blob`` may be bytes, a memoryview into the payload, or a _Span of a block list; only its
+    small header is copied.  A _Span's element bytes are gathered into ``alloc(nbytes)`` (a host
+    uint8 tensor, e.g. a page-locked ingress buffer) when given, else joined."""
+    span = blob if isinstance(blob, _Span) else None
+    if span is None:
+        blob = memoryview(blob)
+        head = bytes(blob[:65536])
+    else:
+        head = span.read(0, min(65536, len(span)))
+    f = io.BytesIO(head)  # the four header pickles are a few hundred bytes
     u = _BlobUnpickler(f)
     if u.load() != _LEGACY_MAGIC or u.load() != _LEGACY_PROTOCOL:
         raise UnsafePayloadError("not a legacy storage blob")
@@ -77,14 +131,22 @@ def _parse_storage_blob(blob) -> torch.TypedStorage:
     _, dtype, _, numel = obj
     pos = f.tell()
     esize = torch.empty((), dtype=dtype).element_size()
-    if pos + 8 > len(f.getbuffer()):
+    if pos + 8 > len(head):
         raise UnsafePayloadError("storage blob header too long")
-    n_saved = int.from_bytes(blob[pos:pos + 8], "little")
+    n_saved = int.from_bytes(head[pos:pos + 8], "little")
     start, nbytes = pos + 8, numel * esize
     if n_saved != numel or start + nbytes != len(blob):
         raise UnsafePayloadError("storage blob size mismatch")
     if numel == 0:
         data = torch.empty(0, dtype=dtype)
+    elif span is not None:
+        pieces = span.sub(start, start + nbytes)
+        if alloc is not None:
+            dst = alloc(nbytes)
+            _gather(pieces, dst)
+            data = dst.view(dtype)
+        else:
+            data = torch.frombuffer(bytearray(b"".join(pieces)), dtype=dtype)
     else:
         import warnings
 
@@ -94,12 +156,14 @@ def _parse_storage_blob(blob) -> torch.TypedStorage:
     return torch.TypedStorage(wrap_storage=data.untyped_storage(), dtype=dtype, _internal=True)
 
 
-def _load_storage_blob(blob: bytes):
+def _load_storage_blob(blob, alloc=None):
     try:
-        return _parse_storage_blob(blob)
+        return _parse_storage_blob(blob, alloc)
     except UnsafePayloadError:
         raise
     except Exception:  # any other layout: torch's own safe loader
+        if isinstance(blob, _Span):
+            blob = blob.read(0, len(blob))
         return torch.load(io.BytesIO(blob), weights_only=True)
 
 
@@ -132,24 +196,70 @@ class _Global:
 _MARK = object()
 
 
-def _vm_loads(data) -> object:
+class _BlockReader:
+    """Sequential reads over a list of byte blocks (EVA's ``data_list``, before its
+    ``b''.join``, accdfl/util/eva/transfer/incoming.py:35): a read inside one block is a
+    memoryview into it, a short read across blocks is joined, a long one is a _Span."""
+
+    def __init__(self, blocks):
+        self.views = [memoryview(b).cast("B") for b in blocks if len(b)]
+        self.bi = 0      # current block
+        self.bo = 0      # offset in it
+        self.left = sum(len(v) for v in self.views)
+
+    def take(self, k: int):
+        if k > self.left:
+            raise UnsafePayloadError("truncated payload")
+        self.left -= k
+        v = self.views[self.bi] if self.bi < len(self.views) else None
+        if v is not None and self.bo + k <= len(v):
+            out = v[self.bo:self.bo + k]
+            self.bo += k
+            if self.bo == len(v):
+                self.bi, self.bo = self.bi + 1, 0
+            return out
+        pieces = []
+        while k:
+            v = self.views[self.bi]
+            m = min(k, len(v) - self.bo)
+            pieces.append(v[self.bo:self.bo + m])
+            self.bo += m
+            k -= m
+            if self.bo == len(v):
+                self.bi, self.bo = self.bi + 1, 0
+        return b"".join(pieces) if sum(len(p) for p in pieces) <= 4096 else _Span(pieces)
+
+
+def _vm_loads(data, alloc: Optional[Callable[[int], torch.Tensor]] = None) -> object:
     """A pickle VM for exactly the opcode subset ``pickle.dumps(state_dict)`` emits
     (protocols 2-4).  BINBYTES payloads come back as memoryviews into ``data``, so the
     nested storage blobs — i.e. all parameter bytes — are never copied; the only callables
-    it can invoke are the three in ``_ALLOWED``."""
-    mv = memoryview(data).cast("B")
-    n = len(mv)
+    it can invoke are the three in ``_ALLOWED``.  ``data`` may also be a list of blocks (an EVA
+    transfer's ``data_list``): storage bytes that cross blocks are then gathered into
+    ``alloc(nbytes)`` (a host uint8 tensor) in place of the reference's full ``b''.join``."""
+    if isinstance(data, (list, tuple)):
+        rd = _BlockReader(data)
+        n = rd.left
+
+        def take(k):
+            return rd.take(k)
+    else:
+        mv = memoryview(data).cast("B")
+        n = len(mv)
+        rd = None
+
+        def take(k):
+            nonlocal pos
+            if pos + k > n:
+                raise UnsafePayloadError("truncated payload")
+            out = mv[pos:pos + k]
+            pos += k
+            return out
     pos = 0
     stack: list = []
     memo: dict = {}
-
-    def take(k):
-        nonlocal pos
-        if pos + k > n:
-            raise UnsafePayloadError("truncated payload")
-        out = mv[pos:pos + k]
-        pos += k
-        return out
+    storage_loader = _Global(_load_storage_blob if alloc is None else
+                             (lambda blob: _load_storage_blob(blob, alloc)))
 
     def u(k):
         return int.from_bytes(take(k), "little")
@@ -164,11 +274,20 @@ def _vm_loads(data) -> object:
         del stack[i:]
         return items
 
+    def allowed(module, name):
+        fn = _ALLOWED.get((module, name))
+        if fn is None:
+            raise UnsafePayloadError("accdfl_amd: refusing global %s.%s in a model payload" % (module, name))
+        return storage_loader if fn is _load_storage_blob else _Global(fn)
+
     while True:
-        if pos >= n:
-            raise UnsafePayloadError("truncated payload")
-        op = mv[pos]
-        pos += 1
+        if rd is None:
+            if pos >= n:
+                raise UnsafePayloadError("truncated payload")
+            op = mv[pos]
+            pos += 1
+        else:
+            op = take(1)[0]
         if op == 0x80:        # PROTO
             if u(1) > 4:
                 raise _Unsupported()
@@ -199,19 +318,14 @@ def _vm_loads(data) -> object:
         elif op == 0x93:      # STACK_GLOBAL
             name = stack.pop()
             module = stack.pop()
-            fn = _ALLOWED.get((module, name))
-            if fn is None:
-                raise UnsafePayloadError("accdfl_amd: refusing global %s.%s in a model payload" % (module, name))
-            stack.append(_Global(fn))
+            stack.append(allowed(module, name))
         elif op == 0x63:      # GLOBAL (protocol <= 3)
+            if rd is not None:
+                raise _Unsupported()
             rest = bytes(mv[pos:pos + 256])
             module, name = rest.split(b"\n", 2)[:2]
             pos += len(module) + len(name) + 2
-            fn = _ALLOWED.get((module.decode(), name.decode()))
-            if fn is None:
-                raise UnsafePayloadError("accdfl_amd: refusing global %s.%s in a model payload" % (
-                    module.decode(errors="replace"), name.decode(errors="replace")))
-            stack.append(_Global(fn))
+            stack.append(allowed(module.decode(errors="replace"), name.decode(errors="replace")))
         elif op == 0x29:      # EMPTY_TUPLE
             stack.append(())
         elif op == 0x85:      # TUPLE1
@@ -283,16 +397,25 @@ def _vm_loads(data) -> object:
             raise _Unsupported()
 
 
-def loads_state_dict(data: bytes, copy: bool = True) -> "collections.OrderedDict[str, torch.Tensor]":
+def loads_state_dict(data, copy: bool = True, alloc: Optional[Callable[[int], torch.Tensor]] = None
+                     ) -> "collections.OrderedDict[str, torch.Tensor]":
     """Decode ``serialize_model`` bytes into the state dict (CPU tensors).
 
+    ``data``: the payload as bytes / a memoryview (e.g. the model part of a DFL message,
+    ``memoryview(result.data)[:model_data_len]``, accdfl/dfl/community.py:587, without the
+    reference's slice copy), or the list of blocks an EVA transfer received, before the
+    reference's ``b''.join(data_list)`` (accdfl/util/eva/transfer/incoming.py:35).
     The tensors' element data is parsed in place from the payload (no ``torch.load``
-    pass, no copy of the parameter bytes: see ``_vm_loads``).  ``copy=True`` gives each tensor its own writable memory; ``copy=False``
-    returns read-only views of the payload (what the ingress path stages to HBM)."""
+    pass, no copy of the parameter bytes: see ``_vm_loads``); a tensor whose bytes cross
+    EVA blocks is gathered into ``alloc(nbytes)`` (a host uint8 tensor; a page-locked ingress
+    buffer on the staging path) or, without ``alloc``, joined for that tensor alone.
+    ``copy=True`` gives each tensor its own writable memory; ``copy=False`` returns views (what
+    the ingress path stages to HBM)."""
     try:
-        obj = _vm_loads(data)
+        obj = _vm_loads(data, alloc)
     except _Unsupported:
-        obj = _StateDictUnpickler(io.BytesIO(bytes(data))).load()
+        flat = b"".join(memoryview(b) for b in data) if isinstance(data, (list, tuple)) else bytes(data)
+        obj = _StateDictUnpickler(io.BytesIO(flat)).load()
     if not isinstance(obj, dict) or not all(isinstance(k, str) and torch.is_tensor(v) for k, v in obj.items()):
         raise UnsafePayloadError("accdfl_amd: payload is not a state_dict")
     if copy:
@@ -317,3 +440,31 @@ def parameter_tensors(state_dict: Dict[str, torch.Tensor], template: nn.Module):
     """The state dict's parameter tensors in ``template.parameters()`` order (the order
     fedavg.py:24 zips them in); raises KeyError if one is missing."""
     return [state_dict[name] for name, _ in template.named_parameters()]
+
+
+def split_blocks(blocks: Sequence, n: int):
+    """(the first n bytes, the rest) of a block list, as two block lists of memoryviews — the
+    DFL message split at ``model_data_len`` (accdfl/dfl/community.py:587-588) with no copy."""
+    head: List[memoryview] = []
+    tail: List[memoryview] = []
+    off = 0
+    for b in blocks:
+        v = memoryview(b).cast("B")
+        if off + len(v) <= n:
+            head.append(v)
+        elif off >= n:
+            tail.append(v)
+        else:
+            head.append(v[:n - off])
+            tail.append(v[n - off:])
+        off += len(v)
+    if off < n:
+        raise ValueError("split_blocks: the blocks hold %d bytes, fewer than %d" % (off, n))
+    return head, tail
+
+
+def payload_blocks(data: bytes, block_size: int) -> List[bytes]:
+    """``data`` cut into ``block_size`` blocks, as an EVA transfer delivers them
+    (accdfl/util/eva/transfer/outgoing.py:37-40 ``_get_block``: one ``block_size`` slice per
+    data packet)."""
+    return [data[i:i + block_size] for i in range(0, len(data), block_size)]

@@ -173,3 +173,62 @@ def test_vm_rejects_truncated_and_garbage():
     # a REDUCE on anything but an allowed global is refused
     with pytest.raises(wire.UnsafePayloadError):
         wire.loads_state_dict(pickle.dumps({"w": _Evil()}, protocol=4))
+
+
+@pytest.mark.parametrize("block_size", [1, 7, 1000, 60_000, 10 ** 9])
+def test_eva_block_list_decodes_like_the_joined_payload(block_size):
+    """An EVA transfer's block list (before the reference's b''.join,
+    accdfl/util/eva/transfer/incoming.py:35) decodes to the same state dict as the joined
+    bytes; tensors whose bytes cross blocks are gathered into the caller's buffer."""
+    from accdfl_amd.core import wire
+
+    torch.manual_seed(block_size % 97)
+    m = nn.Sequential(nn.Linear(300, 200), nn.BatchNorm1d(200), nn.Linear(200, 3)).to(torch.bfloat16)
+    data = wire.serialize_model(m)
+    blocks = wire.payload_blocks(data, block_size)
+    arena = torch.empty(len(data), dtype=torch.uint8)
+    used = [0]
+
+    def alloc(n):
+        a = used[0]
+        used[0] = a + (n + 255) // 256 * 256
+        return arena[a:a + n]
+
+    want = wire.loads_state_dict(data)
+    for kw in ({"alloc": alloc}, {}):
+        got = wire.loads_state_dict(blocks, copy=False, **kw)
+        assert list(got.keys()) == list(want.keys())
+        for k in want:
+            assert got[k].dtype == want[k].dtype and torch.equal(got[k], want[k]), k
+    if block_size < 60_000:  # the 300 x 200 weight crosses blocks: gathered, not joined
+        assert used[0] >= 300 * 200 * 2
+
+
+def test_dfl_split_without_copies():
+    """The DFL message = model bytes + pickled population view, split at model_data_len
+    (accdfl/dfl/community.py:587-588): on a memoryview and on a block list, no copy."""
+    from accdfl_amd.core import wire
+
+    m = nn.Linear(50, 40)
+    model_bytes = wire.serialize_model(m)
+    view = pickle.dumps({"peers": [1, 2, 3]})
+    msg = model_bytes + view
+    mv = memoryview(msg)
+    sd = wire.loads_state_dict(mv[:len(model_bytes)], copy=False)
+    assert torch.equal(sd["weight"], m.weight.detach())
+    head, tail = wire.split_blocks(wire.payload_blocks(msg, 333), len(model_bytes))
+    assert b"".join(tail) == view and sum(len(h) for h in head) == len(model_bytes)
+    sd2 = wire.loads_state_dict(head, copy=True)
+    assert torch.equal(sd2["bias"], m.bias.detach())
+    with pytest.raises(ValueError):
+        wire.split_blocks([b"abc"], 10)
+
+
+def test_block_list_refuses_foreign_globals():
+    from accdfl_amd.core import wire
+
+    payload = pickle.dumps({"w": _Evil()})
+    with pytest.raises(wire.UnsafePayloadError):
+        wire.loads_state_dict(wire.payload_blocks(payload, 5))
+    with pytest.raises(wire.UnsafePayloadError):
+        wire.loads_state_dict(wire.payload_blocks(wire.serialize_model(nn.Linear(3, 2)), 64)[:-1])  # truncated
