@@ -35,11 +35,13 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <new>
 #include <set>
 #include <string>
+#include <thread>
 #include <utility>
 #include <vector>
 
@@ -1632,6 +1634,18 @@ int wsum_sharded_impl(int dtype, int n_shards, const int* dev_ids, const void* c
   return DLA_OK;
 }
 
+// Threads for one dla_host_copy_batch: one per 8 MiB up to DLA_COPY_THREADS (default 8; the GPU
+// box's CPU share is 16); batches under 8 MiB stay on the calling thread.
+int copy_threads(int64_t total) {
+  static const int cap = [] {
+    const char* e = std::getenv("DLA_COPY_THREADS");
+    const int v = e ? std::atoi(e) : 8;
+    return v < 1 ? 1 : v > 64 ? 64 : v;
+  }();
+  const int64_t by_size = total >> 23;
+  return static_cast<int>(by_size < 1 ? 1 : by_size < cap ? by_size : cap);
+}
+
 }  // namespace
 
 struct dla_plan {
@@ -1800,8 +1814,31 @@ int dla_host_copy_batch(void* const* dsts, const void* const* srcs, const int64_
     if (bytes[i] > 0 && (!dsts[i] || !srcs[i]))
       return fail(DLA_E_INVALID, "dla_host_copy_batch: null pointer at " + std::to_string(i));
   }
-  for (int i = 0; i < n; ++i)
-    if (bytes[i] > 0) std::memcpy(dsts[i], srcs[i], static_cast<size_t>(bytes[i]));
+  int64_t total = 0;
+  for (int i = 0; i < n; ++i) total += bytes[i];
+  const int threads = copy_threads(total);
+  if (threads <= 1) {
+    for (int i = 0; i < n; ++i)
+      if (bytes[i] > 0) std::memcpy(dsts[i], srcs[i], static_cast<size_t>(bytes[i]));
+    return DLA_OK;
+  }
+  // Large batches (an EVA block list gathered into a page-locked ingress buffer: ~1 700
+  // blocks per 100 MB model) split into equal byte ranges, one per thread; a range may start
+  // or end inside a segment.
+  auto copy_range = [&](int64_t lo, int64_t hi) {
+    int64_t off = 0;
+    for (int i = 0; i < n && off < hi; off += bytes[i], ++i) {
+      const int64_t s0 = lo > off ? lo : off, e0 = hi < off + bytes[i] ? hi : off + bytes[i];
+      if (s0 < e0)
+        std::memcpy(static_cast<char*>(dsts[i]) + (s0 - off), static_cast<const char*>(srcs[i]) + (s0 - off),
+                    static_cast<size_t>(e0 - s0));
+    }
+  };
+  std::vector<std::thread> pool;
+  const int64_t per = (total + threads - 1) / threads;
+  for (int t = 1; t < threads; ++t) pool.emplace_back(copy_range, per * t, per * (t + 1) < total ? per * (t + 1) : total);
+  copy_range(0, per < total ? per : total);
+  for (auto& th : pool) th.join();
   return DLA_OK;
 }
 

@@ -251,3 +251,19 @@ def test_result_memory_pool_reuses_blocks_only_after_release():
         assert small.numel() == 10
     finally:
         hm.set_result_memory(prev)
+
+
+def test_host_copy_batch_threaded_ranges(lib_path):
+    """dla_host_copy_batch splits batches above 8 MiB into equal byte ranges over threads (a
+    range may start and end inside a segment): every byte lands exactly once."""
+    import numpy as np
+
+    from accdfl_amd import _lib
+
+    rng = np.random.default_rng(0)
+    sizes = [int(x) for x in rng.integers(1, 200_000, size=400)] + [9_000_001, 0, 3]
+    src = [rng.integers(0, 255, size=s, dtype=np.uint8) for s in sizes]
+    dst = np.zeros(sum(sizes) + 64, dtype=np.uint8)
+    offs = np.cumsum([0] + sizes[:-1])
+    _lib.host_copy_batch([dst.ctypes.data + int(o) for o in offs], [a.ctypes.data for a in src], sizes)
+    assert np.array_equal(dst[: sum(sizes)], np.concatenate(src)) and not dst[sum(sizes):].any()

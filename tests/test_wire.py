@@ -232,3 +232,29 @@ def test_block_list_refuses_foreign_globals():
         wire.loads_state_dict(wire.payload_blocks(payload, 5))
     with pytest.raises(wire.UnsafePayloadError):
         wire.loads_state_dict(wire.payload_blocks(wire.serialize_model(nn.Linear(3, 2)), 64)[:-1])  # truncated
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16, torch.float64])
+def test_single_copy_serializer_is_the_reference_format(dtype):
+    """serialize_model writes tensors of >= 64 KiB with one copy (dumps_state_dict); the bytes
+    decode with the reference's own path — plain pickle.loads, i.e. torch's legacy
+    _load_from_bytes per storage, then load_state_dict (accdfl/core/models/__init__.py:13-16) —
+    to the same tensors, dtypes, shapes and _metadata, and with our restricted decoder."""
+    from accdfl_amd.core import wire
+
+    torch.manual_seed(3)
+    m = nn.Sequential(nn.Linear(300, 200), nn.BatchNorm1d(200), nn.Linear(200, 3)).to(dtype)
+    ref = m.state_dict()
+    data = wire.serialize_model(m)
+    assert b"_load_from_bytes" in data and b"_rebuild_tensor_v2" in data
+    sd = pickle.loads(data)
+    assert list(sd.keys()) == list(ref.keys()) and sd._metadata == ref._metadata
+    for k in ref:
+        assert sd[k].dtype == ref[k].dtype and torch.equal(sd[k], ref[k]), k
+    m2 = nn.Sequential(nn.Linear(300, 200), nn.BatchNorm1d(200), nn.Linear(200, 3)).to(dtype)
+    m2.load_state_dict(sd)
+    for k, v in wire.loads_state_dict(data).items():
+        assert torch.equal(v, ref[k]), k
+    # a tensor that does not own its storage (a view) takes the stock pickler, same result
+    view_sd = {"v": torch.arange(40_000, dtype=torch.float32)[7:30_007]}
+    assert torch.equal(pickle.loads(wire.dumps_state_dict(view_sd))["v"], view_sd["v"])
