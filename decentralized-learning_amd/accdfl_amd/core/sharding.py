@@ -129,6 +129,11 @@ class BucketShardedFedAvg:
         the sum across ranks, so it is NOT bit-exact.  Both orders are within
         (N-1)*u*sum|w_k p_k| of the exact sum (u = 2^-24), so per element
         |this - reference| <= N * 2^-23 * sum_k |w_k p_k| (fp32; the tolerance the tests state)."""
+        if not exact and self.dtype not in (torch.float32, torch.float64):
+            # the stated bound is derived for an fp32 / fp64 running sum; a 16-bit reduce-scatter
+            # rounds every cross-rank partial sum to 8 or 11 bits, which that bound does not cover
+            raise ValueError("aggregate_peer_sharded(exact=False) is offered for float32 / float64 only; "
+                             "use exact=True (all-to-all, bit-exact) for %s" % self.dtype)
         if exact:
             rows = self.transpose_peer_sharded(local_peers)
             out = self.reduce_bucket(list(rows), weights)

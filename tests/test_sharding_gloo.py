@@ -49,25 +49,34 @@ def _worker(rank, world, port, n_peers, n_elems, root, q, reducer="oracle"):
 
     for p in (os.path.join(root, "decentralized-learning_amd"), root):
         sys.path.insert(0, p)
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
+    nccl = reducer == "nccl"
+    dev = torch.device("cuda", rank) if nccl else torch.device("cpu")
+    if nccl:
+        torch.cuda.set_device(dev)
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    else:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
+        from accdfl_amd.core import wsum
         from accdfl_amd.core.sharding import BucketShardedFedAvg
 
         peers, weights = _inputs(n_peers, n_elems)
-        sh = BucketShardedFedAvg(n_elems, torch.float32,
-                                 reducer=_hip_reducer if reducer == "hip" else _oracle_reducer)
+        red = {"hip": _hip_reducer, "oracle": _oracle_reducer,
+               "nccl": lambda ps, w, out: wsum.wsum(list(ps), w, out=out)}[reducer]
+        sh = BucketShardedFedAvg(n_elems, torch.float32, device=dev, reducer=red)
         # (1) bucket-sharded: this rank holds its bucket of every peer
         s, e = sh.local_range
         buckets = [torch.from_numpy(peers[k, s:e].copy()) for k in range(n_peers)]
-        padded = [torch.cat([b, torch.zeros(sh.bucket_len - b.numel())]) for b in buckets]
+        padded = [torch.cat([b, torch.zeros(sh.bucket_len - b.numel())]).to(dev) for b in buckets]
         full = sh.all_gather(sh.reduce_bucket(padded, weights))
         # (2) peer-sharded: rank r holds whole peers r*m .. r*m+m-1
         m = n_peers // world
-        local = torch.from_numpy(peers[rank * m:(rank + 1) * m].copy())
+        local = torch.from_numpy(peers[rank * m:(rank + 1) * m].copy()).to(dev)
         full2 = sh.aggregate_peer_sharded(local, weights)
         full3 = sh.aggregate_peer_sharded(local, weights, exact=False)
-        q.put((rank, full.numpy().view(np.uint32).copy(), full2.numpy().view(np.uint32).copy(), full3.numpy().copy()))
+        q.put((rank, full.cpu().numpy().view(np.uint32).copy(), full2.cpu().numpy().view(np.uint32).copy(),
+               full3.cpu().numpy().copy()))
     finally:
         dist.destroy_process_group()
 
@@ -83,6 +92,25 @@ def test_sharded_fedavg_hip_reducer_is_bit_exact(world, n_peers, n_elems):
     """The same exchange steps with the libdlagg kernel as each rank's bucket reducer
     (gloo ranks sharing the box's one GPU; the RCCL transport is the driver's 8-GPU run)."""
     _run_sharded(world, n_peers, n_elems, "hip")
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not torch.cuda.is_available() or torch.cuda.device_count() < 2,
+                    reason="RCCL needs one GPU per rank (the driver's multi-GPU node)")
+@pytest.mark.parametrize("world,n_peers,n_elems", [(2, 8, 1_000_003)])
+def test_sharded_fedavg_over_rccl(world, n_peers, n_elems):
+    """The same exchange steps over RCCL (backend "nccl"), one GPU per rank, device tensors:
+    all-gather and all-to-all bit-exact, reduce-scatter within its stated bound."""
+    _run_sharded(world, n_peers, n_elems, "nccl")
+
+
+def test_reduce_scatter_mode_is_fp32_fp64_only():
+    """exact=False (reduce-scatter, re-associated) states its bound for fp32 / fp64 sums only."""
+    from accdfl_amd.core.sharding import BucketShardedFedAvg
+
+    sh = BucketShardedFedAvg(64, torch.bfloat16, reducer=_oracle_reducer)
+    with pytest.raises(ValueError, match="float32 / float64 only"):
+        sh.aggregate_peer_sharded(torch.zeros((2, 64), dtype=torch.bfloat16), exact=False)
 
 
 def _run_sharded(world, n_peers, n_elems, reducer):
