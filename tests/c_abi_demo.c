@@ -3,8 +3,8 @@
  * Builds with gcc against the HIP runtime for device allocation only:
  *   gcc -std=c11 -O2 -ffp-contract=off tests/c_abi_demo.c -Iinclude -I/opt/rocm/include \
  *       -D__HIP_PLATFORM_AMD__ -Ldecentralized-learning_amd/lib -ldlagg -L/opt/rocm/lib -lamdhip64 -o c_abi_demo
- * Runs FedAvg (dla_wsum, then a dla_plan with changed weights) and the teacher-logit mean
- * (dla_mean) on N peers and checks every element bit-for-bit against the reference's
+ * Runs FedAvg (dla_wsum, a dla_plan with changed weights, the bucket-sharded dla_wsum_sharded and
+ * the tile-interleaved dla_wsum_slab_tiled) and the teacher-logit mean (dla_mean) on N peers and checks every element bit-for-bit against the reference's
  * sequential arithmetic written out in C (fedavg.py:21-25).  Exit status 0 = all equal.
  */
 #include <hip/hip_runtime_api.h>
@@ -113,7 +113,57 @@ int main(void) {
     }
   }
 
-  /* 4. errors come back as codes with a message */
+  /* 4. bucket-sharded over the GPUs of this process (dla_wsum_sharded): three shards, every
+   *    one on device 0 here (ids may repeat), each writing its bucket straight into dev_out */
+  {
+    int ids[3] = {0, 0, 0};
+    void* outs[3] = {dev_out, dev_out, dev_out};
+    void* streams[3] = {NULL, NULL, NULL};
+    CHECK_HIP(hipMemset(dev_out, 0xff, sizeof(float) * P));
+    CHECK_DLA(dla_wsum_sharded(DLA_F32, 3, ids, (const void* const*)dev, w, N, P, outs, 0, streams));
+    CHECK_HIP(hipMemcpy(out_host, dev_out, sizeof(float) * P, hipMemcpyDeviceToHost));
+    for (int64_t j = 0; j < P; ++j) {
+      volatile float acc = host[0][j] * 0.0f;
+      for (int k = 0; k < N; ++k) {
+        volatile float prod = (float)w[k] * host[k][j];
+        acc = acc + prod;
+      }
+      if (!same_f32(acc, out_host[j])) {
+        fprintf(stderr, "dla_wsum_sharded mismatch at %lld\n", (long long)j);
+        return 1;
+      }
+    }
+    CHECK_DLA(dla_shutdown());
+  }
+
+  /* 5. the tile-interleaved slab (dla_wsum_slab_tiled): row k's tile t at (t * N + k) * T */
+  {
+    const int64_t T = dla_slab_tile_elems(DLA_F32, N, P);
+    const int64_t n_t = (P + T - 1) / T;
+    float* tiled = (float*)calloc((size_t)(n_t * N * T), sizeof(float));
+    void* dev_tiled;
+    for (int k = 0; k < N; ++k)
+      for (int64_t j = 0; j < P; ++j) tiled[((j / T) * N + k) * T + j % T] = host[k][j];
+    CHECK_HIP(hipMalloc(&dev_tiled, sizeof(float) * (size_t)(n_t * N * T)));
+    CHECK_HIP(hipMemcpy(dev_tiled, tiled, sizeof(float) * (size_t)(n_t * N * T), hipMemcpyHostToDevice));
+    CHECK_DLA(dla_wsum_slab_tiled(DLA_F32, dev_tiled, T, N, w, N, P, dev_out, NULL, NULL));
+    CHECK_HIP(hipMemcpy(out_host, dev_out, sizeof(float) * P, hipMemcpyDeviceToHost));
+    for (int64_t j = 0; j < P; ++j) {
+      volatile float acc = host[0][j] * 0.0f;
+      for (int k = 0; k < N; ++k) {
+        volatile float prod = (float)w[k] * host[k][j];
+        acc = acc + prod;
+      }
+      if (!same_f32(acc, out_host[j])) {
+        fprintf(stderr, "dla_wsum_slab_tiled mismatch at %lld\n", (long long)j);
+        return 1;
+      }
+    }
+    CHECK_HIP(hipFree(dev_tiled));
+    free(tiled);
+  }
+
+  /* 6. errors come back as codes with a message */
   if (dla_wsum(DLA_F32, (const void* const*)dev, w, 0, P, dev_out, NULL) != DLA_E_INVALID ||
       strlen(dla_last_error()) == 0) {
     fprintf(stderr, "expected DLA_E_INVALID for n_peers = 0\n");
@@ -126,6 +176,7 @@ int main(void) {
   }
   CHECK_HIP(hipFree(dev_out));
   free(out_host);
-  printf("c_abi_demo ok: dla_wsum, dla_plan, dla_mean bit-exact on %d peers x %lld fp32\n", N, (long long)P);
+  printf("c_abi_demo ok: dla_wsum, dla_plan, dla_mean, dla_wsum_sharded, dla_wsum_slab_tiled bit-exact on %d peers "
+         "x %lld fp32\n", N, (long long)P);
   return 0;
 }
