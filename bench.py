@@ -730,7 +730,7 @@ def time_graph(launch, per_graph=20, reps=10):
     return ev0.elapsed_time(ev1) / 1e3 / (reps * per_graph)
 
 
-def baseline_configs(device, steps=50, cpu=True):
+def baseline_configs(device, steps=40, cpu=True):
     """Device-resident reduce rate of each BASELINE config's per-GPU share staged as PeerSlab
     holds it (SlabInput, a prepared launch; bytes = (N + 1) * share * sizeof), beside the reference op sequence
     on the host's cores for the same share (flat, one tensor per peer: a lower bound on
@@ -744,7 +744,9 @@ def baseline_configs(device, steps=50, cpu=True):
         share = -(-params // gpus)
         inp = SlabInput(n, share, dt, device, 1000, [float(1.0 / n)] * n)
         sp = torch.cuda.current_stream().cuda_stream
-        _, ev = time_kernel(lambda: inp.launch(sp), steps, 10, 1)
+        # median of 5 timed runs of `steps` launches (the first run after the slab's setup
+        # idles the GPU reads a few % slow)
+        ev = statistics.median(time_kernel(lambda: inp.launch(sp), steps, 10, 1)[1] for _ in range(5))
         tg = time_graph(inp.launch)
         byts = (n + 1) * share * es
         res[name] = {"peers": n, "params_per_gpu": share, "dtype": dts, "us_per_reduce": round(ev / steps * 1e6, 2),

@@ -62,47 +62,68 @@ class _BlobUnpickler(pickle.Unpickler):
 
 class _Span:
     """A byte range of a block list (EVA's ``data_list``) that crosses block boundaries:
-    kept as pieces (memoryviews into the blocks), never joined unless asked."""
-    __slots__ = ("pieces", "n")
+    kept as pieces (memoryviews into the blocks, and their host addresses), never joined
+    unless asked."""
+    __slots__ = ("pieces", "addrs", "n")
 
-    def __init__(self, pieces):
+    def __init__(self, pieces, addrs):
         self.pieces = pieces
+        self.addrs = addrs
         self.n = sum(len(p) for p in pieces)
 
     def __len__(self):
         return self.n
 
-    def sub(self, a: int, b: int) -> "list":
-        """The pieces covering [a, b) of this span."""
-        out, off = [], 0
-        for p in self.pieces:
+    def sub(self, a: int, b: int):
+        """(pieces, addresses) covering [a, b) of this span."""
+        out, adr, off = [], [], 0
+        for p, q in zip(self.pieces, self.addrs):
             s, e = max(a, off), min(b, off + len(p))
             if s < e:
                 out.append(p[s - off:e - off])
+                adr.append(q + (s - off))
             off += len(p)
             if off >= b:
                 break
-        return out
+        return out, adr
 
     def read(self, a: int, b: int) -> bytes:
-        return b"".join(self.sub(a, b))
+        return b"".join(self.sub(a, b)[0])
 
 
-def _gather(pieces, dst: torch.Tensor) -> None:
+_BYTES_DATA = bytes.__basicsize__ - 1  # CPython: offset of a bytes object's payload
+
+
+def _check_bytes_layout() -> bool:
+    import ctypes
+
+    probe = b"accdfl-amd-probe"
+    return ctypes.string_at(id(probe) + _BYTES_DATA, len(probe)) == probe
+
+
+_BYTES_ADDR_OK = _check_bytes_layout()
+
+
+def _block_address(block) -> int:
+    """Host address of a block's first byte (no copy): bytes objects from the object itself,
+    other buffers through numpy."""
+    if type(block) is bytes and _BYTES_ADDR_OK:
+        return id(block) + _BYTES_DATA
+    return np.frombuffer(block, dtype=np.uint8).__array_interface__["data"][0]
+
+
+def _gather(pieces, addrs, dst: torch.Tensor) -> None:
     """Copy the pieces back to back into the host uint8 tensor ``dst`` (one native batched
-    memcpy: libdlagg's dla_host_copy_batch)."""
+    memcpy, threaded above 8 MiB: libdlagg's dla_host_copy_batch)."""
     from accdfl_amd import _lib
 
-    dsts, srcs, sizes, keep, off = [], [], [], [], 0
+    dsts, sizes, off = [], [], 0
     base = dst.data_ptr()
     for p in pieces:
-        a = np.frombuffer(p, dtype=np.uint8)
-        keep.append(a)
         dsts.append(base + off)
-        srcs.append(a.ctypes.data)
         sizes.append(len(p))
         off += len(p)
-    _lib.host_copy_batch(dsts, srcs, sizes)
+    _lib.host_copy_batch(dsts, addrs, sizes)
 
 
 def _parse_storage_blob(blob, alloc=None) -> torch.TypedStorage:
@@ -141,10 +162,10 @@ def _parse_storage_blob(blob, alloc=None) -> torch.TypedStorage:
     if numel == 0:
         data = torch.empty(0, dtype=dtype)
     elif span is not None:
-        pieces = span.sub(start, start + nbytes)
+        pieces, addrs = span.sub(start, start + nbytes)
         if alloc is not None:
             dst = alloc(nbytes)
-            _gather(pieces, dst)
+            _gather(pieces, addrs, dst)
             data = dst.view(dtype)
         else:
             data = torch.frombuffer(bytearray(b"".join(pieces)), dtype=dtype)
@@ -203,10 +224,18 @@ class _BlockReader:
     memoryview into it, a short read across blocks is joined, a long one is a _Span."""
 
     def __init__(self, blocks):
-        self.views = [memoryview(b).cast("B") for b in blocks if len(b)]
+        self.blocks = [b for b in blocks if len(b)]
+        self.views = [memoryview(b).cast("B") for b in self.blocks]
+        self.addr = [None] * len(self.blocks)
         self.bi = 0      # current block
         self.bo = 0      # offset in it
         self.left = sum(len(v) for v in self.views)
+
+    def _addr(self, i: int) -> int:
+        a = self.addr[i]
+        if a is None:
+            a = self.addr[i] = _block_address(self.blocks[i])
+        return a
 
     def take(self, k: int):
         if k > self.left:
@@ -219,16 +248,19 @@ class _BlockReader:
             if self.bo == len(v):
                 self.bi, self.bo = self.bi + 1, 0
             return out
-        pieces = []
+        long = k > 4096
+        pieces, addrs = [], []
         while k:
             v = self.views[self.bi]
             m = min(k, len(v) - self.bo)
             pieces.append(v[self.bo:self.bo + m])
+            if long:
+                addrs.append(self._addr(self.bi) + self.bo)
             self.bo += m
             k -= m
             if self.bo == len(v):
                 self.bi, self.bo = self.bi + 1, 0
-        return b"".join(pieces) if sum(len(p) for p in pieces) <= 4096 else _Span(pieces)
+        return _Span(pieces, addrs) if long else b"".join(pieces)
 
 
 def _vm_loads(data, alloc: Optional[Callable[[int], torch.Tensor]] = None) -> object:
