@@ -61,34 +61,37 @@ class _BlobUnpickler(pickle.Unpickler):
 
 
 class _Span:
-    """A byte range of a block list (EVA's ``data_list``) that crosses block boundaries:
-    kept as pieces (memoryviews into the blocks, and their host addresses), never joined
-    unless asked."""
-    __slots__ = ("pieces", "addrs", "n")
+    """A byte range of a block list (EVA's ``data_list``) that crosses block boundaries, kept
+    as (host address, length) pieces of the blocks — never joined unless asked.  ``owner``
+    keeps the blocks alive."""
+    __slots__ = ("addrs", "lens", "n", "owner")
 
-    def __init__(self, pieces, addrs):
-        self.pieces = pieces
+    def __init__(self, addrs, lens, owner):
         self.addrs = addrs
-        self.n = sum(len(p) for p in pieces)
+        self.lens = lens
+        self.n = sum(lens)
+        self.owner = owner
 
     def __len__(self):
         return self.n
 
     def sub(self, a: int, b: int):
-        """(pieces, addresses) covering [a, b) of this span."""
-        out, adr, off = [], [], 0
-        for p, q in zip(self.pieces, self.addrs):
-            s, e = max(a, off), min(b, off + len(p))
+        """(addresses, lengths) of the pieces covering [a, b) of this span."""
+        out_a, out_l, off = [], [], 0
+        for q, ln in zip(self.addrs, self.lens):
+            s, e = max(a, off), min(b, off + ln)
             if s < e:
-                out.append(p[s - off:e - off])
-                adr.append(q + (s - off))
-            off += len(p)
+                out_a.append(q + (s - off))
+                out_l.append(e - s)
+            off += ln
             if off >= b:
                 break
-        return out, adr
+        return out_a, out_l
 
     def read(self, a: int, b: int) -> bytes:
-        return b"".join(self.sub(a, b)[0])
+        import ctypes
+
+        return b"".join(ctypes.string_at(q, ln) for q, ln in zip(*self.sub(a, b)))
 
 
 _BYTES_DATA = bytes.__basicsize__ - 1  # CPython: offset of a bytes object's payload
@@ -112,18 +115,16 @@ def _block_address(block) -> int:
     return np.frombuffer(block, dtype=np.uint8).__array_interface__["data"][0]
 
 
-def _gather(pieces, addrs, dst: torch.Tensor) -> None:
+def _gather(addrs, lens, dst: torch.Tensor) -> None:
     """Copy the pieces back to back into the host uint8 tensor ``dst`` (one native batched
     memcpy, threaded above 8 MiB: libdlagg's dla_host_copy_batch)."""
     from accdfl_amd import _lib
 
-    dsts, sizes, off = [], [], 0
-    base = dst.data_ptr()
-    for p in pieces:
-        dsts.append(base + off)
-        sizes.append(len(p))
-        off += len(p)
-    _lib.host_copy_batch(dsts, addrs, sizes)
+    dsts, off = [], dst.data_ptr()
+    for ln in lens:
+        dsts.append(off)
+        off += ln
+    _lib.host_copy_batch(dsts, addrs, lens)
 
 
 def _parse_storage_blob(blob, alloc=None) -> torch.TypedStorage:
@@ -162,13 +163,12 @@ def _parse_storage_blob(blob, alloc=None) -> torch.TypedStorage:
     if numel == 0:
         data = torch.empty(0, dtype=dtype)
     elif span is not None:
-        pieces, addrs = span.sub(start, start + nbytes)
         if alloc is not None:
             dst = alloc(nbytes)
-            _gather(pieces, addrs, dst)
+            _gather(*span.sub(start, start + nbytes), dst)
             data = dst.view(dtype)
         else:
-            data = torch.frombuffer(bytearray(b"".join(pieces)), dtype=dtype)
+            data = torch.frombuffer(bytearray(span.read(start, start + nbytes)), dtype=dtype)
     else:
         import warnings
 
@@ -248,19 +248,30 @@ class _BlockReader:
             if self.bo == len(v):
                 self.bi, self.bo = self.bi + 1, 0
             return out
-        long = k > 4096
-        pieces, addrs = [], []
+        if k <= 4096:  # a short read across a block boundary: joined
+            pieces = []
+            while k:
+                v = self.views[self.bi]
+                m = min(k, len(v) - self.bo)
+                pieces.append(v[self.bo:self.bo + m])
+                self.bo += m
+                k -= m
+                if self.bo == len(v):
+                    self.bi, self.bo = self.bi + 1, 0
+            return b"".join(pieces)
+        addrs, lens = [], []
+        views, addr = self.views, self._addr
+        bi, bo = self.bi, self.bo
         while k:
-            v = self.views[self.bi]
-            m = min(k, len(v) - self.bo)
-            pieces.append(v[self.bo:self.bo + m])
-            if long:
-                addrs.append(self._addr(self.bi) + self.bo)
-            self.bo += m
+            m = min(k, len(views[bi]) - bo)
+            addrs.append(addr(bi) + bo)
+            lens.append(m)
+            bo += m
             k -= m
-            if self.bo == len(v):
-                self.bi, self.bo = self.bi + 1, 0
-        return _Span(pieces, addrs) if long else b"".join(pieces)
+            if bo == len(views[bi]):
+                bi, bo = bi + 1, 0
+        self.bi, self.bo = bi, bo
+        return _Span(addrs, lens, self.blocks)
 
 
 def _vm_loads(data, alloc: Optional[Callable[[int], torch.Tensor]] = None) -> object:

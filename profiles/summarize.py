@@ -35,7 +35,7 @@ if stats:
 # configs at other grid sizes, so the per-name stats file mixes them).
 kname, kgrid = None, None
 # the kernel the bench's headline launch used, as the bench line names it (dla_select_kernel)
-bench_kernel, bench_peers = KERNEL, 8
+bench_kernel, bench_peers, bench_tiled = KERNEL, 8, False
 DTYPES = {"f32": (0, 4), "bf16": (1, 2), "f16": (2, 2)}  # bench --dtype -> (DLA dtype code, bytes)
 dtype_name = args[args.index("--dtype") + 1] if "--dtype" in args else "f32"
 dtype_code, esize = DTYPES[dtype_name]
@@ -46,6 +46,7 @@ if os.path.exists(trace_log):
             try:
                 d = json.loads(line)
                 bench_kernel = d["roofline"]["kernel"].split()[0]
+                bench_tiled = "tile-interleaved" in d["roofline"]["kernel"]
                 bench_peers = int(d["config"]["n_peers"])
             except (ValueError, KeyError):
                 pass
@@ -63,6 +64,8 @@ if trace:
     kmax = 8 if bench_peers <= 8 else 32 if bench_peers <= 32 else 128
     lead = "%d, %d," % (dtype_code, bench_peers if bench_kernel == "wsum_bigtile_kernel" else kmax)
     ns = {k: v for k, v in groups.items() if k[0].split(bench_kernel + "<")[1].startswith(lead)}
+    if bench_kernel == "wsum_vec_kernel":  # the TILED template flag: the headline, not separate_buffers
+        ns = {k: v for k, v in ns.items() if (", true>(" in k[0]) == bench_tiled}
     groups = ns or groups
     if groups:
         (kname, kgrid), durs = max(groups.items(), key=lambda kv: sum(kv[1]))
