@@ -97,6 +97,8 @@ def parse():
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) for real runs; gloo only to rehearse "
                                                              "several ranks on one GPU")
     ap.add_argument("--no-strong", action="store_true", help="skip the strong-scaling (fixed-model) lines")
+    ap.add_argument("--settle-ms", type=float, default=200.0,
+                    help="untimed launches before each measurement's warmup (clock ramp)")
     ap.add_argument("--layout", default="slab", choices=["slab", "rows"],
                     help="HBM layout of the headline's peers: the PeerSlab tile-interleaved slab (default) or "
                          "one buffer per peer")
@@ -228,9 +230,21 @@ class SlabInput:
         self.plan.launch(stream_ptr)
 
 
-def time_kernel(fn, steps, warmup, world):
-    """Warmup, then exactly `steps` calls bracketed by barrier + synchronize; returns
-    (wall seconds max over ranks, HIP-event seconds on the launch stream)."""
+SETTLE_S = 0.2  # --settle-ms: untimed launches before the warmup (GPU clocks ramp under load)
+
+
+def time_kernel(fn, steps, warmup, world, settle_s=None):
+    """Untimed launches for `settle_s` (the GPU ramps its clocks over the first tens of ms of
+    load: a 25-launch run right after setup reads several % slow), `warmup` untimed calls,
+    then exactly `steps` calls bracketed by barrier + synchronize; returns (wall seconds max
+    over ranks, HIP-event seconds on the launch stream)."""
+    settle_s = SETTLE_S if settle_s is None else settle_s
+    if settle_s > 0:
+        t_end = time.perf_counter() + settle_s
+        while time.perf_counter() < t_end:
+            for _ in range(8):
+                fn()
+            torch.cuda.synchronize()
     for _ in range(warmup):
         fn()
     stream = torch.cuda.current_stream()
@@ -489,7 +503,7 @@ def collectives(n, p, dt, es, world, device, slab, w, iters=10):
     sh = BucketShardedFedAvg(p * world, dt, device=cdev, reducer=reducer)
     bucket = torch.zeros(sh.bucket_len, dtype=dt, device=cdev)
     full = torch.empty(p * world, dtype=dt, device=cdev)
-    wall, _ = time_kernel(lambda: sh.all_gather(bucket, full), iters, 2, world)
+    wall, _ = time_kernel(lambda: sh.all_gather(bucket, full), iters, 2, world, settle_s=0)
     res["allgather"] = {"ms": round(wall / iters * 1e3, 3), "bytes_out_per_rank": p * world * es,
                         "GBps_per_rank_in": round((world - 1) * sh.bucket_len * es / (wall / iters) / 1e9, 1)}
     if n % world == 0:
@@ -497,7 +511,7 @@ def collectives(n, p, dt, es, world, device, slab, w, iters=10):
         local = torch.empty((m, p * world), dtype=dt, device=cdev).normal_(0.0, 0.05)
         for exact in (True, False):
             fn = lambda: sh.aggregate_peer_sharded(local, w, exact=exact)  # noqa: E731
-            wall, _ = time_kernel(fn, iters, 2, world)
+            wall, _ = time_kernel(fn, iters, 2, world, settle_s=0)
             key = "peer_sharded_exact" if exact else "peer_sharded_reduce_scatter"
             res[key] = {"ms": round(wall / iters * 1e3, 3), "peers_per_rank": m,
                         "model_params": p * world, "bit_exact": exact}
@@ -744,9 +758,9 @@ def baseline_configs(device, steps=40, cpu=True):
         share = -(-params // gpus)
         inp = SlabInput(n, share, dt, device, 1000, [float(1.0 / n)] * n)
         sp = torch.cuda.current_stream().cuda_stream
-        # median of 5 timed runs of `steps` launches (the first run after the slab's setup
-        # idles the GPU reads a few % slow)
-        ev = statistics.median(time_kernel(lambda: inp.launch(sp), steps, 10, 1)[1] for _ in range(5))
+        # median of 5 timed runs of `steps` launches, the first after the settle phase
+        ev = statistics.median(time_kernel(lambda: inp.launch(sp), steps, 10, 1, settle_s=None if i == 0 else 0)[1]
+                               for i in range(5))
         tg = time_graph(inp.launch)
         byts = (n + 1) * share * es
         res[name] = {"peers": n, "params_per_gpu": share, "dtype": dts, "us_per_reduce": round(ev / steps * 1e6, 2),
@@ -831,7 +845,7 @@ def strong_scaling(rank, world, device, steps, warmup):
                 sh = BucketShardedFedAvg(params, dt, device=cdev)
                 bucket = torch.zeros(sh.bucket_len, dtype=dt, device=cdev)
                 full = torch.empty(params, dtype=dt, device=cdev)
-                wall_g, _ = time_kernel(lambda: sh.all_gather(bucket, full), 10, 2, world)
+                wall_g, _ = time_kernel(lambda: sh.all_gather(bucket, full), 10, 2, world, settle_s=0)
                 row["allgather_ms"] = round(wall_g / 10 * 1e3, 4)
                 row["with_allgather_value"] = round(total / (wall / steps + wall_g / 10) / 1e9, 2)
                 del bucket, full
@@ -889,7 +903,7 @@ def sweep(args, device):
                 sl = make_slab(args.peers, pitch, dt, device, 1000)
                 pp = [sl[k].data_ptr() for k in range(args.peers)]
                 fn = lambda: _lib.wsum_ptrs(code, pp, w, args.params, out.data_ptr(), sp)  # noqa: E731
-                _, ev = time_kernel(fn, 50, 5, 1)
+                _, ev = time_kernel(fn, 50, 5, 1, settle_s=0.02)
                 res.setdefault(pad, []).append(ev / 50)
                 del sl
                 torch.cuda.empty_cache()  # fresh physical pages for the next allocation
@@ -908,14 +922,14 @@ def sweep(args, device):
         variants = [int(x) for x in (args.sweep_cfgs.split(",") if args.sweep_cfgs else ["9", "12", "10"])]
         for rnd in range(5):
             fn = lambda: _lib.wsum_ptrs(code, ptrs, w, args.params, out.data_ptr(), sp)  # noqa: E731
-            _, ev = time_kernel(fn, 50, 5, 1)
+            _, ev = time_kernel(fn, 50, 5, 1, settle_s=0.02)
             res.setdefault(("row-major default", 0), []).append(ev / 50)
             for tb in tiles:
                 for v in variants:
                     cfg = _lib.LaunchCfg(v, 0, 0, 0)
                     fn = lambda: _lib.wsum_slab_tiled_ptr(code, slabs[tb].data_ptr(), tb // es, args.peers, w,  # noqa
                                                           args.params, out.data_ptr(), sp, cfg)
-                    _, ev = time_kernel(fn, 50, 5, 1)
+                    _, ev = time_kernel(fn, 50, 5, 1, settle_s=0.02)
                     res.setdefault(("tiled %d B" % tb, v), []).append(ev / 50)
         for t, k in sorted((statistics.median(v), k) for k, v in res.items()):
             print(json.dumps({"layout": k[0], "variant": k[1], "us": round(t * 1e6, 2),
@@ -938,7 +952,7 @@ def sweep(args, device):
                     cfg = _lib.LaunchCfg(*c)
                     fn = lambda: so.dla_wsum_ex(code, pa, wa, len(ptrs), args.params, out.data_ptr(), sp,  # noqa
                                                 ctypes.byref(cfg))
-                    _, ev = time_kernel(fn, 50, 5, 1)
+                    _, ev = time_kernel(fn, 50, 5, 1, settle_s=0.02)
                     res[(name,) + c].append(ev / 50)
         byts = (args.peers + 1) * args.params * es
         for t, k in sorted((statistics.median(v), k) for k, v in res.items()):
@@ -950,7 +964,7 @@ def sweep(args, device):
         for c in cfgs:
             cfg = _lib.LaunchCfg(*c)
             fn = lambda: _lib.wsum_ptrs(code, ptrs, w, args.params, out.data_ptr(), sp, cfg)  # noqa: E731
-            _, ev = time_kernel(fn, 50, 5, 1)
+            _, ev = time_kernel(fn, 50, 5, 1, settle_s=0.02)
             res[c].append(ev / 50)
     byts = (args.peers + 1) * args.params * es
     # in place: the average overwrites peer 0's row (allowed by the ABI: out may alias peers[0])
@@ -960,7 +974,7 @@ def sweep(args, device):
         res[key] = []
         for rnd in range(5):
             fn = lambda: _lib.wsum_ptrs(code, ptrs, w, args.params, ptrs[0], sp, cfg)  # noqa: E731
-            _, ev = time_kernel(fn, 50, 5, 1)
+            _, ev = time_kernel(fn, 50, 5, 1, settle_s=0.02)
             res[key].append(ev / 50)
     rows = sorted(((statistics.median(v), c) for c, v in res.items()))
     for t, c in rows:
@@ -991,12 +1005,12 @@ def measured_ceilings(device, nbytes=1 << 30):
     res = {}
     for ch in (1, 4, 8):
         for nt in (0, 1):
-            _, ev = time_kernel(lambda: so.dlp_read(a.data_ptr(), nbytes, sink.data_ptr(), ch, nt, sp()), 30, 3, 1)
+            _, ev = time_kernel(lambda: so.dlp_read(a.data_ptr(), nbytes, sink.data_ptr(), ch, nt, sp()), 30, 3, 1, settle_s=0.02)
             res["read_ch%d_nt%d" % (ch, nt)] = round(nbytes / (ev / 30) / 1e9, 1)
     for nt in (0, 1):
-        _, ev = time_kernel(lambda: so.dlp_copy(a.data_ptr(), b.data_ptr(), nbytes, nt, sp()), 30, 3, 1)
+        _, ev = time_kernel(lambda: so.dlp_copy(a.data_ptr(), b.data_ptr(), nbytes, nt, sp()), 30, 3, 1, settle_s=0.02)
         res["copy_nt%d" % nt] = round(2 * nbytes / (ev / 30) / 1e9, 1)
-    _, ev = time_kernel(lambda: b.copy_(a), 30, 3, 1)
+    _, ev = time_kernel(lambda: b.copy_(a), 30, 3, 1, settle_s=0.02)
     res["torch_copy"] = round(2 * nbytes / (ev / 30) / 1e9, 1)
     del a, b
     # the FedAvg access pattern without arithmetic: 8 streams of 100 MB (+ 1 output stream)
@@ -1018,7 +1032,7 @@ def measured_ceilings(device, nbytes=1 << 30):
     so.dlp_policy8.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
     for rnd in range(3):
         for pol, name in enumerate(("nt", "sc1", "sc0sc1", "sc0sc1nt", "sc1nt")):
-            _, ev = time_kernel(lambda: so.dlp_policy8(arr, each, dst.data_ptr(), pol, sp()), 30, 3, 1)
+            _, ev = time_kernel(lambda: so.dlp_policy8(arr, each, dst.data_ptr(), pol, sp()), 30, 3, 1, settle_s=0.02)
             res["policy8_%s_r%d" % (name, rnd)] = round(9 * each / (ev / 30) / 1e9, 1)
     del srcs
     # tile-interleaved peer layout ([tiles][8 (+1 out)][T]) — one contiguous region per workgroup
@@ -1035,6 +1049,8 @@ def measured_ceilings(device, nbytes=1 << 30):
 
 def main():
     args = parse()
+    global SETTLE_S
+    SETTLE_S = args.settle_ms / 1e3
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(spawn_ranks(args))  # nothing has touched a GPU in this process
     rank, world, device, cpu_group = setup_dist(args)
