@@ -530,15 +530,12 @@ __global__ __launch_bounds__(BS) void wsum_stream_kernel(
 // the same box: 8-stream read alone 116.4-117.5 us + the 100 MB sc1 write alone 14.8 us.
 template <int DT, int NP, int BT>
 __device__ __attribute__((always_inline)) inline void fold_big_tile(
-    const void* const* __restrict__ p, const typename Ops<DT>::w_t* __restrict__ w, int64_t in_base,
-    int64_t base, uint4* __restrict__ out) {
+    const void* const* __restrict__ p, const typename Ops<DT>::w_t* __restrict__ w, int64_t base,
+    int64_t n_chunks, uint4* __restrict__ out) {
   using O = Ops<DT>;
   using acc_t = typename O::acc_t;
   constexpr int E = O::E;
-  // chunk c of this lane: in_base + c * 64 in every peer (the tile's place in the input: the
-  // same as the output's in one buffer per peer, t * rows * tile in the tile-interleaved slab),
-  // base + c * 64 in the output (full tiles only: one base plus immediate offsets)
-  auto in_at = [&](int c) -> int64_t { return in_base + c * 64; };
+  // chunk c of this lane: base + c * 64 (full tiles only: one base plus immediate offsets)
   auto at = [&](int c) -> int64_t { return base + c * 64; };
   // pointers and weights into registers first: the compiler barrier below must not force
   // them to be re-read from the kernel-argument segment
@@ -552,12 +549,12 @@ __device__ __attribute__((always_inline)) inline void fold_big_tile(
   acc_t acc[BT][E];
   u32x4 a[BT], b[BT];
 #pragma unroll
-  for (int c = 0; c < BT; ++c) a[c] = __builtin_nontemporal_load(src[0] + in_at(c));
+  for (int c = 0; c < BT; ++c) a[c] = __builtin_nontemporal_load(src[0] + at(c));
 #pragma unroll
   for (int k = 0; k < NP; ++k) {
     if (k + 1 < NP) {
 #pragma unroll
-      for (int c = 0; c < BT; ++c) b[c] = __builtin_nontemporal_load(src[k + 1] + in_at(c));
+      for (int c = 0; c < BT; ++c) b[c] = __builtin_nontemporal_load(src[k + 1] + at(c));
     }
     asm volatile("" ::: "memory");  // peer k+2's loads stay below peer k's fold: two buffers
     const typename O::w_t wk = wv[k];
@@ -588,15 +585,11 @@ __device__ __attribute__((always_inline)) inline void fold_big_tile(
 // tile.  Balanced launch (variant 17): n_big = whole rounds of resident big tiles only, and
 // the rest spread over up to one round of segment workgroups, so a partial last round does
 // not leave most of the chip idle.
-// in_stride: chunks between consecutive big tiles of one peer in the input — kTile for one
-// buffer per peer, rows * kTile for the tile-interleaved slab whose tile is one big tile
-// (dla_wsum_slab_tiled with 16 KiB tiles; plain launch only, the chunks after the full tiles
-// then lie in one last slab tile).
 template <int DT, int NP, int BT, int KMAX = 8>
 __global__ __launch_bounds__(64) void wsum_bigtile_kernel(const PeerTable<typename Ops<DT>::w_t, KMAX> tab,
                                                           int64_t n_chunks, int64_t n_elems,
                                                           int64_t n_big, int64_t n_seg_wg,
-                                                          void* __restrict__ out_v, int64_t in_stride) {
+                                                          void* __restrict__ out_v) {
   constexpr int64_t kTile = 64 * BT;
   const int64_t b = blockIdx.x;
   uint4* out = static_cast<uint4*>(out_v);
@@ -606,21 +599,15 @@ __global__ __launch_bounds__(64) void wsum_bigtile_kernel(const PeerTable<typena
     // loads outstanding, <= 256 VGPRs); as straight-line code it waits for every load before
     // each fold and spills the peers' data into AGPRs.
     for (int64_t t = b; t < n_big; t += gridDim.x)
-      fold_big_tile<DT, NP, BT>(tab.p, tab.w, t * in_stride + threadIdx.x, t * kTile + threadIdx.x, out);
+      fold_big_tile<DT, NP, BT>(tab.p, tab.w, t * kTile + threadIdx.x, n_chunks, out);
     return;
   }
-  // the chunks after the big tiles: input chunk i (i >= n_big * kTile) sits at
-  // i + n_big * (in_stride - kTile) of every peer (no shift with one buffer per peer)
-  const void* ps[NP];
-  const int64_t shift = n_big * (in_stride - kTile) * 16;
-#pragma unroll
-  for (int k = 0; k < NP; ++k) ps[k] = static_cast<const char*>(tab.p[k]) + shift;
-  if (b < n_big + n_seg_wg) {  // as 64-chunk segments
+  if (b < n_big + n_seg_wg) {  // the chunks after the big tiles, as 64-chunk segments
     for (int64_t t0 = n_big * kTile + (b - n_big) * 64; t0 < n_chunks; t0 += n_seg_wg * 64)
-      fold_tile<DT, 64, 1, true, 2, false>(ps, tab.w, NP, t0, n_chunks, out);
+      fold_tile<DT, 64, 1, true, 2, false>(tab.p, tab.w, NP, t0, n_chunks, out);
     return;
   }
-  fold_tail<DT, false>(ps, tab.w, NP, n_chunks * Ops<DT>::E, n_elems, out_v);  // no-op without a tail
+  fold_tail<DT, false>(tab.p, tab.w, NP, n_chunks * Ops<DT>::E, n_elems, out_v);  // no-op without a tail
 }
 
 // ------------------------------------------------ word-per-lane ("wide") kernel
@@ -1196,29 +1183,6 @@ hipError_t launch_vec_tiled(const PeerTable<typename Ops<DT>::w_t, KMAX>& tab, i
   }
 }
 
-template <int DT, int KMAX>
-hipError_t launch_bigtile(const PeerTable<typename Ops<DT>::w_t, KMAX>& tab, int n, int64_t n_elems, void* out,
-                          hipStream_t s, bool balanced, int64_t in_stride = 64 * kBigTileChunks);
-
-// Variant 16 over the tile-interleaved slab: the big-tile kernel reading one slab tile (exactly
-// one 16 KiB big tile) of each peer in turn — fp32, the pass's peer count one it is built for.
-template <int DT>
-bool tiled_bigtile(int variant, int m, int64_t tile_elems) {
-  return DT == DLA_F32 && variant == 16 && tile_elems * 4 == 64 * kBigTileChunks * 16 &&
-         (m <= 8 || m == 16 || m == 32);
-}
-
-template <int DT, int KM>
-hipError_t tiled_pass(const PeerTable<typename Ops<DT>::w_t, KM>& tab, int m, bool acc_in, int64_t n_elems, void* out,
-                      hipStream_t s, int variant, int64_t tile_elems, int tshift, int64_t stride_elems) {
-  if constexpr (DT == DLA_F32 && KM != kMaxPeersPerPass) {
-    if (!acc_in && tiled_bigtile<DT>(variant, m, tile_elems))
-      return launch_bigtile<DT, KM>(tab, m, n_elems, out, s, false, stride_elems / Ops<DT>::E);
-  }
-  return acc_in ? launch_vec_tiled<DT, KM, true>(tab, m, n_elems, out, s, variant, tshift, stride_elems)
-                : launch_vec_tiled<DT, KM, false>(tab, m, n_elems, out, s, variant, tshift, stride_elems);
-}
-
 template <int DT>
 hipError_t run_tiled(const void* base, int64_t tile_elems, int tshift, int64_t stride_elems, const double* weights,
                      int n, int64_t n_elems, void* out, hipStream_t s, int variant) {
@@ -1234,7 +1198,8 @@ hipError_t run_tiled(const void* base, int64_t tile_elems, int tshift, int64_t s
       tab.p[k] = static_cast<const char*>(base) + (k0 + k) * tile_elems * es;                                \
       tab.w[k] = static_cast<typename Ops<DT>::w_t>(weights[k0 + k]);                                        \
     }                                                                                                        \
-    e = tiled_pass<DT, KM>(tab, m, k0 > 0, n_elems, out, s, variant, tile_elems, tshift, stride_elems);       \
+    e = k0 > 0 ? launch_vec_tiled<DT, KM, true>(tab, m, n_elems, out, s, variant, tshift, stride_elems)       \
+               : launch_vec_tiled<DT, KM, false>(tab, m, n_elems, out, s, variant, tshift, stride_elems);     \
   } while (0)
     if (m <= 8)
       DLA_TILED_PASS(8);
@@ -1250,10 +1215,9 @@ hipError_t run_tiled(const void* base, int64_t tile_elems, int tshift, int64_t s
 
 template <int DT, int KMAX>
 hipError_t launch_bigtile(const PeerTable<typename Ops<DT>::w_t, KMAX>& tab, int n, int64_t n_elems, void* out,
-                          hipStream_t s, bool balanced, int64_t in_stride) {
+                          hipStream_t s, bool balanced) {
   constexpr int BT = kBigTileChunks;
   constexpr int64_t kTile = 64 * BT;
-  if (in_stride != kTile && balanced) return hipErrorInvalidValue;  // tiled input: plain launch only
   const int64_t n_chunks = n_elems / Ops<DT>::E;
   const int64_t n_full = n_chunks / kTile;
   int64_t n_big = n_full, n_seg_wg = n_full * kTile < n_chunks ? 1 : 0;  // + the partial-tile workgroup
@@ -1268,7 +1232,7 @@ hipError_t launch_bigtile(const PeerTable<typename Ops<DT>::w_t, KMAX>& tab, int
   const dim3 g(static_cast<unsigned>(grid)), b(64);
 #define DLA_BIGTILE(NPV)                                                                                      \
   hipLaunchKernelGGL((wsum_bigtile_kernel<DT, NPV, BT, KMAX>), g, b, 0, s, tab, n_chunks, n_elems, n_big, n_seg_wg, \
-                     out, in_stride)
+                     out)
   if constexpr (KMAX == 32) {  // 16 or 32 fp32 peers
     switch (n) {
       case 16: DLA_BIGTILE(16); break;
@@ -1928,8 +1892,8 @@ int dla_wsum_slab_tiled(int dtype, const void* base, int64_t tile_elems, int64_t
   while ((int64_t{1} << tshift) < tile_elems) ++tshift;
   const int variant = cfg && cfg->variant ? cfg->variant : vec_variant(n_peers < kMaxPeersPerPass ? n_peers
                                                                                                  : kMaxPeersPerPass);
-  if (variant != 9 && variant != 10 && variant != 12 && variant != 16)
-    return fail(DLA_E_CONFIG, "dla_wsum_slab_tiled: variant must be 0 (by shape), 9, 10, 12 or 16");
+  if (variant != 9 && variant != 10 && variant != 12)
+    return fail(DLA_E_CONFIG, "dla_wsum_slab_tiled: variant must be 0 (= 9), 9, 10 or 12");
   const int64_t stride = slab_rows * tile_elems;
   hipStream_t s = static_cast<hipStream_t>(stream);
   hipError_t e;

@@ -601,9 +601,9 @@ def _tiled_slab(peers, tile_elems, dtype):
 
 
 @pytest.mark.parametrize("dtype", ["f32", "bf16", "f16"])
-@pytest.mark.parametrize("n", [1, 8, 16, 33, 130])
-@pytest.mark.parametrize("numel", [5, 4097, 300_007, 4096 * 9 + 3])
-@pytest.mark.parametrize("tile_bytes", [16, 1024, 4096, 16384])
+@pytest.mark.parametrize("n", [1, 8, 33, 130])
+@pytest.mark.parametrize("numel", [5, 4097, 300_007])
+@pytest.mark.parametrize("tile_bytes", [16, 1024, 4096])
 def test_tiled_slab_bit_exact(dtype, n, numel, tile_bytes):
     """dla_wsum_slab_tiled (tile-interleaved PeerSlab layout): every kernel form, ragged tails
     (tiled addressing in the tail workgroup too), multi-pass peer counts, IEEE specials."""
@@ -618,7 +618,7 @@ def test_tiled_slab_bit_exact(dtype, n, numel, tile_bytes):
     want = c_wsum([_bits(p, dtype) for p in peers], w, dtype)
     te = tile_bytes // es
     slab = _tiled_slab(peers, te, dtype)
-    for v in (0, 9, 10, 12, 16):  # 16: the big-tile kernel over 16 KiB fp32 slab tiles (else the default)
+    for v in (0, 9, 10, 12):
         out = torch.empty(numel, dtype=TDT[dtype], device="cuda")
         _lib.wsum_slab_tiled_ptr(wsum.dtype_code(TDT[dtype]), slab.data_ptr(), te, n, w, numel, out.data_ptr(),
                                  torch.cuda.current_stream().cuda_stream, _lib.LaunchCfg(v, 0, 0, 0))
