@@ -755,18 +755,17 @@ __device__ inline void store_vec_sc1(u32x4* p, u32x4 v) {
   asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
 }
 
-template <int DT, int KMAX, int G, int VW, int U, bool FULL, bool ACC_IN>
+template <int DT, int KMAX, int G, int VW, bool FULL, bool ACC_IN>
 __device__ __attribute__((always_inline)) inline void vec_round(
-    const PeerTable<typename Ops<DT>::w_t, KMAX>& tab, int k0, int m, bool first_round, const int64_t (&a)[U],
-    typename Ops<DT>::acc_t (&acc)[U][VW][Ops<DT>::WE]) {
+    const PeerTable<typename Ops<DT>::w_t, KMAX>& tab, int k0, int m, bool first_round, int64_t a,
+    typename Ops<DT>::acc_t (&acc)[VW][Ops<DT>::WE]) {
   using V = typename VecOf<VW>::T;
-  V v[U][G];
+  V v[G];
 #pragma unroll
   for (int g = 0; g < G; ++g) {
     // partial round: slots past the last peer reload it (cached; branch-free issue)
     const int k = FULL || g < m ? k0 + g : k0 + m - 1;
-#pragma unroll
-    for (int u = 0; u < U; ++u) v[u][g] = __builtin_nontemporal_load(static_cast<const V*>(tab.p[k]) + a[u]);
+    v[g] = __builtin_nontemporal_load(static_cast<const V*>(tab.p[k]) + a);
   }
   typename Ops<DT>::w_t wk[G];
 #pragma unroll
@@ -775,18 +774,14 @@ __device__ __attribute__((always_inline)) inline void vec_round(
   for (int g = 0; g < G; ++g) {
     if (FULL || g < m) {
 #pragma unroll
-      for (int u = 0; u < U; ++u)
-#pragma unroll
-        for (int d = 0; d < VW; ++d) fold_dword<DT>(acc[u][d], wk[g], v[u][g][d], !ACC_IN && first_round && g == 0);
+      for (int d = 0; d < VW; ++d) fold_dword<DT>(acc[d], wk[g], v[g][d], !ACC_IN && first_round && g == 0);
     }
   }
 }
 
 // TILED: the peers are rows of a tile-interleaved slab (dla_wsum_slab_tiled): vector i of a peer at
 // p[k] + (i >> tshift_v) * tstride_v + (i & (2^tshift_v - 1)); the output stays contiguous.
-// U: vectors per lane — workgroup b covers vectors [b * 64 * U, (b + 1) * 64 * U), lane l the U
-// vectors b * 64 * U + u * 64 + l, all U * G loads of a round in flight before the fold.
-template <int DT, int KMAX, int G, int VW, bool ACC_IN, bool TILED = false, int U = 1>
+template <int DT, int KMAX, int G, int VW, bool ACC_IN, bool TILED = false>
 __global__ __launch_bounds__(64) void wsum_vec_kernel(
     const PeerTable<typename Ops<DT>::w_t, KMAX> tab, int n_peers, int64_t n_vecs,
     int64_t n_elems, void* __restrict__ out_v, int tshift_v = 0, int64_t tstride_v = 0, int tshift_e = -1,
@@ -796,48 +791,37 @@ __global__ __launch_bounds__(64) void wsum_vec_kernel(
   using acc_t = typename O::acc_t;
   using V = typename VecOf<VW>::T;
   constexpr int WE = O::WE;               // elements per dword
-  const int64_t main_grid = (n_vecs + 64 * U - 1) / (64 * U);
+  const int64_t main_grid = (n_vecs + 63) / 64;
   if (blockIdx.x >= main_grid) {  // the ragged-tail workgroup (< VW * WE elements)
     fold_tail<DT, ACC_IN>(tab.p, tab.w, n_peers, n_vecs * VW * WE, n_elems, out_v, TILED ? tshift_e : -1,
                           tstride_e);
     return;
   }
-  int64_t idx[U], a[U];
-  bool live[U];
-#pragma unroll
-  for (int u = 0; u < U; ++u) {
-    const int64_t j = (static_cast<int64_t>(blockIdx.x) * U + u) * 64 + threadIdx.x;
-    live[u] = j < n_vecs;
-    idx[u] = live[u] ? j : n_vecs - 1;  // clamped: loads stay unpredicated
-    a[u] = TILED ? (idx[u] >> tshift_v) * tstride_v + (idx[u] & ((int64_t{1} << tshift_v) - 1)) : idx[u];
-  }
+  const int64_t j = static_cast<int64_t>(blockIdx.x) * 64 + threadIdx.x;
+  const bool live = j < n_vecs;
+  const int64_t i = live ? j : n_vecs - 1;  // clamped: loads stay unpredicated
+  const int64_t a = TILED ? (i >> tshift_v) * tstride_v + (i & ((int64_t{1} << tshift_v) - 1)) : i;
   V* out = static_cast<V*>(out_v);
-  acc_t acc[U][VW][WE];
+  acc_t acc[VW][WE];
   if constexpr (ACC_IN) {
+    const V o = out[i];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const V o = out[idx[u]];
-#pragma unroll
-      for (int d = 0; d < VW; ++d) O::unpack_w(o[d], acc[u][d]);
-    }
+    for (int d = 0; d < VW; ++d) O::unpack_w(o[d], acc[d]);
   }
 #pragma unroll
   for (int r = 0; r < (KMAX + G - 1) / G; ++r) {
     const int k0 = r * G;
     if (k0 >= n_peers) break;
     if (k0 + G <= n_peers)  // full round: its own unpredicated path (as wsum_wide_kernel)
-      vec_round<DT, KMAX, G, VW, U, true, ACC_IN>(tab, k0, G, r == 0, a, acc);
+      vec_round<DT, KMAX, G, VW, true, ACC_IN>(tab, k0, G, r == 0, a, acc);
     else
-      vec_round<DT, KMAX, G, VW, U, false, ACC_IN>(tab, k0, n_peers - k0, r == 0, a, acc);
+      vec_round<DT, KMAX, G, VW, false, ACC_IN>(tab, k0, n_peers - k0, r == 0, a, acc);
   }
+  if (live) {
+    V o;
 #pragma unroll
-  for (int u = 0; u < U; ++u) {
-    if (live[u]) {
-      V o;
-#pragma unroll
-      for (int d = 0; d < VW; ++d) o[d] = O::pack_w(acc[u][d]);
-      store_vec_sc1(out + idx[u], o);
-    }
+    for (int d = 0; d < VW; ++d) o[d] = O::pack_w(acc[d]);
+    store_vec_sc1(out + i, o);
   }
 }
 
@@ -1174,7 +1158,7 @@ hipError_t launch_vec_tiled(const PeerTable<typename Ops<DT>::w_t, KMAX>& tab, i
     return hipErrorInvalidValue;
   } else {
     constexpr int WE = Ops<DT>::WE;
-#define DLA_VECT(G_, VW_, U_)                                                                                  \
+#define DLA_VECT(G_, VW_)                                                                                     \
   do {                                                                                                        \
     constexpr int G = KMAX < (G_) ? KMAX : (G_);                                                              \
     constexpr int per_vec = (VW_) * WE;                                                                       \
@@ -1182,19 +1166,17 @@ hipError_t launch_vec_tiled(const PeerTable<typename Ops<DT>::w_t, KMAX>& tab, i
     while ((1 << vs) < per_vec) ++vs;                                                                         \
     if (tshift_e < vs) return hipErrorInvalidValue;                                                           \
     const int64_t n_vecs = n_elems / per_vec;                                                                 \
-    int64_t grid = (n_vecs + 64 * (U_) - 1) / (64 * (U_));                                                    \
+    int64_t grid = (n_vecs + 63) / 64;                                                                        \
     if (n_elems > n_vecs * per_vec) ++grid;                                                                   \
     if (grid < 1 || grid > 0x7fffffff) return hipErrorInvalidValue;                                           \
-    hipLaunchKernelGGL((wsum_vec_kernel<DT, KMAX, G, VW_, ACC_IN, true, U_>), dim3(static_cast<unsigned>(grid)), \
+    hipLaunchKernelGGL((wsum_vec_kernel<DT, KMAX, G, VW_, ACC_IN, true>), dim3(static_cast<unsigned>(grid)),   \
                        dim3(64), 0, s, tab, n, n_vecs, n_elems, out, tshift_e - vs, tstride_e / per_vec, tshift_e, \
                        tstride_e);                                                                            \
   } while (0)
     switch (variant) {
-      case 12: DLA_VECT(16, 2, 1); break;
-      case 10: DLA_VECT(16, 4, 1); break;
-      case 13: DLA_VECT(16, 2, 2); break;
-      case 14: DLA_VECT(16, 2, 4); break;
-      default: DLA_VECT(32, 2, 1); break;
+      case 12: DLA_VECT(16, 2); break;
+      case 10: DLA_VECT(16, 4); break;
+      default: DLA_VECT(32, 2); break;
     }
 #undef DLA_VECT
     return hipGetLastError();
@@ -1910,8 +1892,8 @@ int dla_wsum_slab_tiled(int dtype, const void* base, int64_t tile_elems, int64_t
   while ((int64_t{1} << tshift) < tile_elems) ++tshift;
   const int variant = cfg && cfg->variant ? cfg->variant : vec_variant(n_peers < kMaxPeersPerPass ? n_peers
                                                                                                  : kMaxPeersPerPass);
-  if (variant != 9 && variant != 10 && variant != 12 && variant != 13 && variant != 14)
-    return fail(DLA_E_CONFIG, "dla_wsum_slab_tiled: variant must be 0 (by shape), 9, 10, 12, 13 or 14");
+  if (variant != 9 && variant != 10 && variant != 12)
+    return fail(DLA_E_CONFIG, "dla_wsum_slab_tiled: variant must be 0 (= 9), 9, 10 or 12");
   const int64_t stride = slab_rows * tile_elems;
   hipStream_t s = static_cast<hipStream_t>(stream);
   hipError_t e;
