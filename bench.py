@@ -17,25 +17,30 @@ torch.distributed.run before anything touches a GPU, and wait for them; every ra
 checks that the process group really has G ranks.
 
 Extra objects on the JSON line:
-  roofline      dominant kernel (the one dla_select_kernel names): achieved GB/s from HIP events on
-                the launch stream over the timed region vs 8 TB/s HBM peak; traffic =
-                PMC HBM bytes per launch from profiles/ (null if not collected)
-  cpu_baseline  the reference's torch-CPU op sequence (oracle/fedavg_oracle.py, kind
-                "port") on this host's cores, rank 0 at N=1 only, bounded sample
-  host_inclusive  FedAvg.aggregate on CPU modules (the reference call sites'
-                situation): pack + H2D + reduce + D2H, rank 0 at N=1 only
-  baseline_configs  every BASELINE config at its per-GPU share (prepared launch), with
-                the torch-CPU op sequence timed on the same share beside it
-  host_inclusive_sharded  (N > 1, rank 0) the CPU-module path bucket-sharded over GPUs
-                0..N-1 of one process (each bucket over its own PCIe link), strong scaling
-  collectives   (N > 1) the RCCL legs: all-gather reassembly, exact peer-sharded
-                all-to-all path, reduce-scatter tolerance path
+  roofline      dominant kernel (the headline launch's): achieved GB/s from HIP events on the
+                launch stream over the timed region vs 8 TB/s HBM peak; traffic = PMC HBM
+                bytes per launch from profiles/pmc_traffic.json (null if not collected)
+  separate_buffers  the same peers as one buffer per peer (what FedAvg.aggregate on device
+                modules reduces) — the row-major comparison to the PeerSlab layout
+  launch        backend, world size and who started the ranks (rank-count check)
   strong_scaling  ("scaling": "strong") FIXED models — the north-star 8 x 25 M fp32 model,
                 configs[3] / configs[3'] (64 peers) and configs[4] (128 peers, bf16) — each
                 split into N parameter buckets, one per rank: whole-model bytes / max-over-ranks
                 step time, inputs rotated so the working set exceeds the 256 MiB Infinity
                 Cache; the RCCL all-gather that reassembles the model is timed on its own
-  launch        backend, world size and who started the ranks (rank-count check)
+  collectives   (N > 1) the RCCL legs: all-gather reassembly, exact peer-sharded
+                all-to-all path, reduce-scatter tolerance path
+  host_inclusive_sharded  (N > 1, rank 0) the CPU-module path bucket-sharded over GPUs
+                0..N-1 of one process (each bucket over its own PCIe link)
+  baseline_configs  (N = 1) every BASELINE config at its per-GPU share, staged as PeerSlab
+                holds it (prepared launch)
+  host_inclusive, host_inclusive_small, wire_ingress, dfl_round  (N = 1) FedAvg.aggregate on
+                CPU modules (PCIe-inclusive), the GNLeNet small rounds, one peer's wire bytes
+                into HBM, one DFL round from EVA blocks to outgoing bytes
+  cpu_baseline  (N = 1, rank 0) the reference's torch-CPU op sequence (oracle/fedavg_oracle.py,
+                kind "port") on this host's CPU share, bounded sample; every other CPU
+                comparison (per config, GNLeNet rounds, the reference-style DFL round) is
+                timed in this leg too, the only one that runs the oracle port
 """
 from __future__ import annotations
 
@@ -519,33 +524,39 @@ def collectives(n, p, dt, es, world, device, slab, w, iters=10):
     return res
 
 
-def host_inclusive_small(reps=50):
-    """The reference's most frequent call: FedAvg.aggregate on small CPU models (GNLeNet,
-    configs[1]; GL merges N=2 every round, DFL N=8), end to end, next to the torch-CPU op
-    sequence on the same modules (per-call overhead, not bandwidth, decides here)."""
+GNLENET = [(32, 3, 5, 5), (32,), (32,), (32,), (32, 32, 5, 5), (32,), (32,), (32,), (64, 32, 5, 5), (64,),
+           (64,), (64,), (10, 576), (10,)]  # accdfl/core/models/cifar10.py GNLeNet parameters
+
+
+def _gnlenet_models(n):
     from torch import nn
 
-    sys.path.insert(0, ROOT)
-    from oracle.fedavg_oracle import fedavg_modules_torch  # timed CPU baseline
+    g = torch.Generator().manual_seed(n)
+    return [nn.ParameterList([nn.Parameter(torch.randn(s, generator=g) * 0.05) for s in GNLENET]) for _ in range(n)]
+
+
+def _median_ms(fn, reps):
+    fn()
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        fn()
+        ts.append(time.perf_counter() - t0)
+    return round(statistics.median(ts) * 1e3, 3)
+
+
+def host_inclusive_small(reps=50):
+    """The reference's most frequent call: FedAvg.aggregate on small CPU models (GNLeNet,
+    configs[1]; GL merges N=2 every round, DFL N=8), end to end (per-call overhead, not
+    bandwidth, decides here; the torch-CPU op sequence on the same modules is timed in the
+    cpu_baseline leg)."""
     from accdfl_amd.core.gradient_aggregation.fedavg import FedAvg
 
-    shapes = [(32, 3, 5, 5), (32,), (32,), (32,), (32, 32, 5, 5), (32,), (32,), (32,), (64, 32, 5, 5), (64,),
-              (64,), (64,), (10, 576), (10,)]
     out = {}
     for n in (2, 8):
-        g = torch.Generator().manual_seed(n)
-        models = [nn.ParameterList([nn.Parameter(torch.randn(s, generator=g) * 0.05) for s in shapes])
-                  for _ in range(n)]
+        models = _gnlenet_models(n)
         w = [float(1.0 / n)] * n
-        for name, fn in (("ours_ms", lambda: FedAvg.aggregate(models, w)),
-                         ("cpu_port_ms", lambda: fedavg_modules_torch(models, w))):
-            fn()
-            ts = []
-            for _ in range(reps):
-                t0 = time.perf_counter()
-                fn()
-                ts.append(time.perf_counter() - t0)
-            out.setdefault("gnlenet_n%d" % n, {})[name] = round(statistics.median(ts) * 1e3, 3)
+        out["gnlenet_n%d" % n] = {"ours_ms": _median_ms(lambda: FedAvg.aggregate(models, w), reps)}
     return out
 
 
@@ -744,11 +755,11 @@ def time_graph(launch, per_graph=20, reps=10):
     return ev0.elapsed_time(ev1) / 1e3 / (reps * per_graph)
 
 
-def baseline_configs(device, steps=40, cpu=True):
+def baseline_configs(device, steps=40):
     """Device-resident reduce rate of each BASELINE config's per-GPU share staged as PeerSlab
-    holds it (SlabInput, a prepared launch; bytes = (N + 1) * share * sizeof), beside the reference op sequence
-    on the host's cores for the same share (flat, one tensor per peer: a lower bound on
-    the reference's per-tensor loop, which pays T dispatches per peer)."""
+    holds it (SlabInput, a prepared launch; bytes = (N + 1) * share * sizeof).  The reference
+    op sequence on the same shares is timed in the cpu_baseline leg (cpu_per_config) and the
+    ratio filled in as gpu_over_cpu."""
     from accdfl_amd import _lib
 
     res = {}
@@ -770,12 +781,37 @@ def baseline_configs(device, steps=40, cpu=True):
                      "kernel": inp.kernel}
         del inp
         torch.cuda.empty_cache()
-        if cpu:
-            ms, threads = _cpu_port_ms(n, share, dt)
-            if ms is not None:
-                res[name].update({"cpu_port_ms": round(ms, 3), "cpu_port_GB/s": round(byts / (ms / 1e3) / 1e9, 2),
-                                  "cpu_threads": threads, "gpu_over_cpu": round(ms * 1e3 / (ev / steps * 1e6), 1)})
     return res
+
+
+def cpu_per_config():
+    """The reference op sequence (oracle port, torch-CPU) on every BASELINE config's per-GPU
+    share, on this host's CPU share (flat, one tensor per peer: a lower bound on the
+    reference's per-tensor loop, which pays T dispatches per peer)."""
+    res = {}
+    for name, (n, params, dts, gpus) in CONFIGS.items():
+        dt = torch.float32 if dts == "f32" else torch.bfloat16
+        es = 4 if dts == "f32" else 2
+        share = -(-params // gpus)
+        ms, threads = _cpu_port_ms(n, share, dt)
+        if ms is not None:
+            res[name] = {"cpu_port_ms": round(ms, 3), "cpu_port_GB/s": round((n + 1) * share * es / (ms / 1e3) / 1e9, 2),
+                         "cpu_threads": threads}
+    return res
+
+
+def cpu_gnlenet_small(reps=50):
+    """The torch-CPU op sequence (oracle port of fedavg.py:13-26) on the GNLeNet rounds of
+    host_inclusive_small."""
+    sys.path.insert(0, ROOT)
+    from oracle.fedavg_oracle import fedavg_modules_torch  # timed CPU baseline (kind "port")
+
+    out = {}
+    for n in (2, 8):
+        models = _gnlenet_models(n)
+        w = [float(1.0 / n)] * n
+        out["gnlenet_n%d" % n] = {"cpu_port_ms": _median_ms(lambda: fedavg_modules_torch(models, w), reps)}
+    return out
 
 
 # Fixed models for the strong-scaling lines: (peers, params of the whole model, dtype).
@@ -1068,7 +1104,7 @@ def main():
         print(json.dumps(host_breakdown(args.peers, args.params, device)))
         return
     if args.configs_only:
-        for name, row in baseline_configs(device, cpu=False).items():
+        for name, row in baseline_configs(device).items():
             print(json.dumps(dict(config=name, **row)))
         return
     dt = {"f32": torch.float32, "bf16": torch.bfloat16, "f16": torch.float16}[args.dtype]
@@ -1189,10 +1225,20 @@ def main():
             del msgs
         if not args.no_cpu_baseline and args.dtype == "f32":
             log("cpu baseline")
-            result["cpu_baseline"] = cpu_baseline(n, p, args.cpu_seconds)
+            cb = result["cpu_baseline"] = cpu_baseline(n, p, args.cpu_seconds)
+            # every CPU comparison lives in this leg (the only one that runs the oracle port)
+            if not args.no_small:
+                cb["per_config"] = cpu_per_config()
+                for name, row in cb["per_config"].items():
+                    g = result.get("baseline_configs", {}).get(name)
+                    if g:
+                        g["gpu_over_cpu"] = round(row["cpu_port_ms"] * 1e3 / g["us_per_reduce"], 1)
             if not args.no_host_inclusive:
+                cb["gnlenet_small"] = cpu_gnlenet_small()
+                for key, row in cb["gnlenet_small"].items():
+                    result.get("host_inclusive_small", {}).get(key, {})["cpu_port_ms"] = row["cpu_port_ms"]
                 msgs = dfl_messages(n, p)
-                result["cpu_baseline"]["dfl_round_reference_style"] = dfl_round_reference_style(msgs, p)
+                cb["dfl_round_reference_style"] = dfl_round_reference_style(msgs, p)
                 del msgs
     if rank == 0:
         print(json.dumps(result), flush=True)
