@@ -781,7 +781,9 @@ __device__ __attribute__((always_inline)) inline void vec_round(
 
 // TILED: the peers are rows of a tile-interleaved slab (dla_wsum_slab_tiled): vector i of a peer at
 // p[k] + (i >> tshift_v) * tstride_v + (i & (2^tshift_v - 1)); the output stays contiguous.
-template <int DT, int KMAX, int G, int VW, bool ACC_IN, bool TILED = false>
+// PLAIN_ST: plain (L2 write-back) output stores instead of sc1 — faster when the output is small
+// and many peers are read per element, slower for large outputs (vec_store_policy).
+template <int DT, int KMAX, int G, int VW, bool ACC_IN, bool TILED = false, bool PLAIN_ST = false>
 __global__ __launch_bounds__(64) void wsum_vec_kernel(
     const PeerTable<typename Ops<DT>::w_t, KMAX> tab, int n_peers, int64_t n_vecs,
     int64_t n_elems, void* __restrict__ out_v, int tshift_v = 0, int64_t tstride_v = 0, int tshift_e = -1,
@@ -821,7 +823,10 @@ __global__ __launch_bounds__(64) void wsum_vec_kernel(
     V o;
 #pragma unroll
     for (int d = 0; d < VW; ++d) o[d] = O::pack_w(acc[d]);
-    store_vec_sc1(out + i, o);
+    if constexpr (PLAIN_ST)
+      out[i] = o;
+    else
+      store_vec_sc1(out + i, o);
   }
 }
 
@@ -989,6 +994,17 @@ void shape_for(int64_t n_chunks, int n_peers, int elems_per_chunk, int* block, i
 // 33.4 vs 34.4, 64 x 1 233 086 f32 48.4 vs 48.4, 128 x 85 354 f32 10.9 vs 11.1.
 int vec_variant(int n_peers) { return n_peers >= 32 ? 9 : 12; }
 
+// Plain output stores (variant 21) for passes of >= 32 peers whose output is at most 8 MiB (it
+// then stays in the 8 x 4 MB of L2 until written back).  r02 interleaved A/B, sc1 -> plain, us
+// (profiles/r02r_sweep_store_policy.log): tiled slab 32 x 1.69 M f32 32.78 -> 31.87, 64 x 1.23 M
+// f32 47.53 -> 46.30, 128 x 2.66 M bf16 103.65 -> 102.51, 128 x 85 354 f32 8.88 -> 8.76;
+// separate buffers 128 x 2.66 M bf16 105.81 -> 103.70, 128 x 665 511 bf16 28.52 -> 28.08.
+// Larger outputs lose: 64 x 4.93 M f32 (19.7 MB) 192.8 -> 203.7, 128 x 21.3 M bf16 791.4 ->
+// 812.8, 8 x 25 M f32 130.4 -> 135.7; 16-peer passes (G = 16) lose at every size tried.
+int vec_store_policy(int variant, int64_t out_bytes) {
+  return variant == 9 && out_bytes <= (int64_t{8} << 20) ? 21 : variant;
+}
+
 constexpr int64_t kWideMaxChunks = 64 * 1024;
 bool use_wide(int64_t n_chunks, int n_peers, int elems_per_chunk) {
   if (n_peers <= kGroup) return false;
@@ -1128,21 +1144,22 @@ hipError_t launch_vec(const PeerTable<typename Ops<DT>::w_t, KMAX>& tab, int n, 
     return hipErrorInvalidValue;
   } else {
     constexpr int WE = Ops<DT>::WE;
-#define DLA_VEC(G_, VW_)                                                                                   \
+#define DLA_VEC(G_, VW_, PST_)                                                                                   \
   do {                                                                                                     \
     constexpr int G = KMAX < (G_) ? KMAX : (G_);                                                           \
     const int64_t n_vecs = n_elems / ((VW_) * WE);                                                         \
     int64_t grid = (n_vecs + 63) / 64;                                                                     \
     if (n_elems > n_vecs * (VW_) * WE) ++grid;                                                             \
     if (grid < 1 || grid > 0x7fffffff) return hipErrorInvalidValue;                                        \
-    hipLaunchKernelGGL((wsum_vec_kernel<DT, KMAX, G, VW_, ACC_IN>), dim3(static_cast<unsigned>(grid)), dim3(64), \
+    hipLaunchKernelGGL((wsum_vec_kernel<DT, KMAX, G, VW_, ACC_IN, false, PST_>), dim3(static_cast<unsigned>(grid)), dim3(64), \
                        0, s, tab, n, n_vecs, n_elems, out);                                                \
   } while (0)
     switch (variant) {
-      case 9: DLA_VEC(32, 2); break;
-      case 10: DLA_VEC(16, 4); break;
-      case 11: DLA_VEC(32, 4); break;
-      default: DLA_VEC(16, 2); break;  // 12
+      case 9: DLA_VEC(32, 2, false); break;
+      case 21: DLA_VEC(32, 2, true); break;
+      case 10: DLA_VEC(16, 4, false); break;
+      case 11: DLA_VEC(32, 4, false); break;
+      default: DLA_VEC(16, 2, false); break;  // 12
     }
 #undef DLA_VEC
     return hipGetLastError();
@@ -1150,7 +1167,8 @@ hipError_t launch_vec(const PeerTable<typename Ops<DT>::w_t, KMAX>& tab, int n, 
 }
 
 // The tile-interleaved slab (dla_wsum_slab_tiled) through the vector-per-lane kernel: variant 12 =
-// dwordx2 x 16 peers in flight, 10 = dwordx4 x 16, otherwise (default, 9) dwordx2 x 32.
+// dwordx2 x 16 peers in flight, 10 = dwordx4 x 16, 21 = dwordx2 x 32 with plain stores, otherwise
+// (default, 9) dwordx2 x 32.
 template <int DT, int KMAX, bool ACC_IN>
 hipError_t launch_vec_tiled(const PeerTable<typename Ops<DT>::w_t, KMAX>& tab, int n, int64_t n_elems, void* out,
                             hipStream_t s, int variant, int tshift_e, int64_t tstride_e) {
@@ -1158,7 +1176,7 @@ hipError_t launch_vec_tiled(const PeerTable<typename Ops<DT>::w_t, KMAX>& tab, i
     return hipErrorInvalidValue;
   } else {
     constexpr int WE = Ops<DT>::WE;
-#define DLA_VECT(G_, VW_)                                                                                     \
+#define DLA_VECT(G_, VW_, PST_)                                                                                     \
   do {                                                                                                        \
     constexpr int G = KMAX < (G_) ? KMAX : (G_);                                                              \
     constexpr int per_vec = (VW_) * WE;                                                                       \
@@ -1169,14 +1187,15 @@ hipError_t launch_vec_tiled(const PeerTable<typename Ops<DT>::w_t, KMAX>& tab, i
     int64_t grid = (n_vecs + 63) / 64;                                                                        \
     if (n_elems > n_vecs * per_vec) ++grid;                                                                   \
     if (grid < 1 || grid > 0x7fffffff) return hipErrorInvalidValue;                                           \
-    hipLaunchKernelGGL((wsum_vec_kernel<DT, KMAX, G, VW_, ACC_IN, true>), dim3(static_cast<unsigned>(grid)),   \
+    hipLaunchKernelGGL((wsum_vec_kernel<DT, KMAX, G, VW_, ACC_IN, true, PST_>), dim3(static_cast<unsigned>(grid)),   \
                        dim3(64), 0, s, tab, n, n_vecs, n_elems, out, tshift_e - vs, tstride_e / per_vec, tshift_e, \
                        tstride_e);                                                                            \
   } while (0)
     switch (variant) {
-      case 12: DLA_VECT(16, 2); break;
-      case 10: DLA_VECT(16, 4); break;
-      default: DLA_VECT(32, 2); break;
+      case 12: DLA_VECT(16, 2, false); break;
+      case 10: DLA_VECT(16, 4, false); break;
+      case 21: DLA_VECT(32, 2, true); break;
+      default: DLA_VECT(32, 2, false); break;
     }
 #undef DLA_VECT
     return hipGetLastError();
@@ -1267,14 +1286,16 @@ hipError_t launch_pass(const PeerTable<typename Ops<DT>::w_t, KMAX>& tab, int n,
                        dim3(kBlock), 0, s, tab, n, n_elems, out);
     return hipGetLastError();
   }
-  if (l.variant >= 9 && l.variant <= 12) {
+  if ((l.variant >= 9 && l.variant <= 12) || l.variant == 21) {
     if constexpr (DT != DLA_F64 && KMAX != 8) return launch_vec<DT, KMAX, ACC_IN>(tab, n, n_elems, out, s, l.variant);
   }
   if constexpr (DT != DLA_F64 && KMAX != 8) {
     // more than 8 peers: the vector-per-lane kernel, unless an fp32 big tile applies (below)
     const bool big = DT == DLA_F32 && !ACC_IN && (n == 16 || n == 32) &&
                      use_bigtile(n_elems / Ops<DT>::E, Ops<DT>::E, n) != 0;
-    if (l.auto_kernel && !big) return launch_vec<DT, KMAX, ACC_IN>(tab, n, n_elems, out, s, vec_variant(n));
+    if (l.auto_kernel && !big)
+      return launch_vec<DT, KMAX, ACC_IN>(tab, n, n_elems, out, s,
+                                          vec_store_policy(vec_variant(n), n_elems * int64_t{sizeof(typename Ops<DT>::elem_t)}));
   }
   if (l.variant == 8 || (l.auto_kernel && use_wide(n_elems / Ops<DT>::E, n, Ops<DT>::E)))
     return launch_wide<DT, KMAX, ACC_IN>(tab, n, n_elems, out, s);
@@ -1450,9 +1471,9 @@ int wsum_impl(int dtype, const void* const* peers, const double* weights, int n_
   }
   const Launch l = resolve(cfg);
   if (l.variant != 1 && l.variant != 2 && l.variant != 4 && !(l.variant >= 8 && l.variant <= 12) && l.variant != 16 &&
-      l.variant != 17)
+      l.variant != 17 && l.variant != 21)
     return fail(DLA_E_CONFIG,
-                "dla_wsum: unsupported variant " + std::to_string(l.variant) + " (1, 2, 4, 8-12, 16 or 17)");
+                "dla_wsum: unsupported variant " + std::to_string(l.variant) + " (1, 2, 4, 8-12, 16, 17 or 21)");
   if (l.chunks != 0 && l.chunks != 1 && l.chunks != 2 && l.chunks != 4)
     return fail(DLA_E_CONFIG, "dla_wsum: chunks must be 0 (auto), 1, 2 or 4");
   if (l.block != 0 && l.block != 64 && l.block != 256)
@@ -1890,10 +1911,12 @@ int dla_wsum_slab_tiled(int dtype, const void* base, int64_t tile_elems, int64_t
   if (!out) return fail(DLA_E_INVALID, "dla_wsum_slab_tiled: null out");
   int tshift = 0;
   while ((int64_t{1} << tshift) < tile_elems) ++tshift;
-  const int variant = cfg && cfg->variant ? cfg->variant : vec_variant(n_peers < kMaxPeersPerPass ? n_peers
-                                                                                                 : kMaxPeersPerPass);
-  if (variant != 9 && variant != 10 && variant != 12)
-    return fail(DLA_E_CONFIG, "dla_wsum_slab_tiled: variant must be 0 (= 9), 9, 10 or 12");
+  const int variant =
+      cfg && cfg->variant
+          ? cfg->variant
+          : vec_store_policy(vec_variant(n_peers < kMaxPeersPerPass ? n_peers : kMaxPeersPerPass), n_elems * es);
+  if (variant != 9 && variant != 10 && variant != 12 && variant != 21)
+    return fail(DLA_E_CONFIG, "dla_wsum_slab_tiled: variant must be 0 (auto), 9, 10, 12 or 21");
   const int64_t stride = slab_rows * tile_elems;
   hipStream_t s = static_cast<hipStream_t>(stream);
   hipError_t e;

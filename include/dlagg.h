@@ -59,7 +59,7 @@ extern "C" {
 /* Launch tuning knobs for dla_wsum_ex (0 = library default for each field). */
 typedef struct dla_launch_cfg {
   int variant;      /* 0 = by shape: passes of more than 8 fp32 / bf16 / f16 peers take 9
-                       (>= 32 peers) or 12; fp32 shares over 8, 16 or 32 peers beyond
+                       (>= 32 peers; 21 when the output is <= 8 MiB) or 12; fp32 shares over 8, 16 or 32 peers beyond
                        256 MiB whose big tiles fill >= 80 % of their last round of 1024
                        resident waves take 16 (17 from one full round up), fp64 over 4..8
                        likewise; fp64 small shares over more than 8 peers 8; otherwise 4.
@@ -71,7 +71,8 @@ typedef struct dla_launch_cfg {
                        9 = vector-per-lane kernel: 8 bytes per lane per load, 32 peers in
                            flight per lane (passes of more than 8 peers; fp64 and smaller
                            passes take 4); 10 = 16 bytes x 16 peers; 11 = 16 bytes x 32;
-                           12 = 8 bytes x 16
+                           12 = 8 bytes x 16; 21 = 9 with plain (L2 write-back)
+                           output stores instead of sc1
                       16 = peer-major big-tile kernel (fp32 <= 8, 16 or 32 peers, fp64 <= 8:
                            16 KiB of output per wave, one peer's 16 KiB streamed at a
                            time; chunks/block/grid are ignored; other dtypes take 4)
@@ -118,7 +119,8 @@ int dla_wsum_slab(int dtype, const void* base, int64_t pitch_elems, const double
  * of HBM instead of n_peers distant ones.  Peers 0..n_peers-1 (n_peers <= slab_rows) are
  * reduced in row order into the contiguous `out` (n_elems elements).  tile_elems: a power of
  * two of >= 16 bytes; base and out 16-byte aligned; F32, BF16 or F16.  cfg (may be NULL):
- * variant 9 (default), 10 or 12 picks the vector-per-lane kernel form.  ABI v5. */
+ * variant 0 (by shape, as dla_wsum), 9, 10, 12 or 21 picks the vector-per-lane kernel form.
+ * ABI v5. */
 int dla_wsum_slab_tiled(int dtype, const void* base, int64_t tile_elems, int64_t slab_rows, const double* weights,
                         int n_peers, int64_t n_elems, void* out, void* stream, const dla_launch_cfg_t* cfg);
 

@@ -125,7 +125,7 @@ def test_every_launch_variant_is_bit_exact(dtype):
 @pytest.mark.parametrize("numel", [1, 2, 63, 21_339, 100_007])
 def test_wide_kernel_bit_exact(dtype, n, numel):
     """Word-per-lane kernel (variant 8; auto-picked for small shares over > 8 peers), its
-    8- and 16-byte-per-lane forms (variants 9-12), and the 16-byte stream's lane-parallel ragged
+    8- and 16-byte-per-lane forms (variants 9-12; 21 = 9 with plain stores), and the 16-byte stream's lane-parallel ragged
     tail (up to 7 tail elements for 16-bit dtypes), every dtype, single and multi-pass peer counts."""
     from accdfl_amd import _lib
     from accdfl_amd.core import wsum
@@ -138,7 +138,7 @@ def test_wide_kernel_bit_exact(dtype, n, numel):
     want = c_wsum([_bits(p, dtype) for p in peers], w, dtype)
     dev = [p.cuda() for p in peers]
     cfgs = [_lib.LaunchCfg(8, 0, 0, 0), None, _lib.LaunchCfg(4, 1, 0, 64), _lib.LaunchCfg(4, 4, 0, 256)]
-    cfgs += [_lib.LaunchCfg(v, 0, 0, 0) for v in (9, 10, 11, 12)]  # vector-per-lane (dwordx2 / dwordx4)
+    cfgs += [_lib.LaunchCfg(v, 0, 0, 0) for v in (9, 10, 11, 12, 21)]  # vector-per-lane (dwordx2 / dwordx4)
     for cfg in cfgs:
         out = wsum.wsum(dev, w, cfg=cfg)
         torch.cuda.synchronize()
@@ -618,7 +618,7 @@ def test_tiled_slab_bit_exact(dtype, n, numel, tile_bytes):
     want = c_wsum([_bits(p, dtype) for p in peers], w, dtype)
     te = tile_bytes // es
     slab = _tiled_slab(peers, te, dtype)
-    for v in (0, 9, 10, 12):
+    for v in (0, 9, 10, 12, 21):
         out = torch.empty(numel, dtype=TDT[dtype], device="cuda")
         _lib.wsum_slab_tiled_ptr(wsum.dtype_code(TDT[dtype]), slab.data_ptr(), te, n, w, numel, out.data_ptr(),
                                  torch.cuda.current_stream().cuda_stream, _lib.LaunchCfg(v, 0, 0, 0))
