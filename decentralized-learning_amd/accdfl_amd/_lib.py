@@ -23,7 +23,7 @@ LIB_PATH = os.environ.get("DLAGG_LIB", os.path.join(PKG_ROOT, "lib", "libdlagg.s
 
 # dtype codes (include/dlagg.h)
 DLA_F32, DLA_BF16, DLA_F16, DLA_F64 = 0, 1, 2, 3
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 HIPCC_FLAGS = [
     "--offload-arch=gfx950",
@@ -56,6 +56,8 @@ EXPORTED = (
     "dla_shutdown",
     "dla_wsum_slab_tiled",
     "dla_slab_tile_elems",
+    "dla_host_round_start",
+    "dla_host_round_finish",
 )
 
 
@@ -178,6 +180,13 @@ class _Lib:
         so.dla_wsum_slab_tiled.restype = ctypes.c_int
         so.dla_slab_tile_elems.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int64]
         so.dla_slab_tile_elems.restype = ctypes.c_int64
+        so.dla_host_round_start.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(vp),
+                                            ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_double), vp,
+                                            ctypes.c_int64, vp, vp]
+        so.dla_host_round_start.restype = ctypes.c_int
+        so.dla_host_round_finish.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int64), vp,
+                                             ctypes.POINTER(vp), vp]
+        so.dla_host_round_finish.restype = ctypes.c_int
         so.dla_plan_destroy.argtypes = [vp]
         so.dla_plan_destroy.restype = None
         v = so.dla_version()
@@ -291,6 +300,31 @@ def host_copy_batch(dst_ptrs: Sequence[int], src_ptrs: Sequence[int], nbytes: Se
                                   (ctypes.c_int64 * m)(*nbytes), m)
     if rc != 0:
         L.check(rc, "dla_host_copy_batch")
+
+
+def host_round_start(dtype_code: int, n_peers: int, tensor_ptrs: Sequence[int], numels, weights: Sequence[float],
+                     rows_ptr: int, pitch_elems: int, result_ptr: int, stream_ptr: int) -> None:
+    """dla_host_round_start: pack the peers' host tensors (peer-major) into the page-locked rows
+    and enqueue the reduce into the page-locked result.  ``numels``: a sequence or a ctypes
+    int64 array (reused across rounds of one layout)."""
+    L = lib()
+    if not isinstance(numels, ctypes.Array):
+        numels = (ctypes.c_int64 * len(numels))(*numels)
+    rc = L.so.dla_host_round_start(dtype_code, n_peers, len(numels), (ctypes.c_void_p * len(tensor_ptrs))(*tensor_ptrs),
+                                   numels, _dbl_array(weights), rows_ptr, pitch_elems, result_ptr, stream_ptr)
+    if rc != 0:
+        L.check(rc, "dla_host_round_start")
+
+
+def host_round_finish(dtype_code: int, numels, result_ptr: int, out_ptrs: Sequence[int], stream_ptr: int) -> None:
+    """dla_host_round_finish: wait for the reduce, then unpack the result into out_ptrs."""
+    L = lib()
+    if not isinstance(numels, ctypes.Array):
+        numels = (ctypes.c_int64 * len(numels))(*numels)
+    rc = L.so.dla_host_round_finish(dtype_code, len(numels), numels, result_ptr,
+                                    (ctypes.c_void_p * len(out_ptrs))(*out_ptrs), stream_ptr)
+    if rc != 0:
+        L.check(rc, "dla_host_round_finish")
 
 
 def wsum_sharded_ptrs(dtype_code: int, dev_ids: Sequence[int], peer_ptrs: Sequence[int], weights: Sequence[float],

@@ -32,8 +32,11 @@ device-resident path is stream-ordered like any torch op.
 from __future__ import annotations
 
 import copy
+import copyreg
+import ctypes
 import os
 import threading
+from collections import OrderedDict
 from typing import Dict, List, Tuple
 
 import torch
@@ -119,6 +122,7 @@ def release_staging() -> None:
     with _staging_lock:
         _staging.clear()
         _staging_sharded.clear()
+        _host_rounds.clear()
 
 
 # Devices the host-staged path may shard over (one process, several GPUs): the reference
@@ -158,70 +162,77 @@ def _flat_slices(tensors: List[torch.Tensor], numels: List[int], start: int, end
     return out
 
 
-# Below this many input bytes a round is latency-bound: the small path below replaces the
-# per-row pipeline with one H2D, a prepared launch, one D2H and one host unpack
-# (GNLeNet, configs[1]: every call site's common case, e.g. the GL merge of N=2 models).
+# Small rounds are latency-bound: below these sizes a round goes through dla_host_round_*
+# (one native call packs every peer into page-locked rows and enqueues the reduce, which reads
+# them across PCIe; one call waits and unpacks) instead of the chunked H2D/D2H pipeline.  The
+# crossover is per peer row (profiles/r02s_small_round_crossover.log, us small / pipelined):
+# 2 x 1 MiB 140.6 / 269.5, 8 x 1 MiB 403.4 / 478.2, 8 x 2 MiB 619.4 / 639.2, but 2 x 4 MiB
+# 492.6 / 408.9, 2 x 6.8 MB 874.4 / 535.8, 8 x 4 MiB 1228.4 / 981.8.  GNLeNet (configs[1], the
+# GL merge of N=2 every round) is 341 KB per row.
+_SMALL_ROW_BYTES = 2 << 20
 _SMALL_ROUND_BYTES = 64 << 20
 
 
-def _start_host_small(device, dtype, peers: List[List[torch.Tensor]], weights, total: int, pitch: int):
-    """Enqueue pack -> one H2D -> prepared launch -> one D2H; returns (staging, stream).
-    The caller holds _staging_lock until _finish_host_small."""
-    n = len(peers)
-    # exact-fit staging per (device, dtype, pitch): the single DMA below moves n * pitch
-    # elements, so it must not inherit the pitch of an earlier large round
-    key = (device, dtype, ("small", pitch))
-    st = _staging.get(key)
-    if st is None:
-        st = _staging[key] = _HostStaging(device, dtype)
-    st.ensure(n, pitch)
-    compute = torch.cuda.current_stream(device)
-    # flatten every peer into its pinned row with one native batched memcpy (a torch.cat per
-    # peer costs ~30 us of dispatch and threading for a 341 KB GNLeNet row)
-    esize = st.h_in.element_size()
-    row_bytes = st.h_in.stride(0) * esize
-    base = st.h_in.data_ptr()
-    dsts, srcs, nbytes = [], [], []
-    for k in range(n):
-        off = base + k * row_bytes
-        for p in peers[k]:
-            b = p.numel() * esize
-            dsts.append(off)
-            srcs.append(p.data_ptr())
-            nbytes.append(b)
-            off += b
-    _lib.host_copy_batch(dsts, srcs, nbytes)
-    st.d_in[:n].copy_(st.h_in[:n], non_blocking=True)  # one DMA for every row
-    st.plan_for(n, total, weights).launch(int(compute.cuda_stream))
-    st.h_out[:total].copy_(st.d_out[:total], non_blocking=True)
-    return st, compute
+def _is_small(n: int, row_bytes: int) -> bool:
+    return 0 < row_bytes <= _SMALL_ROW_BYTES and n * row_bytes < _SMALL_ROUND_BYTES
 
 
-def _finish_host_small(st, compute, center: List[torch.Tensor], numels: List[int], total: int):
-    """Wait for the D2H, then scatter the averaged row into the (contiguous) result tensors."""
-    compute.synchronize()
-    esize = st.h_out.element_size()
-    src = st.h_out.data_ptr()
-    dsts, srcs, nbytes = [], [], []
-    for c, m in zip(center, numels):
-        dsts.append(c.data_ptr())
-        srcs.append(src)
-        nbytes.append(m * esize)
-        src += m * esize
-    _lib.host_copy_batch(dsts, srcs, nbytes)
+class _HostRound:
+    """Page-locked rows + result of the small-round path for one (device, dtype, pitch), and
+    the int64 numel table of the last layout (reused while the layout repeats)."""
+
+    def __init__(self, dtype: torch.dtype, pitch: int):
+        self.dtype = dtype
+        self.pitch = pitch
+        self.rows = 0
+        self.h_in = None
+        self.h_out = torch.empty(pitch, dtype=dtype, pin_memory=True)
+        self.numels_key = None
+        self.numels_arr = None
+
+    def ensure(self, n: int, numels: List[int]):
+        if n > self.rows:
+            self.h_in = torch.empty((n, self.pitch), dtype=self.dtype, pin_memory=True)
+            self.rows = n
+        key = tuple(numels)
+        if key != self.numels_key:
+            self.numels_arr = (ctypes.c_int64 * len(numels))(*numels)
+            self.numels_key = key
+
+
+_host_rounds: Dict[Tuple[torch.device, torch.dtype, int], _HostRound] = {}
+
+
+def _host_round(device: torch.device, dtype: torch.dtype, pitch: int, n: int, numels: List[int]) -> _HostRound:
+    """The page-locked buffers for a small round (caller holds _staging_lock)."""
+    key = (device, dtype, pitch)
+    hr = _host_rounds.get(key)
+    if hr is None:
+        hr = _host_rounds[key] = _HostRound(dtype, pitch)
+    hr.ensure(n, numels)
+    return hr
 
 
 def _reduce_host_small(device, dtype, center: List[torch.Tensor], peers: List[List[torch.Tensor]], weights,
                        numels: List[int], total: int, pitch: int):
+    """A small round through dla_host_round_* into the (contiguous) result tensors."""
+    code = _wsum.dtype_code(dtype)
     with _staging_lock:
-        st, compute = _start_host_small(device, dtype, peers, weights, total, pitch)
-        _finish_host_small(st, compute, center, numels, total)
+        hr = _host_round(device, dtype, pitch, len(peers), numels)
+        stream = torch.cuda.current_stream(device).cuda_stream
+        _lib.host_round_start(code, len(peers), [p.data_ptr() for pl in peers for p in pl], hr.numels_arr, weights,
+                              hr.h_in.data_ptr(), pitch, hr.h_out.data_ptr(), stream)
+        _lib.host_round_finish(code, hr.numels_arr, hr.h_out.data_ptr(), [c.data_ptr() for c in center], stream)
 
 
 def _small_round(models: List[nn.Module], weights) -> "nn.Module | None":
     """The whole aggregate for a small round of same-layout, one-dtype, contiguous CPU
-    models: the GPU work is enqueued first and the result module is built on the host
-    while it runs.  None when the round does not qualify (the general path handles it)."""
+    models (the reference's call sites: GL merges N=2 every round): one native call packs
+    every peer into page-locked rows and enqueues the reduce, which reads the rows and writes
+    the page-locked result across PCIe (no staging DMA, dla_host_round_start); the result
+    module is built on the host while it runs, then one call waits and unpacks into its
+    parameters (dla_host_round_finish).  None when the round does not qualify (the general
+    path handles it)."""
     peers = [list(m.parameters()) for m in models]
     p0 = peers[0]
     if not p0 or not torch.cuda.is_available():
@@ -229,30 +240,35 @@ def _small_round(models: List[nn.Module], weights) -> "nn.Module | None":
     dtype = p0[0].dtype
     if dtype not in _wsum.SUPPORTED_DTYPES:
         return None
-    layout = [(p.shape, p.dtype) for p in p0]
+    layout = [p.shape for p in p0]
+    ptrs = []
     for pl in peers:
-        if [(p.shape, p.dtype) for p in pl] != layout:
+        if len(pl) != len(layout):
             return None
-        for p in pl:
-            if p.device.type != "cpu" or not p.is_contiguous():
+        for p, shape in zip(pl, layout):
+            if p.shape != shape or p.dtype != dtype or p.device.type != "cpu" or not p.is_contiguous():
                 return None
-    if len({d for _, d in layout}) != 1:
-        return None
+            ptrs.append(p.data_ptr())
     numels = [p.numel() for p in p0]
     total = sum(numels)
     esize = p0[0].element_size()
-    if total == 0 or len(peers) * total * esize >= _SMALL_ROUND_BYTES:
+    n = len(peers)
+    if not _is_small(n, total * esize):
         return None
     device = _wsum.require_device(None)
+    pitch = _round_up(total, _ALIGN_BYTES // esize)
+    code = _wsum.dtype_code(dtype)
     with _staging_lock:
-        st, compute = _start_host_small(device, dtype, peers, weights, total,
-                                        _round_up(total, _ALIGN_BYTES // esize))
-        center = _center_copy(models[0], large=False)  # overlaps the H2D / reduce / D2H
+        hr = _host_round(device, dtype, pitch, n, numels)
+        stream = torch.cuda.current_stream(device).cuda_stream
+        _lib.host_round_start(code, n, ptrs, hr.numels_arr, weights, hr.h_in.data_ptr(), pitch, hr.h_out.data_ptr(),
+                              stream)
+        center = _center_copy(models[0], large=False)  # overlaps the reduce
         params = list(center.parameters())
         if len(params) != len(numels) or not all(c.is_contiguous() for c in params):
-            compute.synchronize()
+            torch.cuda.current_stream(device).synchronize()
             return None
-        _finish_host_small(st, compute, params, numels, total)
+        _lib.host_round_finish(code, hr.numels_arr, hr.h_out.data_ptr(), [c.data_ptr() for c in params], stream)
     return center
 
 
@@ -347,7 +363,7 @@ def _reduce_host_staged(devices: List[torch.device], dtype, center: List[torch.T
         return
     esize = torch.empty((), dtype=dtype).element_size()
     align = _ALIGN_BYTES // esize
-    if (len(peers) * total * esize < _SMALL_ROUND_BYTES and all(c.is_contiguous() for c in center)
+    if (_is_small(len(peers), total * esize) and all(c.is_contiguous() for c in center)
             and all(p.device.type == "cpu" and p.is_contiguous() for pl in peers for p in pl)):
         _reduce_host_small(devices[0], dtype, center, peers, weights, numels, total, _round_up(total, align))
         return
@@ -486,6 +502,53 @@ def reduce_parameters(center_params: List[torch.Tensor], peer_params: List[List[
         _reduce_param(device, center_params[i], [peer_params[k][i] for k in ks], [weights[k] for k in ks])
 
 
+# copy.deepcopy's own protocol for an nn.Module (copy._reconstruct): y = cls.__new__(cls),
+# state = deepcopy(x.__getstate__()), y.__setstate__(state).  _clone_value restates it for module
+# classes that keep torch's __getstate__ and have no other copy hook, and for the plain dicts,
+# OrderedDicts and empty sets a module's __dict__ holds; everything else (tensors, buffers,
+# lists, user objects, classes with their own protocol) goes through copy.deepcopy with the same
+# memo, so identity (tied weights, shared submodules) is preserved exactly as deepcopy does.
+_ATOMIC = frozenset({type(None), bool, int, float, complex, str, bytes, torch.dtype, torch.device})
+_plain_module_cls: Dict[type, bool] = {}
+
+
+def _plain_module(cls: type) -> bool:
+    ok = _plain_module_cls.get(cls)
+    if ok is None:
+        ok = (issubclass(cls, nn.Module) and cls.__getstate__ is nn.Module.__getstate__
+              and cls.__reduce_ex__ is object.__reduce_ex__ and cls.__reduce__ is object.__reduce__
+              and getattr(cls, "__deepcopy__", None) is None and cls not in copyreg.dispatch_table
+              and not any("__slots__" in c.__dict__ for c in cls.__mro__))
+        _plain_module_cls[cls] = ok
+    return ok
+
+
+def _clone_value(v, memo: dict):
+    t = type(v)
+    if t in _ATOMIC:
+        return v
+    y = memo.get(id(v), memo)
+    if y is not memo:
+        return y
+    if t is dict or t is OrderedDict:
+        y = t()
+        memo[id(v)] = y
+        for k, x in v.items():
+            y[k if type(k) in _ATOMIC else copy.deepcopy(k, memo)] = _clone_value(x, memo)
+        return y
+    if t is set and not v:
+        y = set()
+        memo[id(v)] = y
+        return y
+    if _plain_module(t):
+        y = t.__new__(t)
+        memo[id(v)] = y
+        state = {k: _clone_value(x, memo) for k, x in v.__dict__.items() if k != "_compiled_call_impl"}
+        y.__setstate__(state)
+        return y
+    return copy.deepcopy(v, memo)
+
+
 def _center_copy(model0: nn.Module, large: bool = True) -> nn.Module:
     """``copy.deepcopy(models[0])`` (fedavg.py:20) whose parameters are fresh,
     uninitialised tensors of the same shape, strides, dtype, device and
@@ -493,7 +556,9 @@ def _center_copy(model0: nn.Module, large: bool = True) -> nn.Module:
     values first (and page-faulting P fresh elements: 16 ms of a 35 ms host-inclusive
     8 x 25 M reduce) is wasted.  For a ``large`` round the contiguous CPU parameters come
     from core/host_memory.result_tensor (pre-faulted pooled pageable memory by default).
-    Buffers and every other attribute are deep-copied exactly as in the reference."""
+    Buffers and every other attribute are deep-copied exactly as in the reference (the module
+    tree through _clone_value, deepcopy's protocol without its per-object dispatch: the GL
+    merge of two GNLeNet models builds this copy every round)."""
     memo = {}
     for p in model0.parameters():
         if id(p) in memo or type(p) is not nn.Parameter:
@@ -506,7 +571,7 @@ def _center_copy(model0: nn.Module, large: bool = True) -> nn.Module:
         else:
             data = torch.empty_strided(p.size(), p.stride(), dtype=p.dtype, device=p.device)
         memo[id(p)] = nn.Parameter(data, p.requires_grad)
-    return copy.deepcopy(model0, memo)
+    return _clone_value(model0, memo)
 
 
 class FedAvg(GradientAggregation):

@@ -1667,6 +1667,35 @@ int copy_threads(int64_t total) {
   return static_cast<int>(by_size < 1 ? 1 : by_size < cap ? by_size : cap);
 }
 
+// dsts[i] <- srcs[i], bytes[i] each (validated by the caller); threaded above 8 MiB.
+void copy_batch(void* const* dsts, const void* const* srcs, const int64_t* bytes, int n) {
+  int64_t total = 0;
+  for (int i = 0; i < n; ++i) total += bytes[i];
+  const int threads = copy_threads(total);
+  if (threads <= 1) {
+    for (int i = 0; i < n; ++i)
+      if (bytes[i] > 0) std::memcpy(dsts[i], srcs[i], static_cast<size_t>(bytes[i]));
+    return;
+  }
+  // Large batches (an EVA block list gathered into a page-locked ingress buffer: ~1 700
+  // blocks per 100 MB model) split into equal byte ranges, one per thread; a range may start
+  // or end inside a segment.
+  auto copy_range = [&](int64_t lo, int64_t hi) {
+    int64_t off = 0;
+    for (int i = 0; i < n && off < hi; off += bytes[i], ++i) {
+      const int64_t s0 = lo > off ? lo : off, e0 = hi < off + bytes[i] ? hi : off + bytes[i];
+      if (s0 < e0)
+        std::memcpy(static_cast<char*>(dsts[i]) + (s0 - off), static_cast<const char*>(srcs[i]) + (s0 - off),
+                    static_cast<size_t>(e0 - s0));
+    }
+  };
+  std::vector<std::thread> pool;
+  const int64_t per = (total + threads - 1) / threads;
+  for (int t = 1; t < threads; ++t) pool.emplace_back(copy_range, per * t, per * (t + 1) < total ? per * (t + 1) : total);
+  copy_range(0, per < total ? per : total);
+  for (auto& th : pool) th.join();
+}
+
 }  // namespace
 
 struct dla_plan {
@@ -1835,31 +1864,84 @@ int dla_host_copy_batch(void* const* dsts, const void* const* srcs, const int64_
     if (bytes[i] > 0 && (!dsts[i] || !srcs[i]))
       return fail(DLA_E_INVALID, "dla_host_copy_batch: null pointer at " + std::to_string(i));
   }
+  copy_batch(dsts, srcs, bytes, n);
+  return DLA_OK;
+}
+
+int dla_host_round_start(int dtype, int n_peers, int n_tensors, const void* const* tensors, const int64_t* numels,
+                         const double* weights, void* rows, int64_t pitch_elems, void* result, void* stream) {
+  g_last_error.clear();
+  const int es = elem_size(dtype);
+  if (es == 0) return fail(DLA_E_INVALID, "dla_host_round_start: unknown dtype");
+  if (n_peers < 1 || n_tensors < 1 || !tensors || !numels || !weights || !rows || !result)
+    return fail(DLA_E_INVALID, "dla_host_round_start: need n_peers >= 1, n_tensors >= 1 and every table");
   int64_t total = 0;
-  for (int i = 0; i < n; ++i) total += bytes[i];
-  const int threads = copy_threads(total);
-  if (threads <= 1) {
-    for (int i = 0; i < n; ++i)
-      if (bytes[i] > 0) std::memcpy(dsts[i], srcs[i], static_cast<size_t>(bytes[i]));
-    return DLA_OK;
+  for (int t = 0; t < n_tensors; ++t) {
+    if (numels[t] < 0) return fail(DLA_E_INVALID, "dla_host_round_start: negative numel at " + std::to_string(t));
+    total += numels[t];
   }
-  // Large batches (an EVA block list gathered into a page-locked ingress buffer: ~1 700
-  // blocks per 100 MB model) split into equal byte ranges, one per thread; a range may start
-  // or end inside a segment.
-  auto copy_range = [&](int64_t lo, int64_t hi) {
-    int64_t off = 0;
-    for (int i = 0; i < n && off < hi; off += bytes[i], ++i) {
-      const int64_t s0 = lo > off ? lo : off, e0 = hi < off + bytes[i] ? hi : off + bytes[i];
-      if (s0 < e0)
-        std::memcpy(static_cast<char*>(dsts[i]) + (s0 - off), static_cast<const char*>(srcs[i]) + (s0 - off),
-                    static_cast<size_t>(e0 - s0));
+  if (pitch_elems < total || (pitch_elems * es) % 16)
+    return fail(DLA_E_INVALID, "dla_host_round_start: pitch_elems must be >= sum(numels) and a multiple of 16 bytes");
+  if ((reinterpret_cast<uintptr_t>(rows) & 15u) || (reinterpret_cast<uintptr_t>(result) & 15u))
+    return fail(DLA_E_INVALID, "dla_host_round_start: rows and result must be 16-byte aligned");
+  // The kernel reads `rows` and writes `result` across PCIe: both must be page-locked host memory
+  // mapped into the device address space at the same address (hipHostMalloc / torch pin_memory).
+  for (const void* p : {static_cast<const void*>(rows), static_cast<const void*>(result)}) {
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess || a.type != hipMemoryTypeHost || a.devicePointer != p) {
+      (void)hipGetLastError();
+      return fail(DLA_E_INVALID, "dla_host_round_start: rows / result must be page-locked host memory "
+                                 "mapped for the device (hipHostMalloc)");
     }
-  };
-  std::vector<std::thread> pool;
-  const int64_t per = (total + threads - 1) / threads;
-  for (int t = 1; t < threads; ++t) pool.emplace_back(copy_range, per * t, per * (t + 1) < total ? per * (t + 1) : total);
-  copy_range(0, per < total ? per : total);
-  for (auto& th : pool) th.join();
+  }
+  for (int i = 0; i < n_peers * n_tensors; ++i)
+    if (!tensors[i] && numels[i % n_tensors] > 0)
+      return fail(DLA_E_INVALID, "dla_host_round_start: null tensor pointer at " + std::to_string(i));
+  if (total == 0) return DLA_OK;
+  // pack: tensor t of peer k -> row k at the tensor's flat offset (the zip order of fedavg.py:24)
+  std::vector<void*> dsts(static_cast<size_t>(n_peers) * n_tensors);
+  std::vector<const void*> srcs(dsts.size());
+  std::vector<int64_t> bytes(dsts.size());
+  std::vector<const void*> row_ptrs(n_peers);
+  for (int k = 0; k < n_peers; ++k) {
+    char* row = static_cast<char*>(rows) + static_cast<int64_t>(k) * pitch_elems * es;
+    row_ptrs[k] = row;
+    int64_t off = 0;
+    for (int t = 0; t < n_tensors; ++t) {
+      const size_t i = static_cast<size_t>(k) * n_tensors + t;
+      dsts[i] = row + off;
+      srcs[i] = tensors[i];
+      bytes[i] = numels[t] * es;
+      off += bytes[i];
+    }
+  }
+  copy_batch(dsts.data(), srcs.data(), bytes.data(), static_cast<int>(dsts.size()));
+  const int rc = wsum_impl(dtype, row_ptrs.data(), weights, n_peers, total, result, stream, nullptr);
+  return rc;
+}
+
+int dla_host_round_finish(int dtype, int n_tensors, const int64_t* numels, const void* result, void* const* outs,
+                          void* stream) {
+  g_last_error.clear();
+  const int es = elem_size(dtype);
+  if (es == 0) return fail(DLA_E_INVALID, "dla_host_round_finish: unknown dtype");
+  if (n_tensors < 1 || !numels || !result || !outs)
+    return fail(DLA_E_INVALID, "dla_host_round_finish: need n_tensors >= 1 and every table");
+  for (int t = 0; t < n_tensors; ++t)
+    if (numels[t] < 0 || (numels[t] > 0 && !outs[t]))
+      return fail(DLA_E_INVALID, "dla_host_round_finish: bad tensor " + std::to_string(t));
+  const hipError_t e = hipStreamSynchronize(static_cast<hipStream_t>(stream));
+  if (e != hipSuccess) return fail(static_cast<int>(e), std::string("dla_host_round_finish: ") + hipGetErrorString(e));
+  // unpack: the averaged row -> the result's tensors (fedavg.py:25 lands in the deepcopy's params)
+  std::vector<const void*> srcs(n_tensors);
+  std::vector<int64_t> bytes(n_tensors);
+  int64_t off = 0;
+  for (int t = 0; t < n_tensors; ++t) {
+    srcs[t] = static_cast<const char*>(result) + off;
+    bytes[t] = numels[t] * es;
+    off += bytes[t];
+  }
+  copy_batch(outs, srcs.data(), bytes.data(), n_tensors);
   return DLA_OK;
 }
 

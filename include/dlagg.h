@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define DLA_ABI_VERSION 5
+#define DLA_ABI_VERSION 6
 
 /* element dtypes of the peer buffers and of the output */
 #define DLA_F32 0
@@ -204,6 +204,25 @@ void dla_plan_destroy(dla_plan_t* plan);
  * tensors).  One native call instead of a torch op per tensor: the GL merge of two
  * GNLeNet models (configs[1]) packs 28 tensors per round.  Regions must not overlap. */
 int dla_host_copy_batch(void* const* dsts, const void* const* srcs, const int64_t* bytes, int n);
+
+/* A round of CPU-resident models in two calls — fedavg.py:20-25 for the reference's own call
+ * sites, whose models live in host memory (the GL merge of N=2 models every round,
+ * accdfl/gl/community.py:117; DL/DFL rounds of small models, accdfl/dl/community.py:170,
+ * accdfl/dfl/community.py:673) — so the caller builds the result module (the deepcopy of
+ * fedavg.py:20) while the GPU works.  ABI v6.
+ *   dla_host_round_start: packs tensor t of peer k (HOST pointer tensors[k * n_tensors + t],
+ *     numels[t] elements of dtype, the zip order of fedavg.py:24) into row k of `rows`
+ *     (pitch_elems per row, a multiple of 16 bytes), then enqueues the reduce of rows
+ *     0..n_peers-1 on `stream`.  The kernel reads the rows and writes `result`
+ *     (sum(numels) elements) across PCIe, with no staging DMA: `rows` and `result` must be
+ *     page-locked host memory mapped into the device at the same address (hipHostMalloc,
+ *     torch pin_memory; checked), 16-byte aligned, and untouched until finish returns.
+ *   dla_host_round_finish: waits for `stream`, then copies the averaged values into outs[t]
+ *     (HOST pointers, numels[t] elements each). */
+int dla_host_round_start(int dtype, int n_peers, int n_tensors, const void* const* tensors, const int64_t* numels,
+                         const double* weights, void* rows, int64_t pitch_elems, void* result, void* stream);
+int dla_host_round_finish(int dtype, int n_tensors, const int64_t* numels, const void* result, void* const* outs,
+                          void* stream);
 
 #ifdef __cplusplus
 }

@@ -59,7 +59,7 @@ def test_library_version_and_argument_errors(lib_path):
     from accdfl_amd import _lib
 
     L = _lib.lib()
-    assert L.so.dla_version() == 5
+    assert L.so.dla_version() == 6
     assert L.build_id == _lib.source_build_id() == _lib.file_build_id(lib_path)
     assert L.max_peers_per_pass == 128
     # kernel selection by shape (host-only query): north star, configs[3] share, configs[4] share,
@@ -132,6 +132,95 @@ def test_host_copy_batch_runs_on_cpu(lib_path):
         _lib.host_copy_batch([0], [srcs[0].ctypes.data], [12])
     with pytest.raises(_lib.DlaggError, match="negative"):
         _lib.host_copy_batch([row.ctypes.data], [srcs[0].ctypes.data], [-1])
+
+
+def test_host_round_argument_errors(lib_path):
+    """dla_host_round_start / _finish refuse bad tables, pitches and pageable rows before any
+    GPU work (the kernel would read them across PCIe)."""
+    import numpy as np
+
+    from accdfl_amd import _lib
+
+    rows = np.zeros((2, 64), dtype=np.float32)
+    res = np.zeros(64, dtype=np.float32)
+    a = np.ones(10, dtype=np.float32)
+    ptrs = [a.ctypes.data, a.ctypes.data]
+    with pytest.raises(_lib.DlaggError, match="pitch"):
+        _lib.host_round_start(0, 2, ptrs, [10], [0.5, 0.5], rows.ctypes.data, 8, res.ctypes.data, 0)
+    with pytest.raises(_lib.DlaggError, match="page-locked"):
+        _lib.host_round_start(0, 2, ptrs, [10], [0.5, 0.5], rows.ctypes.data, 64, res.ctypes.data, 0)
+    with pytest.raises(_lib.DlaggError, match="dtype"):
+        _lib.host_round_start(9, 2, ptrs, [10], [0.5, 0.5], rows.ctypes.data, 64, res.ctypes.data, 0)
+    with pytest.raises(_lib.DlaggError, match="aligned"):
+        _lib.host_round_start(0, 2, ptrs, [10], [0.5, 0.5], rows.ctypes.data + 4, 64, res.ctypes.data, 0)
+    with pytest.raises(_lib.DlaggError, match="bad tensor"):
+        _lib.host_round_finish(0, [10], res.ctypes.data, [0], 0)
+
+
+class _OddModule(nn.Module):
+    """Tied weights, nested containers, an LSTM (its own __setstate__ / __getstate__), buffers
+    (one non-persistent), a forward hook, plain attributes sharing a dict."""
+
+    def __init__(self):
+        super().__init__()
+        self.enc = nn.Linear(4, 3)
+        self.tied = self.enc
+        self.seq = nn.Sequential(nn.Conv2d(3, 4, 3), nn.BatchNorm2d(4), nn.ReLU(), nn.GroupNorm(2, 4))
+        self.rnn = nn.LSTM(4, 5)
+        self.pl = nn.ParameterList([nn.Parameter(torch.randn(3)), nn.Parameter(torch.randn(2), requires_grad=False)])
+        self.cfg = {"a": [1, 2], "b": (3, 4)}
+        self.lst = [self.cfg, torch.ones(2)]
+        self.name = "x"
+        self.register_buffer("steps", torch.tensor(5))
+        self.register_buffer("np", torch.zeros(2), persistent=False)
+        self.fh = self.register_forward_hook(lambda m, i, o: None)
+
+
+def _same_structure(x, y, seen):
+    if id(x) in seen:
+        return
+    seen.add(id(x))
+    assert type(x) is type(y)
+    if isinstance(x, torch.Tensor):
+        assert x.shape == y.shape and x.dtype == y.dtype and x.requires_grad == y.requires_grad
+        assert x is not y
+        if not isinstance(x, nn.Parameter):
+            assert torch.equal(x, y)
+    elif isinstance(x, nn.Module):
+        assert list(x.__dict__) == list(y.__dict__) and x is not y
+        for k in x.__dict__:
+            _same_structure(x.__dict__[k], y.__dict__[k], seen)
+    elif isinstance(x, dict):
+        assert list(x) == list(y)
+        for k in x:
+            _same_structure(x[k], y[k], seen)
+    elif isinstance(x, (list, tuple)):
+        assert len(x) == len(y)
+        for u, v in zip(x, y):
+            _same_structure(u, v, seen)
+    elif isinstance(x, (set, int, float, str, bool, type(None))):
+        assert x == y
+
+
+def test_center_copy_is_a_deepcopy():
+    """The result module (fedavg.py:20 copy.deepcopy(models[0])) built by _center_copy's module
+    clone matches copy.deepcopy attribute for attribute: same types and key order, fresh
+    objects, buffers equal, identity preserved (tied weights, a dict shared by two attributes),
+    parameters fresh with the same requires_grad, and the copy runs."""
+    import copy
+
+    from accdfl_amd.core.gradient_aggregation.fedavg import _center_copy
+
+    m = _OddModule()
+    want = copy.deepcopy(m)
+    got = _center_copy(m, large=False)
+    _same_structure(want, got, set())
+    assert got.tied is got.enc and got.lst[0] is got.cfg and got.cfg is not m.cfg
+    assert len(got._forward_hooks) == 1 and got._forward_hooks is not m._forward_hooks
+    assert [p.requires_grad for p in got.parameters()] == [p.requires_grad for p in m.parameters()]
+    assert all(p is not q for p, q in zip(got.parameters(), m.parameters()))
+    got.seq(torch.zeros(1, 3, 5, 5))
+    got.rnn(torch.zeros(2, 1, 4))
 
 
 def _tiny_models(n):

@@ -673,3 +673,45 @@ def test_result_memory_modes(mode):
         assert out.a.is_pinned() == (mode == "pinned")
     finally:
         host_memory.set_result_memory(prev)
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16", "f16", "f64"])
+@pytest.mark.parametrize("n", [1, 2, 8, 130])
+def test_host_round_bit_exact(dtype, n):
+    """dla_host_round_start / _finish (the small-round path for CPU-resident models: the kernel
+    reads page-locked rows and writes the page-locked result across PCIe): ragged tensor sizes
+    (one empty), multi-pass peer counts, IEEE specials, two rounds through the same buffers."""
+    from accdfl_amd import _lib
+    from accdfl_amd.core import wsum
+
+    sizes = [5, 0, 4097, 3, 1000]
+    code = wsum.dtype_code(TDT[dtype])
+    es = TDT[dtype].itemsize
+    total = sum(sizes)
+    pitch = -(-total // (256 // es)) * (256 // es)
+    rows = torch.empty((n, pitch), dtype=TDT[dtype], pin_memory=True)
+    result = torch.empty(pitch, dtype=TDT[dtype], pin_memory=True)
+    stream = torch.cuda.current_stream().cuda_stream
+    for rnd in range(2):
+        flat = _random_peers(n, total, dtype, seed=n * 5 + rnd)
+        for i, v in enumerate([-0.0, float("inf"), float("-inf"), float("nan"), 1e-40, -3e38]):
+            flat[(3 * i) % n][(11 * i + rnd) % total] = v
+        peers = [list(torch.split(f, sizes)) for f in flat]
+        w = [float(x) for x in np.random.default_rng(n + rnd).dirichlet(np.ones(n))]
+        outs = [torch.full((s,), 7, dtype=TDT[dtype]) for s in sizes]
+        _lib.host_round_start(code, n, [t.data_ptr() for pl in peers for t in pl], sizes, w, rows.data_ptr(), pitch,
+                              result.data_ptr(), stream)
+        _lib.host_round_finish(code, sizes, result.data_ptr(), [o.data_ptr() for o in outs], stream)
+        want = c_wsum([_bits(f, dtype) for f in flat], w, dtype)
+        assert same_bits(_bits(torch.cat(outs), dtype), want, dtype), (dtype, n, rnd)
+
+
+def test_host_round_refuses_device_memory():
+    """rows / result must be page-locked host memory: device buffers are refused."""
+    from accdfl_amd import _lib
+
+    rows = torch.empty((2, 64), device="cuda")
+    res = torch.empty(64, pin_memory=True)
+    a = torch.ones(10)
+    with pytest.raises(_lib.DlaggError, match="page-locked"):
+        _lib.host_round_start(0, 2, [a.data_ptr()] * 2, [10], [0.5, 0.5], rows.data_ptr(), 64, res.data_ptr(), 0)
