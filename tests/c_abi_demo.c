@@ -4,7 +4,8 @@
  *   gcc -std=c11 -O2 -ffp-contract=off tests/c_abi_demo.c -Iinclude -I/opt/rocm/include \
  *       -D__HIP_PLATFORM_AMD__ -Ldecentralized-learning_amd/lib -ldlagg -L/opt/rocm/lib -lamdhip64 -o c_abi_demo
  * Runs FedAvg (dla_wsum, a dla_plan with changed weights, the bucket-sharded dla_wsum_sharded and
- * the tile-interleaved dla_wsum_slab_tiled) and the teacher-logit mean (dla_mean) on N peers and checks every element bit-for-bit against the reference's
+ * the tile-interleaved dla_wsum_slab_tiled, host-resident peers through dla_host_round_*) and the
+ * teacher-logit mean (dla_mean) on N peers and checks every element bit-for-bit against the reference's
  * sequential arithmetic written out in C (fedavg.py:21-25).  Exit status 0 = all equal.
  */
 #include <hip/hip_runtime_api.h>
@@ -163,7 +164,44 @@ int main(void) {
     free(tiled);
   }
 
-  /* 6. errors come back as codes with a message */
+  /* 6. peers in host memory (dla_host_round_start / _finish): each peer as two tensors, packed
+   *    into page-locked rows the kernel reads across PCIe, unpacked into two host outputs */
+  {
+    const int64_t split = 4099, numels[2] = {split, P - split};
+    const int64_t pitch = (P + 63) / 64 * 64;
+    const void* tensors[2 * N];
+    void *rows, *result;
+    float* outs_host[2] = {out_host, out_host + split};
+    for (int k = 0; k < N; ++k) {
+      tensors[2 * k] = host[k];
+      tensors[2 * k + 1] = host[k] + split;
+    }
+    CHECK_HIP(hipHostMalloc(&rows, sizeof(float) * (size_t)(N * pitch), hipHostMallocDefault));
+    CHECK_HIP(hipHostMalloc(&result, sizeof(float) * (size_t)pitch, hipHostMallocDefault));
+    memset(out_host, 0xff, sizeof(float) * P);
+    CHECK_DLA(dla_host_round_start(DLA_F32, N, 2, tensors, numels, w, rows, pitch, result, NULL));
+    CHECK_DLA(dla_host_round_finish(DLA_F32, 2, numels, result, (void* const*)outs_host, NULL));
+    for (int64_t j = 0; j < P; ++j) {
+      volatile float acc = host[0][j] * 0.0f;
+      for (int k = 0; k < N; ++k) {
+        volatile float prod = (float)w[k] * host[k][j];
+        acc = acc + prod;
+      }
+      if (!same_f32(acc, out_host[j])) {
+        fprintf(stderr, "dla_host_round mismatch at %lld\n", (long long)j);
+        return 1;
+      }
+    }
+    /* pageable rows are refused before any launch */
+    if (dla_host_round_start(DLA_F32, N, 2, tensors, numels, w, out_host, pitch, result, NULL) != DLA_E_INVALID) {
+      fprintf(stderr, "expected DLA_E_INVALID for pageable rows\n");
+      return 1;
+    }
+    CHECK_HIP(hipHostFree(rows));
+    CHECK_HIP(hipHostFree(result));
+  }
+
+  /* 7. errors come back as codes with a message */
   if (dla_wsum(DLA_F32, (const void* const*)dev, w, 0, P, dev_out, NULL) != DLA_E_INVALID ||
       strlen(dla_last_error()) == 0) {
     fprintf(stderr, "expected DLA_E_INVALID for n_peers = 0\n");
@@ -176,7 +214,8 @@ int main(void) {
   }
   CHECK_HIP(hipFree(dev_out));
   free(out_host);
-  printf("c_abi_demo ok: dla_wsum, dla_plan, dla_mean, dla_wsum_sharded, dla_wsum_slab_tiled bit-exact on %d peers "
+  printf("c_abi_demo ok: dla_wsum, dla_plan, dla_mean, dla_wsum_sharded, dla_wsum_slab_tiled, dla_host_round "
+         "bit-exact on %d peers "
          "x %lld fp32\n", N, (long long)P);
   return 0;
 }
