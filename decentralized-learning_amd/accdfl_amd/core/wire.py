@@ -18,7 +18,9 @@ second copy of every parameter): the tensors go straight to a PeerSlab row.
 """
 from __future__ import annotations
 
+import bisect
 import collections
+import itertools
 import io
 import os
 import pickle
@@ -64,29 +66,35 @@ class _Span:
     """A byte range of a block list (EVA's ``data_list``) that crosses block boundaries, kept
     as (host address, length) pieces of the blocks — never joined unless asked.  ``owner``
     keeps the blocks alive."""
-    __slots__ = ("addrs", "lens", "n", "owner")
+    __slots__ = ("addrs", "lens", "n", "owner", "_starts")
 
     def __init__(self, addrs, lens, owner):
         self.addrs = addrs
         self.lens = lens
         self.n = sum(lens)
         self.owner = owner
+        self._starts = None
 
     def __len__(self):
         return self.n
 
     def sub(self, a: int, b: int):
-        """(addresses, lengths) of the pieces covering [a, b) of this span."""
-        out_a, out_l, off = [], [], 0
-        for q, ln in zip(self.addrs, self.lens):
-            s, e = max(a, off), min(b, off + ln)
-            if s < e:
-                out_a.append(q + (s - off))
-                out_l.append(e - s)
-            off += ln
-            if off >= b:
-                break
-        return out_a, out_l
+        """(addresses, lengths) of the pieces covering [a, b) of this span (list slices located
+        by bisection: no per-piece Python work)."""
+        if a >= b:
+            return [], []
+        if self._starts is None:
+            self._starts = list(itertools.accumulate(self.lens[:-1], initial=0))
+        st = self._starts
+        i = bisect.bisect_right(st, a) - 1
+        j = bisect.bisect_right(st, b - 1) - 1
+        addrs = self.addrs[i:j + 1]
+        lens = self.lens[i:j + 1]
+        lens[-1] = b - st[j]
+        d = a - st[i]
+        addrs[0] += d
+        lens[0] -= d
+        return addrs, lens
 
     def read(self, a: int, b: int) -> bytes:
         import ctypes
@@ -120,10 +128,9 @@ def _gather(addrs, lens, dst: torch.Tensor) -> None:
     memcpy, threaded above 8 MiB: libdlagg's dla_host_copy_batch)."""
     from accdfl_amd import _lib
 
-    dsts, off = [], dst.data_ptr()
-    for ln in lens:
-        dsts.append(off)
-        off += ln
+    if not lens:
+        return
+    dsts = list(itertools.accumulate(lens[:-1], initial=dst.data_ptr()))
     _lib.host_copy_batch(dsts, addrs, lens)
 
 
@@ -221,57 +228,63 @@ _MARK = object()
 class _BlockReader:
     """Sequential reads over a list of byte blocks (EVA's ``data_list``, before its
     ``b''.join``, accdfl/util/eva/transfer/incoming.py:35): a read inside one block is a
-    memoryview into it, a short read across blocks is joined, a long one is a _Span."""
+    memoryview into it, a short read across blocks is joined, a long one is a _Span.  A 100 MB
+    model is ~1 700 blocks: the blocks are located by bisection over their start offsets and
+    a long read's pieces are list slices, so no Python code runs per block."""
 
     def __init__(self, blocks):
-        self.blocks = [b for b in blocks if len(b)]
-        self.views = [memoryview(b).cast("B") for b in self.blocks]
-        self.addr = [None] * len(self.blocks)
-        self.bi = 0      # current block
-        self.bo = 0      # offset in it
-        self.left = sum(len(v) for v in self.views)
+        self.blocks = []
+        self.lens = []
+        for b in blocks:
+            ln = len(b) if type(b) is bytes else memoryview(b).nbytes
+            if ln:
+                self.blocks.append(b)
+                self.lens.append(ln)
+        self.starts = list(itertools.accumulate(self.lens[:-1], initial=0)) if self.lens else []
+        self.views = [None] * len(self.blocks)
+        self.addrs = None
+        self.pos = 0
+        self.n = sum(self.lens)
 
-    def _addr(self, i: int) -> int:
-        a = self.addr[i]
-        if a is None:
-            a = self.addr[i] = _block_address(self.blocks[i])
-        return a
+    @property
+    def left(self) -> int:
+        return self.n - self.pos
+
+    def _view(self, i: int) -> memoryview:
+        v = self.views[i]
+        if v is None:
+            v = self.views[i] = memoryview(self.blocks[i]).cast("B")
+        return v
 
     def take(self, k: int):
-        if k > self.left:
+        a = self.pos
+        if k > self.n - a:
             raise UnsafePayloadError("truncated payload")
-        self.left -= k
-        v = self.views[self.bi] if self.bi < len(self.views) else None
-        if v is not None and self.bo + k <= len(v):
-            out = v[self.bo:self.bo + k]
-            self.bo += k
-            if self.bo == len(v):
-                self.bi, self.bo = self.bi + 1, 0
-            return out
+        b = a + k
+        self.pos = b
+        if k == 0:
+            return b""
+        st, lens = self.starts, self.lens
+        i = bisect.bisect_right(st, a) - 1
+        o = a - st[i]
+        if o + k <= lens[i]:
+            return self._view(i)[o:o + k]
+        j = bisect.bisect_right(st, b - 1) - 1
         if k <= 4096:  # a short read across a block boundary: joined
-            pieces = []
-            while k:
-                v = self.views[self.bi]
-                m = min(k, len(v) - self.bo)
-                pieces.append(v[self.bo:self.bo + m])
-                self.bo += m
-                k -= m
-                if self.bo == len(v):
-                    self.bi, self.bo = self.bi + 1, 0
+            pieces = [self._view(i)[o:]]
+            pieces += [self._view(q) for q in range(i + 1, j)]
+            pieces.append(self._view(j)[:b - st[j]])
             return b"".join(pieces)
-        addrs, lens = [], []
-        views, addr = self.views, self._addr
-        bi, bo = self.bi, self.bo
-        while k:
-            m = min(k, len(views[bi]) - bo)
-            addrs.append(addr(bi) + bo)
-            lens.append(m)
-            bo += m
-            k -= m
-            if bo == len(views[bi]):
-                bi, bo = bi + 1, 0
-        self.bi, self.bo = bi, bo
-        return _Span(addrs, lens, self.blocks)
+        if self.addrs is None:
+            ok = _BYTES_ADDR_OK
+            self.addrs = [id(x) + _BYTES_DATA if ok and type(x) is bytes else _block_address(x)
+                          for x in self.blocks]
+        addrs = self.addrs[i:j + 1]
+        out_lens = lens[i:j + 1]
+        addrs[0] += o
+        out_lens[0] -= o
+        out_lens[-1] = b - st[j]
+        return _Span(addrs, out_lens, self.blocks)
 
 
 def _vm_loads(data, alloc: Optional[Callable[[int], torch.Tensor]] = None) -> object:
@@ -552,23 +565,52 @@ def dumps_state_dict(state_dict: Dict[str, torch.Tensor]) -> bytes:
     skel = pickle.dumps(skeleton)
     if not big:
         return skel
+    # (host address, length, keep-alive) of every piece of the output, in order
     pieces, pos = [], 0
-    view = memoryview(skel)
+    skel_addr = id(skel) + _BYTES_DATA
     for i, (token, t) in enumerate(big):
         at = skel.find(token, pos)
         if at < 5 or skel[at - 5] != 0x42 or int.from_bytes(skel[at - 4:at], "little") != _SENTINEL_BYTES:
             return pickle.dumps(state_dict)  # unexpected pickler output: the stock path
-        pieces.append(view[pos:at - 5])
+        pieces.append((skel_addr + pos, at - 5 - pos, skel))
         head = _legacy_blob_header(t, str(i))
         n = len(head) + t.numel() * t.element_size()
-        pieces.append((b"B" + n.to_bytes(4, "little") if n < 1 << 32 else b"\x8e" + n.to_bytes(8, "little")) + head)
-        raw = t.detach()
-        if raw.dtype == torch.bfloat16:
-            raw = raw.view(torch.int16)
-        pieces.append(memoryview(raw.numpy()).cast("B"))
+        head = (b"B" + n.to_bytes(4, "little") if n < 1 << 32 else b"\x8e" + n.to_bytes(8, "little")) + head
+        pieces.append((id(head) + _BYTES_DATA, len(head), head))
+        pieces.append((t.data_ptr(), t.numel() * t.element_size(), t))
         pos = at + _SENTINEL_BYTES
-    pieces.append(view[pos:])
-    return b"".join(pieces)
+    pieces.append((skel_addr + pos, len(skel) - pos, skel))
+    return _join_pieces(pieces)
+
+
+def _join_pieces(pieces) -> bytes:
+    """One ``bytes`` holding the pieces back to back.  The object is created uninitialised
+    (PyBytes_FromStringAndSize(NULL, n), as CPython's own builders do) and filled by libdlagg's
+    threaded batched memcpy before any other code can see it, so a 100 MB model's page faults
+    and copy are spread over threads instead of b''.join's one."""
+    import ctypes
+
+    total = sum(ln for _, ln, _ in pieces)
+    if not _BYTES_ADDR_OK or total < (8 << 20):
+        return b"".join(ctypes.string_at(a, ln) if ln else b"" for a, ln, _ in pieces)
+    from accdfl_amd import _lib
+
+    out = _new_bytes(None, total)
+    dsts = list(itertools.accumulate([ln for _, ln, _ in pieces[:-1]], initial=id(out) + _BYTES_DATA))
+    _lib.host_copy_batch(dsts, [a for a, _, _ in pieces], [ln for _, ln, _ in pieces])
+    return out
+
+
+def _bytes_builder():
+    import ctypes
+
+    fn = ctypes.pythonapi.PyBytes_FromStringAndSize
+    fn.restype = ctypes.py_object
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_ssize_t]
+    return fn
+
+
+_new_bytes = _bytes_builder()
 
 
 def serialize_model(model: nn.Module) -> bytes:
@@ -584,21 +626,24 @@ def parameter_tensors(state_dict: Dict[str, torch.Tensor], template: nn.Module):
 
 
 def split_blocks(blocks: Sequence, n: int):
-    """(the first n bytes, the rest) of a block list, as two block lists of memoryviews — the
-    DFL message split at ``model_data_len`` (accdfl/dfl/community.py:587-588) with no copy."""
-    head: List[memoryview] = []
-    tail: List[memoryview] = []
+    """(the first n bytes, the rest) of a block list, as two block lists — the DFL message split
+    at ``model_data_len`` (accdfl/dfl/community.py:587-588) with no copy: blocks that fall
+    wholly on one side are passed through as they are (so a ``bytes`` block keeps its cheap
+    address), the block holding byte n becomes two memoryview slices."""
+    head: List = []
+    tail: List = []
     off = 0
     for b in blocks:
-        v = memoryview(b).cast("B")
-        if off + len(v) <= n:
-            head.append(v)
+        ln = len(b) if type(b) is bytes else memoryview(b).nbytes
+        if off + ln <= n:
+            head.append(b)
         elif off >= n:
-            tail.append(v)
+            tail.append(b)
         else:
+            v = memoryview(b).cast("B")
             head.append(v[:n - off])
             tail.append(v[n - off:])
-        off += len(v)
+        off += ln
     if off < n:
         raise ValueError("split_blocks: the blocks hold %d bytes, fewer than %d" % (off, n))
     return head, tail
