@@ -23,11 +23,14 @@ ACCDFL_AMD_RESULT_MEMORY=pooled, the default; "pinned" allocates them page-locke
 keeps them page-locked for good; "pageable" allocates them fresh).
 
 Where the arithmetic runs: always on the HIP device (libdlagg.so).  Models already
-on the device are reduced in place of their parameters with no copies; CPU models
-(every reference call site) are packed into a pinned host slab, copied H2D
-row by row on a copy stream (overlapping the packing of the next model), reduced,
-and copied back.  The host-staged path is synchronous like the reference; the
-device-resident path is stream-ordered like any torch op.
+on the device are reduced in place of their parameters with no copies; models on several
+GPUs are bucket-sharded over those GPUs (dla_wsum_sharded).  CPU models (every reference
+call site): small rounds (peer rows <= 2 MiB, the GL merge of two GNLeNet models) are packed
+into page-locked rows that the kernel reads across PCIe (dla_host_round_start / _finish)
+while the result module is built; larger rounds stream element chunks H2D straight from the
+parameters, each chunk's reduce and D2H overlapping the next chunk's H2D, optionally
+bucket-sharded over several GPUs.  The host-staged paths are synchronous like the reference;
+the device-resident path is stream-ordered like any torch op.
 """
 from __future__ import annotations
 
