@@ -221,6 +221,15 @@ def test_center_copy_is_a_deepcopy():
     assert all(p is not q for p, q in zip(got.parameters(), m.parameters()))
     got.seq(torch.zeros(1, 3, 5, 5))
     got.rnn(torch.zeros(2, 1, 4))
+    # a parametrized module (its generated class has its own __deepcopy__: the stock path, same memo)
+    from torch.nn.utils import parametrizations
+
+    pm = nn.Sequential(parametrizations.weight_norm(nn.Linear(4, 3)), nn.Linear(3, 2))
+    want, got = copy.deepcopy(pm), _center_copy(pm, large=False)
+    assert type(got[0]) is type(want[0]) and got[0] is not pm[0]
+    assert [n for n, _ in got.named_parameters()] == [n for n, _ in pm.named_parameters()]
+    assert all(p is not q for p, q in zip(got.parameters(), pm.parameters()))
+    assert got(torch.zeros(1, 4)).shape == (1, 2)
 
 
 def _tiny_models(n):
