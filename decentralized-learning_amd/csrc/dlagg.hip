@@ -779,6 +779,28 @@ __device__ __attribute__((always_inline)) inline void vec_round(
   }
 }
 
+// The m < G peers of a last round as rounds of G/2, G/4, ..., 1 peers (each full, of compile-time
+// size, in list order): no slot reloads a peer, so a 2-peer pass issues 2 loads per lane, not G.
+// Against the partial round that reloaded the last peer into the spare slots (r02 A/B,
+// profiles/r02v_ab_tail.log, tiled slab, us): 2 x 25 M f32 72.4 -> 44.5, 4 x 25 M f32 82.3 ->
+// 73.8, 12 x 11.2 M f32 88.5 -> 84.8, 20 x 5 M f32 73.1 -> 61.0, 48 x 1.23 M f32 39.0 -> 35.0,
+// 100 x 2.66 M bf16 83.3 -> 79.6, 3 x 50 M bf16 77.4 -> 64.0 (separate buffers alike).
+template <int DT, int KMAX, int G, int VW, bool ACC_IN>
+__device__ __attribute__((always_inline)) inline void vec_tail(
+    const PeerTable<typename Ops<DT>::w_t, KMAX>& tab, int k0, int m, bool first_round, int64_t a,
+    typename Ops<DT>::acc_t (&acc)[VW][Ops<DT>::WE]) {
+  if constexpr (G > 1) {
+    constexpr int H = G / 2;
+    if (m >= H) {
+      vec_round<DT, KMAX, H, VW, true, ACC_IN>(tab, k0, H, first_round, a, acc);
+      k0 += H;
+      m -= H;
+      first_round = false;
+    }
+    vec_tail<DT, KMAX, H, VW, ACC_IN>(tab, k0, m, first_round, a, acc);
+  }
+}
+
 // TILED: the peers are rows of a tile-interleaved slab (dla_wsum_slab_tiled): vector i of a peer at
 // p[k] + (i >> tshift_v) * tstride_v + (i & (2^tshift_v - 1)); the output stays contiguous.
 // PLAIN_ST: plain (L2 write-back) output stores instead of sc1 — faster when the output is small
@@ -814,10 +836,12 @@ __global__ __launch_bounds__(64) void wsum_vec_kernel(
   for (int r = 0; r < (KMAX + G - 1) / G; ++r) {
     const int k0 = r * G;
     if (k0 >= n_peers) break;
-    if (k0 + G <= n_peers)  // full round: its own unpredicated path (as wsum_wide_kernel)
+    if (k0 + G <= n_peers) {  // full round: its own unpredicated path (as wsum_wide_kernel)
       vec_round<DT, KMAX, G, VW, true, ACC_IN>(tab, k0, G, r == 0, a, acc);
-    else
-      vec_round<DT, KMAX, G, VW, false, ACC_IN>(tab, k0, n_peers - k0, r == 0, a, acc);
+    } else {
+      vec_tail<DT, KMAX, G, VW, ACC_IN>(tab, k0, n_peers - k0, r == 0, a, acc);
+      break;
+    }
   }
   if (live) {
     V o;

@@ -121,12 +121,14 @@ def test_every_launch_variant_is_bit_exact(dtype):
 
 
 @pytest.mark.parametrize("dtype", ["f32", "bf16", "f16", "f64"])
-@pytest.mark.parametrize("n", [1, 9, 33, 64, 129, 200])
+@pytest.mark.parametrize("n", [1, 7, 9, 31, 33, 64, 95, 129, 200])
 @pytest.mark.parametrize("numel", [1, 2, 63, 21_339, 100_007])
 def test_wide_kernel_bit_exact(dtype, n, numel):
     """Word-per-lane kernel (variant 8; auto-picked for small shares over > 8 peers), its
-    8- and 16-byte-per-lane forms (variants 9-12; 21 = 9 with plain stores), and the 16-byte stream's lane-parallel ragged
-    tail (up to 7 tail elements for 16-bit dtypes), every dtype, single and multi-pass peer counts."""
+    8- and 16-byte-per-lane forms (variants 9-12; 21 = 9 with plain stores), and the 16-byte
+    stream's lane-parallel ragged tail (up to 7 tail elements for 16-bit dtypes), every dtype,
+    single and multi-pass peer counts; 31 and 95 peers leave a last round that the vector kernel
+    splits into 16+8+4+2+1 peers (variant 9)."""
     from accdfl_amd import _lib
     from accdfl_amd.core import wsum
 
@@ -601,12 +603,13 @@ def _tiled_slab(peers, tile_elems, dtype):
 
 
 @pytest.mark.parametrize("dtype", ["f32", "bf16", "f16"])
-@pytest.mark.parametrize("n", [1, 8, 16, 33, 130])
+@pytest.mark.parametrize("n", [1, 3, 7, 8, 16, 31, 33, 130])
 @pytest.mark.parametrize("numel", [5, 4097, 300_007, 4096 * 9 + 3])
 @pytest.mark.parametrize("tile_bytes", [16, 1024, 4096, 16384])
 def test_tiled_slab_bit_exact(dtype, n, numel, tile_bytes):
     """dla_wsum_slab_tiled (tile-interleaved PeerSlab layout): every kernel form, ragged tails
-    (tiled addressing in the tail workgroup too), multi-pass peer counts, IEEE specials."""
+    (tiled addressing in the tail workgroup too), multi-pass peer counts, last rounds split into
+    smaller full rounds (3 = 2+1, 7 = 4+2+1, 31 = 16+8+4+2+1 peers), IEEE specials."""
     from accdfl_amd import _lib
     from accdfl_amd.core import wsum
 
