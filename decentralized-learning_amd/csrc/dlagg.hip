@@ -1164,7 +1164,7 @@ hipError_t launch_wide(const PeerTable<typename Ops<DT>::w_t, KMAX>& tab, int n,
 template <int DT, int KMAX, bool ACC_IN>
 hipError_t launch_vec(const PeerTable<typename Ops<DT>::w_t, KMAX>& tab, int n, int64_t n_elems, void* out,
                       hipStream_t s, int variant) {
-  if constexpr (DT == DLA_F64 || KMAX == 8) {
+  if constexpr (DT == DLA_F64) {
     return hipErrorInvalidValue;
   } else {
     constexpr int WE = Ops<DT>::WE;
@@ -1311,7 +1311,14 @@ hipError_t launch_pass(const PeerTable<typename Ops<DT>::w_t, KMAX>& tab, int n,
     return hipGetLastError();
   }
   if ((l.variant >= 9 && l.variant <= 12) || l.variant == 21) {
-    if constexpr (DT != DLA_F64 && KMAX != 8) return launch_vec<DT, KMAX, ACC_IN>(tab, n, n_elems, out, s, l.variant);
+    if constexpr (DT != DLA_F64) return launch_vec<DT, KMAX, ACC_IN>(tab, n, n_elems, out, s, l.variant);
+  }
+  if constexpr ((DT == DLA_BF16 || DT == DLA_F16) && KMAX == 8) {
+    // up to 8 bf16 / f16 peers: the vector-per-lane kernel too (r02 A/B against the 16-byte
+    // stream, profiles/r02w_vec8.log, us: 6 x 25 M bf16 51.9 vs 58.8, 8 x 50 M bf16 136.3 vs
+    // 138.5, 4 x 50 M f16 72.4 vs 73.1; fp32 keeps the stream / big tile: 4 x 25 M 73.2 vs 72.3,
+    // 8 x 25 M 134.9 vs 135.1)
+    if (l.auto_kernel) return launch_vec<DT, KMAX, ACC_IN>(tab, n, n_elems, out, s, vec_variant(n));
   }
   if constexpr (DT != DLA_F64 && KMAX != 8) {
     // more than 8 peers: the vector-per-lane kernel, unless an fp32 big tile applies (below)
@@ -1747,6 +1754,7 @@ const char* dla_select_kernel(int dtype, int n_peers, int64_t n_elems) {
   if (es == 0 || n_peers < 1 || n_elems < 0) return "";
   const int e = 16 / es;  // elements per 16-byte chunk
   const int first_pass = n_peers < kMaxPeersPerPass ? n_peers : kMaxPeersPerPass;
+  if ((dtype == DLA_BF16 || dtype == DLA_F16) && first_pass <= 8) return "wsum_vec_kernel";
   if (dtype != DLA_F64 && first_pass > 8 &&
       !(dtype == DLA_F32 && (first_pass == 16 || first_pass == 32) && use_bigtile(n_elems / e, e, n_peers)))
     return "wsum_vec_kernel";

@@ -58,8 +58,9 @@ extern "C" {
 
 /* Launch tuning knobs for dla_wsum_ex (0 = library default for each field). */
 typedef struct dla_launch_cfg {
-  int variant;      /* 0 = by shape: passes of more than 8 fp32 / bf16 / f16 peers take 9
-                       (>= 32 peers; 21 when the output is <= 8 MiB) or 12; fp32 shares over 8, 16 or 32 peers beyond
+  int variant;      /* 0 = by shape: passes of bf16 / f16 peers and of more than 8 fp32
+                       peers take 9 (>= 32 peers; 21 when the output is <= 8 MiB) or 12;
+                       fp32 shares over 8, 16 or 32 peers beyond
                        256 MiB whose big tiles fill >= 80 % of their last round of 1024
                        resident waves take 16 (17 from one full round up), fp64 over 4..8
                        likewise; fp64 small shares over more than 8 peers 8; otherwise 4.

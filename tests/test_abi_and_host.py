@@ -83,7 +83,8 @@ def test_library_version_and_argument_errors(lib_path):
     assert _lib.select_kernel(0, 32, 4_110_000) == "wsum_bigtile_kernel"
     assert _lib.select_kernel(0, 32, 8_200_000) == "wsum_bigtile_kernel"
     assert _lib.select_kernel(0, 24, 8_200_000) == "wsum_vec_kernel"
-    assert _lib.select_kernel(1, 8, 50_000_000) == "wsum_stream_kernel"
+    assert _lib.select_kernel(1, 8, 50_000_000) == "wsum_vec_kernel"  # bf16 / f16: any peer count
+    assert _lib.select_kernel(2, 3, 1000) == "wsum_vec_kernel" and _lib.select_kernel(3, 3, 1000) != "wsum_vec_kernel"
     assert _lib.select_kernel(9, 8, 100) == "" and _lib.select_kernel(0, 0, 100) == ""
     # tile of the tile-interleaved PeerSlab (dla_slab_tile_elems, host-only)
     assert _lib.slab_tile_elems(0, 8, 25_000_000) * 4 == 16384
