@@ -113,6 +113,8 @@ def parse():
                          "(what the CPU test of the multi-rank launch runs)")
     ap.add_argument("--sweep", action="store_true", help="interleaved A/B of launch variants, then exit")
     ap.add_argument("--host-breakdown", action="store_true", help="time the host-inclusive phases, then exit")
+    ap.add_argument("--host-configs-only", action="store_true",
+                    help="print the per-config host-inclusive table (CPU modules, real layouts), then exit")
     ap.add_argument("--configs-only", action="store_true",
                     help="print the per-BASELINE-config device-resident table (no CPU legs), then exit")
     ap.add_argument("--sweep-cfgs", default="", help="variant,chunks,grid;... (default: built-in list)")
@@ -543,6 +545,106 @@ def _median_ms(fn, reps):
         fn()
         ts.append(time.perf_counter() - t0)
     return round(statistics.median(ts) * 1e3, 3)
+
+
+LAYOUTS_FILE = os.path.join(ROOT, "tests", "golden", "layouts.json")  # recorded from the reference's create_model
+
+# (layout, peers, dtype) of every GPU config's WHOLE model as the reference aggregator holds it:
+# N CPU modules with the real parameter / buffer layout (SURVEY.md §8d host-inclusive rate).
+HOST_CONFIGS = {
+    "configs[1] CIFAR-10 GNLeNet, 8 peers": ("gnlenet", 8, "f32"),
+    "configs[2] FEMNIST CNN, 32 peers": ("femnist_cnn", 32, "f32"),
+    "configs[3] CIFAR-10 GNLeNet, 64 peers": ("gnlenet", 64, "f32"),
+    "configs[3'] CIFAR-10 ResNet-8, 64 peers": ("cifar10_resnet8", 64, "f32"),
+    "configs[4] google_speech ResNet-34, 128 peers, bf16": ("google_speech_resnet34", 128, "bf16"),
+}
+
+
+def _layout(name):
+    if name == "gnlenet":
+        return [list(s) for s in GNLENET], []
+    lay = json.load(open(LAYOUTS_FILE))[name]
+    return [s for _, s, _ in lay["params"]], [(s, d) for _, s, d in lay["buffers"]]
+
+
+def _layout_models(name, n, dt, pinned, seed=4000):
+    """n CPU modules with the layout `name`: one tensor per parameter (pageable, allocated
+    apart as load_state_dict leaves them) or views of one page-locked row per peer (what a
+    page-locked ingress buffer holds, e.g. DeviceModelManager's EVA gather); BN buffers as
+    the reference models carry them.  Values: one seeded normal(0, 0.05) base scaled per
+    peer (the values do not change any timing)."""
+    from torch import nn
+
+    shapes, bufs = _layout(name)
+    numels = [int(np.prod(s)) if s else 1 for s in shapes]
+    base = torch.randn(sum(numels), generator=torch.Generator().manual_seed(seed)) * 0.05
+    models = []
+    for k in range(n):
+        flat = (base * (1.0 + 0.001 * k)).to(dt)
+        if pinned:
+            flat = flat.pin_memory()
+            parts = [t.view(s) for t, s in zip(flat.split(numels), shapes)]
+        else:
+            parts = [t.view(s).clone() for t, s in zip(flat.split(numels), shapes)]
+        m = nn.Module()
+        m.ps = nn.ParameterList([nn.Parameter(t) for t in parts])
+        for j, (s, bdt) in enumerate(bufs):
+            m.register_buffer("b%d" % j, torch.zeros(s, dtype=getattr(torch, bdt)))
+        models.append(m)
+        del flat
+    return models, sum(numels)
+
+
+def host_inclusive_configs(reps=3):
+    """FedAvg.aggregate on every GPU config's whole model as CPU modules with the reference's
+    real layout, end to end (deepcopy, H2D of N x P, reduce, D2H into the result), with the
+    peers' parameters pageable (every reference call site) and page-locked (peers decoded into
+    page-locked ingress buffers).  The reference op sequence on the same pageable modules is
+    timed in the cpu_baseline leg (cpu_layout_configs)."""
+    from accdfl_amd.core.gradient_aggregation.fedavg import FedAvg, release_staging
+
+    res = {}
+    for name, (lay, n, dts) in HOST_CONFIGS.items():
+        dt = torch.float32 if dts == "f32" else torch.bfloat16
+        es = 4 if dts == "f32" else 2
+        row = {"peers": n, "dtype": dts}
+        for mem in ("pageable", "pinned"):
+            log("host-inclusive %s (%s peers)" % (name, mem))
+            models, p = _layout_models(lay, n, dt, mem == "pinned")
+            w = [float(1.0 / n)] * n
+            ms = _median_ms(lambda: FedAvg.aggregate(models, w), reps)
+            row["params"] = p
+            row["tensors"] = len(list(models[0].parameters()))
+            row[mem + "_ms"] = ms
+            row[mem + "_GB/s"] = round((n + 1) * p * es / (ms / 1e3) / 1e9, 2)
+            del models
+        row["h2d_bytes"] = n * p * es
+        res[name] = row
+    release_staging()
+    return res
+
+
+def cpu_layout_configs(budget_s=2.0):
+    """The reference op sequence (oracle port of fedavg.py:13-26, torch-CPU, T tensors per
+    model) on the pageable modules of host_inclusive_configs."""
+    sys.path.insert(0, ROOT)
+    from oracle.fedavg_oracle import fedavg_modules_torch  # timed CPU baseline (kind "port")
+
+    torch.set_num_threads(cpu_threads()[0])
+    res = {}
+    for name, (lay, n, dts) in HOST_CONFIGS.items():
+        dt = torch.float32 if dts == "f32" else torch.bfloat16
+        models, p = _layout_models(lay, n, dt, False)
+        w = [float(1.0 / n)] * n
+        ts = []
+        start = time.perf_counter()
+        while (time.perf_counter() - start < budget_s and len(ts) < 20) or len(ts) < 1:
+            t0 = time.perf_counter()
+            fedavg_modules_torch(models, w)
+            ts.append(time.perf_counter() - t0)
+        res[name] = {"cpu_port_ms": round(statistics.median(ts) * 1e3, 2), "reps": len(ts)}
+        del models
+    return res
 
 
 def host_inclusive_small(reps=50):
@@ -1103,6 +1205,12 @@ def main():
     if args.host_breakdown:
         print(json.dumps(host_breakdown(args.peers, args.params, device)))
         return
+    if args.host_configs_only:
+        print(json.dumps(dict(config="north star 8 x 25 M f32 (one tensor per peer)",
+                              **host_inclusive(args.peers, args.params))), flush=True)
+        for name, row in host_inclusive_configs().items():
+            print(json.dumps(dict(config=name, **row)), flush=True)
+        return
     if args.configs_only:
         for name, row in baseline_configs(device).items():
             print(json.dumps(dict(config=name, **row)))
@@ -1219,6 +1327,7 @@ def main():
             result["host_inclusive"] = host_inclusive(n, p)
             result["wire_ingress"] = wire_ingress(p, device)
             result["host_inclusive_small"] = host_inclusive_small()
+            result["host_inclusive_configs"] = host_inclusive_configs()
             log("DFL round from EVA blocks")
             msgs = dfl_messages(n, p)
             result["dfl_round"] = dfl_round(msgs, p, device)
@@ -1240,6 +1349,13 @@ def main():
                 msgs = dfl_messages(n, p)
                 cb["dfl_round_reference_style"] = dfl_round_reference_style(msgs, p)
                 del msgs
+                log("cpu baseline: reference op sequence on the config layouts")
+                cb["layout_configs"] = cpu_layout_configs()
+                for name, row in cb["layout_configs"].items():
+                    g = result.get("host_inclusive_configs", {}).get(name)
+                    if g:
+                        g["cpu_port_ms"] = row["cpu_port_ms"]
+                        g["pageable_over_cpu"] = round(row["cpu_port_ms"] / g["pageable_ms"], 1)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

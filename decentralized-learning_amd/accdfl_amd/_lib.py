@@ -23,7 +23,7 @@ LIB_PATH = os.environ.get("DLAGG_LIB", os.path.join(PKG_ROOT, "lib", "libdlagg.s
 
 # dtype codes (include/dlagg.h)
 DLA_F32, DLA_BF16, DLA_F16, DLA_F64 = 0, 1, 2, 3
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 HIPCC_FLAGS = [
     "--offload-arch=gfx950",
@@ -58,6 +58,7 @@ EXPORTED = (
     "dla_slab_tile_elems",
     "dla_host_round_start",
     "dla_host_round_finish",
+    "dla_host_reduce",
 )
 
 
@@ -187,6 +188,10 @@ class _Lib:
         so.dla_host_round_finish.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int64), vp,
                                              ctypes.POINTER(vp), vp]
         so.dla_host_round_finish.restype = ctypes.c_int
+        so.dla_host_reduce.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(vp),
+                                       ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_double),
+                                       ctypes.POINTER(vp), ctypes.c_int64, vp, vp, vp, vp, vp, vp]
+        so.dla_host_reduce.restype = ctypes.c_int
         so.dla_plan_destroy.argtypes = [vp]
         so.dla_plan_destroy.restype = None
         v = so.dla_version()
@@ -314,6 +319,21 @@ def host_round_start(dtype_code: int, n_peers: int, tensor_ptrs: Sequence[int], 
                                    numels, _dbl_array(weights), rows_ptr, pitch_elems, result_ptr, stream_ptr)
     if rc != 0:
         L.check(rc, "dla_host_round_start")
+
+
+def host_reduce(dtype_code: int, n_peers: int, tensor_ptrs: Sequence[int], numels, weights: Sequence[float],
+                out_ptrs: Sequence[int], chunk_elems: int, h_stage: int, d_stage: int, h_out: int, d_out: int,
+                stream_ptr: int, copy_stream_ptr: int) -> None:
+    """dla_host_reduce: a large round of host tensors through the GPU in packed chunks (synchronous).
+    ``tensor_ptrs``: peer-major, n_peers * len(numels) host pointers; ``out_ptrs``: one per tensor."""
+    L = lib()
+    if not isinstance(numels, ctypes.Array):
+        numels = (ctypes.c_int64 * len(numels))(*numels)
+    rc = L.so.dla_host_reduce(dtype_code, n_peers, len(numels), (ctypes.c_void_p * len(tensor_ptrs))(*tensor_ptrs),
+                              numels, _dbl_array(weights), (ctypes.c_void_p * len(out_ptrs))(*out_ptrs), chunk_elems,
+                              h_stage, d_stage, h_out, d_out, stream_ptr, copy_stream_ptr)
+    if rc != 0:
+        L.check(rc, "dla_host_reduce")
 
 
 def host_round_finish(dtype_code: int, numels, result_ptr: int, out_ptrs: Sequence[int], stream_ptr: int) -> None:

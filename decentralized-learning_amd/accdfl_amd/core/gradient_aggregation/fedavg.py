@@ -27,9 +27,10 @@ on the device are reduced in place of their parameters with no copies; models on
 GPUs are bucket-sharded over those GPUs (dla_wsum_sharded).  CPU models (every reference
 call site): small rounds (peer rows <= 2 MiB, the GL merge of two GNLeNet models) are packed
 into page-locked rows that the kernel reads across PCIe (dla_host_round_start / _finish)
-while the result module is built; larger rounds stream element chunks H2D straight from the
-parameters, each chunk's reduce and D2H overlapping the next chunk's H2D, optionally
-bucket-sharded over several GPUs.  The host-staged paths are synchronous like the reference;
+while the result module is built; larger rounds stream element chunks through the GPU in one
+native call (dla_host_reduce: a threaded pack of every peer's chunk into page-locked rows, one
+DMA per chunk, the reduce, the D2H and the unpack into the result, two chunks in flight),
+optionally bucket-sharded over several GPUs.  The host-staged paths are synchronous like the reference;
 the device-resident path is stream-ordered like any torch op.
 """
 from __future__ import annotations
@@ -125,6 +126,7 @@ def release_staging() -> None:
     with _staging_lock:
         _staging.clear()
         _staging_sharded.clear()
+        _native_staging.clear()
         _host_rounds.clear()
 
 
@@ -340,18 +342,101 @@ def _bucket_pipelined(st, dev, flats: List[List[torch.Tensor]], numels: List[int
         compute.synchronize()
 
 
-# How the host-staged path moves a large round: "pipelined" (default) — one Python thread
-# per GPU, each streaming its bucket through _bucket_pipelined (H2D straight from the
-# pageable parameters, no host pack; torch releases the GIL inside the copies, so the GPUs'
-# copies run concurrently) — or "packed": one thread packing every peer into pinned
-# staging peer-major and issuing the DMAs (the packs are serial, the DMAs overlap).
-# ACCDFL_AMD_HOST_PATH=packed selects the latter.
-_SHARD_THREADS = os.environ.get("ACCDFL_AMD_HOST_PATH", "pipelined") != "packed"
+class _NativeStaging:
+    """Double-buffered chunk staging of dla_host_reduce for one (device, dtype, slot): page-locked
+    h_stage / h_out and device d_stage / d_out, grown on demand and reused across rounds."""
+
+    def __init__(self, device: torch.device, dtype: torch.dtype):
+        self.device = device
+        self.dtype = dtype
+        self.rows = self.chunk = 0
+        self.h_stage = self.d_stage = self.h_out = self.d_out = None
+        self.copy_stream = torch.cuda.Stream(device)
+
+    def ensure(self, rows: int, chunk: int):
+        if rows <= self.rows and chunk <= self.chunk:
+            return
+        rows, chunk = max(rows, self.rows), max(chunk, self.chunk)
+        self.h_stage = self.d_stage = self.h_out = self.d_out = None
+        self.h_stage = torch.empty(2 * rows * chunk, dtype=self.dtype, pin_memory=True)
+        self.d_stage = torch.empty(2 * rows * chunk, dtype=self.dtype, device=self.device)
+        self.h_out = torch.empty(2 * chunk, dtype=self.dtype, pin_memory=True)
+        self.d_out = torch.empty(2 * chunk, dtype=self.dtype, device=self.device)
+        self.rows, self.chunk = rows, chunk
+
+
+_native_staging: Dict[Tuple[torch.device, torch.dtype, int], _NativeStaging] = {}
+
+# Bytes of every peer's rows per chunk of dla_host_reduce (two chunks in flight): large enough that
+# one DMA per chunk runs at the PCIe rate, small enough that packing chunk c+1 overlaps the DMA of
+# chunk c from the start of the round.
+_NATIVE_CHUNK_BYTES = int(float(os.environ.get("ACCDFL_AMD_HOST_CHUNK_MB", "32")) * (1 << 20))
+
+
+def _native_chunk(n: int, esize: int, bucket: int, align: int) -> int:
+    chunk = max(align, _NATIVE_CHUNK_BYTES // (n * esize) // align * align)
+    return min(chunk, _round_up(bucket, align))
+
+
+def _get_native_staging(device: torch.device, dtype: torch.dtype, slot: int, rows: int,
+                        chunk: int) -> _NativeStaging:
+    """(caller holds _staging_lock)"""
+    key = (device, dtype, slot)
+    st = _native_staging.get(key)
+    if st is None:
+        st = _native_staging[key] = _NativeStaging(device, dtype)
+    st.ensure(rows, chunk)
+    return st
+
+
+def _bucket_native(st: _NativeStaging, dev, flats: List[List[torch.Tensor]], numels: List[int], s: int, e: int,
+                   weights, center: List[torch.Tensor], h_out, align: int):
+    """Bucket [s, e) of every peer through one GPU by dla_host_reduce: per chunk, one threaded pack
+    of every peer's slices into page-locked rows, ONE H2D DMA, the list-order reduce, the D2H and
+    the unpack into the result, two chunks in flight.  (The pipelined path issues one DMA per
+    tensor per peer per chunk: 14 080 per chunk for 128 ResNet-34 models.)"""
+    n = len(flats)
+    dtype = st.dtype
+    chunk = _native_chunk(n, st.h_stage.element_size(), e - s, align)
+    parts = [_flat_slices(f, numels, s, e) for f in flats]
+    sizes = [t.numel() for t in parts[0]]
+    ptrs = [t.data_ptr() for pl in parts for t in pl]
+    outs = _flat_slices(center, numels, s, e) if h_out is None else [h_out[s:e]]
+    compute = torch.cuda.current_stream(dev)
+    st.copy_stream.wait_stream(compute)  # earlier users of the device staging are done
+    with torch.cuda.device(dev):
+        _lib.host_reduce(_wsum.dtype_code(dtype), n, ptrs, sizes, weights, [o.data_ptr() for o in outs], chunk,
+                         st.h_stage.data_ptr(), st.d_stage.data_ptr(), st.h_out.data_ptr(), st.d_out.data_ptr(),
+                         compute.cuda_stream, st.copy_stream.cuda_stream)
+
+
+# How the host-staged path moves a large round (ACCDFL_AMD_HOST_PATH):
+# * "native" (default): one host thread per GPU, each streaming its bucket through
+#   dla_host_reduce (_bucket_native: threaded pack into page-locked chunk rows, one DMA per chunk);
+# * "pipelined": one host thread per GPU, each streaming its bucket through _bucket_pipelined
+#   (one H2D per tensor per peer per chunk, straight from the pageable parameters);
+# * "packed": one thread packing every peer into pinned staging peer-major and issuing the DMAs.
+# Peers that are not contiguous CPU tensors take "pipelined".
+_HOST_PATHS = ("native", "pipelined", "packed")
+_HOST_PATH = os.environ.get("ACCDFL_AMD_HOST_PATH", "native")
+if _HOST_PATH not in _HOST_PATHS:
+    raise ValueError("ACCDFL_AMD_HOST_PATH must be one of %s" % (_HOST_PATHS,))
+
+
+def set_host_path(mode: str) -> None:
+    global _HOST_PATH
+    if mode not in _HOST_PATHS:
+        raise ValueError("host path must be one of %s" % (_HOST_PATHS,))
+    _HOST_PATH = mode
+
+
+def host_path() -> str:
+    return _HOST_PATH
 
 
 def set_shard_threads(enabled: bool) -> None:
-    global _SHARD_THREADS
-    _SHARD_THREADS = bool(enabled)
+    """True: one host thread per GPU (the default "native" path); False: the serial "packed" path."""
+    set_host_path("native" if enabled else "packed")
 
 
 def _reduce_host_staged(devices: List[torch.device], dtype, center: List[torch.Tensor],
@@ -375,12 +460,17 @@ def _reduce_host_staged(devices: List[torch.device], dtype, center: List[torch.T
     bounds = bucket_bounds(total, len(devices), align)
     n = len(peers)
     flats = [[p.detach().reshape(-1) for p in pl] for pl in peers]
+    native = _HOST_PATH == "native" and all(t.device.type == "cpu" and t.is_contiguous() for f in flats for t in f)
     with _staging_lock:
         stages = []
         for dev, (s, e) in zip(devices, bounds):
-            st = _get_staging(dev, dtype) if len(devices) == 1 else _get_staging_sharded(dev, dtype, len(stages))
-            st.ensure(n, _round_up(max(e - s, 1), align))
-            st.copy_stream.wait_stream(torch.cuda.current_stream(dev))  # previous users of d_in are done
+            if native:
+                st = _get_native_staging(dev, dtype, len(stages) if len(devices) > 1 else -1, n,
+                                         _native_chunk(n, esize, max(e - s, 1), align))
+            else:
+                st = _get_staging(dev, dtype) if len(devices) == 1 else _get_staging_sharded(dev, dtype, len(stages))
+                st.ensure(n, _round_up(max(e - s, 1), align))
+                st.copy_stream.wait_stream(torch.cuda.current_stream(dev))  # previous users of d_in are done
             stages.append(st)
         # D2H straight into the result's parameters when they are dense (pageable ones through the
         # runtime's staging, page-locked ones directly); non-dense results go through one pinned buffer.
@@ -396,13 +486,16 @@ def _reduce_host_staged(devices: List[torch.device], dtype, center: List[torch.T
 def _run_bucket_jobs(jobs, devices, flats, numels, weights, center, h_out, align, n):
     """Every bucket's H2D -> reduce -> D2H, one thread per GPU (pipelined) or peer-major from
     this thread (packed); returns when every D2H has landed."""
-    if _SHARD_THREADS:
+    if _HOST_PATH != "packed":
         from concurrent.futures import ThreadPoolExecutor
 
         def bucket(job):
             st, dev, s, e = job
             with torch.no_grad():  # grad mode is per thread; the result's parameters are leaves
-                _bucket_pipelined(st, dev, flats, numels, s, e, weights, center, h_out, align)
+                if isinstance(st, _NativeStaging):
+                    _bucket_native(st, dev, flats, numels, s, e, weights, center, h_out, align)
+                else:
+                    _bucket_pipelined(st, dev, flats, numels, s, e, weights, center, h_out, align)
 
         if len(jobs) == 1:
             bucket(jobs[0])

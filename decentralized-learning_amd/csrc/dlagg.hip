@@ -34,9 +34,14 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <chrono>
 #include <cstdint>
+#include <cstdio>
 #include <cstdlib>
+#include <condition_variable>
 #include <cstring>
+#include <functional>
 #include <mutex>
 #include <new>
 #include <set>
@@ -805,8 +810,11 @@ __device__ __attribute__((always_inline)) inline void vec_tail(
 // p[k] + (i >> tshift_v) * tstride_v + (i & (2^tshift_v - 1)); the output stays contiguous.
 // PLAIN_ST: plain (L2 write-back) output stores instead of sc1 — faster when the output is small
 // and many peers are read per element, slower for large outputs (vec_store_policy).
-template <int DT, int KMAX, int G, int VW, bool ACC_IN, bool TILED = false, bool PLAIN_ST = false>
-__global__ __launch_bounds__(64) void wsum_vec_kernel(
+// BS: threads per workgroup (one lane per vector either way); XCD: remap workgroup ids so each of
+// the 8 XCDs (which take workgroups round-robin) walks one contiguous eighth of the vectors.
+template <int DT, int KMAX, int G, int VW, bool ACC_IN, bool TILED = false, bool PLAIN_ST = false, int BS = 64,
+          bool XCD = false>
+__global__ __launch_bounds__(BS) void wsum_vec_kernel(
     const PeerTable<typename Ops<DT>::w_t, KMAX> tab, int n_peers, int64_t n_vecs,
     int64_t n_elems, void* __restrict__ out_v, int tshift_v = 0, int64_t tstride_v = 0, int tshift_e = -1,
     int64_t tstride_e = 0) {
@@ -815,13 +823,18 @@ __global__ __launch_bounds__(64) void wsum_vec_kernel(
   using acc_t = typename O::acc_t;
   using V = typename VecOf<VW>::T;
   constexpr int WE = O::WE;               // elements per dword
-  const int64_t main_grid = (n_vecs + 63) / 64;
+  const int64_t main_grid = (n_vecs + BS - 1) / BS;
   if (blockIdx.x >= main_grid) {  // the ragged-tail workgroup (< VW * WE elements)
     fold_tail<DT, ACC_IN>(tab.p, tab.w, n_peers, n_vecs * VW * WE, n_elems, out_v, TILED ? tshift_e : -1,
                           tstride_e);
     return;
   }
-  const int64_t j = static_cast<int64_t>(blockIdx.x) * 64 + threadIdx.x;
+  int64_t b = blockIdx.x;
+  if constexpr (XCD) {
+    const int64_t q = main_grid >> 3;
+    if (b < (q << 3)) b = (b & 7) * q + (b >> 3);
+  }
+  const int64_t j = b * BS + threadIdx.x;
   const bool live = j < n_vecs;
   const int64_t i = live ? j : n_vecs - 1;  // clamped: loads stay unpredicated
   const int64_t a = TILED ? (i >> tshift_v) * tstride_v + (i & ((int64_t{1} << tshift_v) - 1)) : i;
@@ -1200,7 +1213,7 @@ hipError_t launch_vec_tiled(const PeerTable<typename Ops<DT>::w_t, KMAX>& tab, i
     return hipErrorInvalidValue;
   } else {
     constexpr int WE = Ops<DT>::WE;
-#define DLA_VECT(G_, VW_, PST_)                                                                                     \
+#define DLA_VECT(G_, VW_, PST_, BS_, XCD_)                                                                          \
   do {                                                                                                        \
     constexpr int G = KMAX < (G_) ? KMAX : (G_);                                                              \
     constexpr int per_vec = (VW_) * WE;                                                                       \
@@ -1208,18 +1221,21 @@ hipError_t launch_vec_tiled(const PeerTable<typename Ops<DT>::w_t, KMAX>& tab, i
     while ((1 << vs) < per_vec) ++vs;                                                                         \
     if (tshift_e < vs) return hipErrorInvalidValue;                                                           \
     const int64_t n_vecs = n_elems / per_vec;                                                                 \
-    int64_t grid = (n_vecs + 63) / 64;                                                                        \
+    int64_t grid = (n_vecs + (BS_) - 1) / (BS_);                                                              \
     if (n_elems > n_vecs * per_vec) ++grid;                                                                   \
     if (grid < 1 || grid > 0x7fffffff) return hipErrorInvalidValue;                                           \
-    hipLaunchKernelGGL((wsum_vec_kernel<DT, KMAX, G, VW_, ACC_IN, true, PST_>), dim3(static_cast<unsigned>(grid)),   \
-                       dim3(64), 0, s, tab, n, n_vecs, n_elems, out, tshift_e - vs, tstride_e / per_vec, tshift_e, \
-                       tstride_e);                                                                            \
+    hipLaunchKernelGGL((wsum_vec_kernel<DT, KMAX, G, VW_, ACC_IN, true, PST_, BS_, XCD_>),                    \
+                       dim3(static_cast<unsigned>(grid)), dim3(BS_), 0, s, tab, n, n_vecs, n_elems, out,       \
+                       tshift_e - vs, tstride_e / per_vec, tshift_e, tstride_e);                              \
   } while (0)
     switch (variant) {
-      case 12: DLA_VECT(16, 2, false); break;
-      case 10: DLA_VECT(16, 4, false); break;
-      case 21: DLA_VECT(32, 2, true); break;
-      default: DLA_VECT(32, 2, false); break;
+      case 12: DLA_VECT(16, 2, false, 64, false); break;
+      case 10: DLA_VECT(16, 4, false, 64, false); break;
+      case 21: DLA_VECT(32, 2, true, 64, false); break;
+      case 22: DLA_VECT(32, 2, false, 256, false); break;
+      case 23: DLA_VECT(32, 2, false, 64, true); break;
+      case 24: DLA_VECT(32, 2, false, 256, true); break;
+      default: DLA_VECT(32, 2, false, 64, false); break;
     }
 #undef DLA_VECT
     return hipGetLastError();
@@ -1686,16 +1702,76 @@ int wsum_sharded_impl(int dtype, int n_shards, const int* dev_ids, const void* c
   return DLA_OK;
 }
 
-// Threads for one dla_host_copy_batch: one per 8 MiB up to DLA_COPY_THREADS (default 8; the GPU
-// box's CPU share is 16); batches under 8 MiB stay on the calling thread.
+// Threads for one dla_host_copy_batch: one per 2 MiB up to DLA_COPY_THREADS (default 8; the GPU
+// box's CPU share is 16); batches under 4 MiB stay on the calling thread.
 int copy_threads(int64_t total) {
   static const int cap = [] {
     const char* e = std::getenv("DLA_COPY_THREADS");
     const int v = e ? std::atoi(e) : 8;
     return v < 1 ? 1 : v > 64 ? 64 : v;
   }();
-  const int64_t by_size = total >> 23;
-  return static_cast<int>(by_size < 1 ? 1 : by_size < cap ? by_size : cap);
+  const int64_t by_size = total >> 21;
+  return static_cast<int>(by_size < 2 ? 1 : by_size < cap ? by_size : cap);
+}
+
+// Persistent copy workers.  dla_host_reduce packs every chunk of a round (hundreds of chunks for
+// the 128-peer google_speech round), so threads spawned per call (10-20 us each) would add up.
+// One round at a time runs on the pool; a concurrent caller (the bucket-sharded host path runs one
+// host thread per GPU) spawns its own threads instead.  The pool is never destroyed: its workers
+// sleep on the condition variable until the process exits.
+class CopyPool {
+ public:
+  // fn(0) on the calling thread and fn(1..n-1) on workers; false if another round holds the pool.
+  template <typename F>
+  bool try_run(int n, F& fn) {
+    std::unique_lock<std::mutex> busy(run_mu_, std::try_to_lock);
+    if (!busy.owns_lock()) return false;
+    std::function<void(int)> task = [&fn](int t) { fn(t); };
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      while (static_cast<int>(workers_.size()) < n - 1) workers_.emplace_back([this] { loop(); });
+      task_ = &task;
+      n_ = n;
+      next_ = 1;
+      pending_ = n - 1;
+      ++gen_;
+    }
+    cv_.notify_all();
+    fn(0);
+    std::unique_lock<std::mutex> g(mu_);
+    done_cv_.wait(g, [this] { return pending_ == 0; });
+    task_ = nullptr;
+    return true;
+  }
+
+ private:
+  void loop() {
+    uint64_t seen = 0;
+    std::unique_lock<std::mutex> g(mu_);
+    for (;;) {
+      cv_.wait(g, [&] { return gen_ != seen; });
+      seen = gen_;
+      while (task_ && next_ < n_) {
+        const int t = next_++;
+        const std::function<void(int)>* f = task_;
+        g.unlock();
+        (*f)(t);
+        g.lock();
+        if (--pending_ == 0) done_cv_.notify_one();
+      }
+    }
+  }
+  std::mutex run_mu_, mu_;
+  std::condition_variable cv_, done_cv_;
+  std::vector<std::thread> workers_;
+  const std::function<void(int)>* task_ = nullptr;
+  int n_ = 0, next_ = 0, pending_ = 0;
+  uint64_t gen_ = 0;
+};
+
+CopyPool& copy_pool() {
+  static CopyPool* pool = new CopyPool;  // leaked on purpose: no join at exit
+  return *pool;
 }
 
 // dsts[i] <- srcs[i], bytes[i] each (validated by the caller); threaded above 8 MiB.
@@ -1720,10 +1796,12 @@ void copy_batch(void* const* dsts, const void* const* srcs, const int64_t* bytes
                     static_cast<size_t>(e0 - s0));
     }
   };
-  std::vector<std::thread> pool;
   const int64_t per = (total + threads - 1) / threads;
-  for (int t = 1; t < threads; ++t) pool.emplace_back(copy_range, per * t, per * (t + 1) < total ? per * (t + 1) : total);
-  copy_range(0, per < total ? per : total);
+  auto part = [&](int t) { copy_range(per * t < total ? per * t : total, per * (t + 1) < total ? per * (t + 1) : total); };
+  if (copy_pool().try_run(threads, part)) return;
+  std::vector<std::thread> pool;
+  for (int t = 1; t < threads; ++t) pool.emplace_back(part, t);
+  part(0);
   for (auto& th : pool) th.join();
 }
 
@@ -1977,6 +2055,174 @@ int dla_host_round_finish(int dtype, int n_tensors, const int64_t* numels, const
   return DLA_OK;
 }
 
+namespace {
+bool is_pinned_host(const void* p) {
+  hipPointerAttribute_t a;
+  const bool ok = hipPointerGetAttributes(&a, p) == hipSuccess && a.type == hipMemoryTypeHost;
+  if (!ok) (void)hipGetLastError();
+  return ok;
+}
+bool is_device_mem(const void* p) {
+  hipPointerAttribute_t a;
+  const bool ok = hipPointerGetAttributes(&a, p) == hipSuccess && a.type == hipMemoryTypeDevice;
+  if (!ok) (void)hipGetLastError();
+  return ok;
+}
+struct Events {
+  hipEvent_t e[6] = {};
+  hipError_t create() {
+    for (auto& x : e) {
+      const hipError_t r = hipEventCreateWithFlags(&x, hipEventDisableTiming);
+      if (r != hipSuccess) return r;
+    }
+    return hipSuccess;
+  }
+  ~Events() {
+    for (auto x : e)
+      if (x) (void)hipEventDestroy(x);
+  }
+};
+}  // namespace
+
+int dla_host_reduce(int dtype, int n_peers, int n_tensors, const void* const* tensors, const int64_t* numels,
+                    const double* weights, void* const* outs, int64_t chunk_elems, void* h_stage, void* d_stage,
+                    void* h_out, void* d_out, void* stream, void* copy_stream) {
+  g_last_error.clear();
+  const int es = elem_size(dtype);
+  if (es == 0) return fail(DLA_E_INVALID, "dla_host_reduce: unknown dtype");
+  if (n_peers < 1 || n_tensors < 1 || !tensors || !numels || !weights || !outs || !h_stage || !d_stage || !h_out ||
+      !d_out)
+    return fail(DLA_E_INVALID, "dla_host_reduce: need n_peers >= 1, n_tensors >= 1 and every table and buffer");
+  if (chunk_elems < 1 || (chunk_elems * es) % 256)
+    return fail(DLA_E_INVALID, "dla_host_reduce: chunk_elems must be >= 1 and a multiple of 256 bytes");
+  std::vector<int64_t> start(n_tensors + 1, 0);
+  for (int t = 0; t < n_tensors; ++t) {
+    if (numels[t] < 0) return fail(DLA_E_INVALID, "dla_host_reduce: negative numel at " + std::to_string(t));
+    if (numels[t] > 0 && !outs[t]) return fail(DLA_E_INVALID, "dla_host_reduce: null output " + std::to_string(t));
+    start[t + 1] = start[t] + numels[t];
+  }
+  for (int i = 0; i < n_peers * n_tensors; ++i)
+    if (!tensors[i] && numels[i % n_tensors] > 0)
+      return fail(DLA_E_INVALID, "dla_host_reduce: null tensor pointer at " + std::to_string(i));
+  const int64_t total = start[n_tensors];
+  if (total == 0) return DLA_OK;
+  if (!is_pinned_host(h_stage) || !is_pinned_host(h_out))
+    return fail(DLA_E_INVALID, "dla_host_reduce: h_stage / h_out must be page-locked host memory (hipHostMalloc)");
+  if (!is_device_mem(d_stage) || !is_device_mem(d_out))
+    return fail(DLA_E_INVALID, "dla_host_reduce: d_stage / d_out must be device memory");
+  const hipStream_t cs_ = static_cast<hipStream_t>(stream);
+  const hipStream_t xs = static_cast<hipStream_t>(copy_stream);
+  Events ev;  // h2d[2], red[2], d2h[2]
+  hipError_t e = ev.create();
+  if (e != hipSuccess) return fail(static_cast<int>(e), std::string("dla_host_reduce: ") + hipGetErrorString(e));
+  hipEvent_t* h2d = ev.e;
+  hipEvent_t* red = ev.e + 2;
+  hipEvent_t* d2h = ev.e + 4;
+  const int64_t row_bytes = chunk_elems * es;
+  const int64_t buf_bytes = row_bytes * n_peers;
+  const int64_t n_chunks = (total + chunk_elems - 1) / chunk_elems;
+  std::vector<void*> dsts;
+  std::vector<const void*> srcs;
+  std::vector<int64_t> bytes;
+  std::vector<const void*> rows(n_peers);
+  // the tensors overlapping elements [c0, c1) of the flat (parameters()-order) vector
+  auto pieces = [&](int64_t c0, int64_t c1, auto&& emit) {
+    int t = static_cast<int>(std::upper_bound(start.begin(), start.end(), c0) - start.begin()) - 1;
+    for (; t < n_tensors && start[t] < c1; ++t) {
+      const int64_t a = c0 > start[t] ? c0 : start[t], b = c1 < start[t + 1] ? c1 : start[t + 1];
+      if (a < b) emit(t, a, b);
+    }
+  };
+  auto check = [&](hipError_t r, const char* what) {
+    if (r != hipSuccess && e == hipSuccess) {
+      e = r;
+      g_last_error = std::string("dla_host_reduce: ") + what + ": " + hipGetErrorString(r);
+    }
+    return r == hipSuccess;
+  };
+  // chunk c's averaged elements (h_out buffer c & 1) -> the result tensors (fedavg.py:25)
+  auto unpack = [&](int64_t c) {
+    const int buf = static_cast<int>(c & 1);
+    if (!check(hipEventSynchronize(d2h[buf]), "D2H")) return;
+    const int64_t c0 = c * chunk_elems, c1 = c0 + chunk_elems < total ? c0 + chunk_elems : total;
+    dsts.clear(), srcs.clear(), bytes.clear();
+    pieces(c0, c1, [&](int t, int64_t a, int64_t b) {
+      dsts.push_back(static_cast<char*>(outs[t]) + (a - start[t]) * es);
+      srcs.push_back(static_cast<const char*>(h_out) + buf * row_bytes + (a - c0) * es);
+      bytes.push_back((b - a) * es);
+    });
+    copy_batch(dsts.data(), srcs.data(), bytes.data(), static_cast<int>(dsts.size()));
+  };
+  // DLA_HOST_REDUCE_STATS=1: per-call phase times on stderr (host-path tuning)
+  static const bool stats = std::getenv("DLA_HOST_REDUCE_STATS") != nullptr;
+  using clk = std::chrono::steady_clock;
+  double t_wait = 0, t_pack = 0, t_issue = 0, t_unpack = 0;
+  auto secs = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double>(b - a).count(); };
+  const auto t_start = clk::now();
+  for (int64_t c = 0; c < n_chunks && e == hipSuccess; ++c) {
+    const int buf = static_cast<int>(c & 1);
+    const int64_t c0 = c * chunk_elems, c1 = c0 + chunk_elems < total ? c0 + chunk_elems : total;
+    const int64_t m = c1 - c0;
+    const auto t0 = clk::now();
+    char* hs = static_cast<char*>(h_stage) + buf * buf_bytes;
+    char* ds = static_cast<char*>(d_stage) + buf * buf_bytes;
+    char* dout = static_cast<char*>(d_out) + buf * row_bytes;
+    char* hout = static_cast<char*>(h_out) + buf * row_bytes;
+    // pack chunk c of every peer into row k of staging buffer `buf`, once the H2D of chunk c-2 has read it
+    if (c >= 2 && !check(hipEventSynchronize(h2d[buf]), "H2D")) break;
+    const auto t1 = clk::now();
+    dsts.clear(), srcs.clear(), bytes.clear();
+    for (int k = 0; k < n_peers; ++k) {
+      rows[k] = ds + k * row_bytes;
+      pieces(c0, c1, [&](int t, int64_t a, int64_t b) {
+        dsts.push_back(hs + k * row_bytes + (a - c0) * es);
+        srcs.push_back(static_cast<const char*>(tensors[static_cast<size_t>(k) * n_tensors + t]) + (a - start[t]) * es);
+        bytes.push_back((b - a) * es);
+      });
+    }
+    copy_batch(dsts.data(), srcs.data(), bytes.data(), static_cast<int>(dsts.size()));
+    const auto t2 = clk::now();
+    // H2D on the copy stream once the reduce of chunk c-2 is done with d_stage[buf]
+    if (c >= 2 && !check(hipStreamWaitEvent(xs, red[buf], 0), "wait")) break;
+    if (m == chunk_elems) {
+      if (!check(hipMemcpyAsync(ds, hs, buf_bytes, hipMemcpyHostToDevice, xs), "H2D")) break;
+    } else if (!check(hipMemcpy2DAsync(ds, row_bytes, hs, row_bytes, m * es, n_peers, hipMemcpyHostToDevice, xs),
+                      "H2D")) {
+      break;
+    }
+    if (!check(hipEventRecord(h2d[buf], xs), "record")) break;
+    // reduce (list order, fedavg.py:23-25) and D2H on the compute stream
+    if (!check(hipStreamWaitEvent(cs_, h2d[buf], 0), "wait")) break;
+    const int rc = wsum_impl(dtype, rows.data(), weights, n_peers, m, dout, stream, nullptr);
+    if (rc != DLA_OK) {  // wsum_impl set the message; drain the copies still reading the caller's buffers
+      (void)hipStreamSynchronize(cs_);
+      (void)hipStreamSynchronize(xs);
+      return rc;
+    }
+    if (!check(hipEventRecord(red[buf], cs_), "record")) break;
+    if (!check(hipMemcpyAsync(hout, dout, m * es, hipMemcpyDeviceToHost, cs_), "D2H")) break;
+    if (!check(hipEventRecord(d2h[buf], cs_), "record")) break;
+    const auto t3 = clk::now();
+    if (c >= 1) unpack(c - 1);  // overlaps chunk c's H2D
+    const auto t4 = clk::now();
+    t_wait += secs(t0, t1), t_pack += secs(t1, t2), t_issue += secs(t2, t3), t_unpack += secs(t3, t4);
+  }
+  if (e == hipSuccess) unpack(n_chunks - 1);
+  if (stats)
+    std::fprintf(stderr,
+                 "dla_host_reduce: %d peers x %lld elems, %lld chunks of %lld: total %.2f ms, wait-h2d %.2f, "
+                 "pack %.2f (%.1f GB/s), issue %.2f, unpack+wait-d2h %.2f\n",
+                 n_peers, static_cast<long long>(total), static_cast<long long>(n_chunks),
+                 static_cast<long long>(chunk_elems), secs(t_start, clk::now()) * 1e3, t_wait * 1e3, t_pack * 1e3,
+                 t_pack > 0 ? double(total) * es * n_peers / t_pack / 1e9 : 0.0, t_issue * 1e3, t_unpack * 1e3);
+  if (e != hipSuccess) {
+    (void)hipStreamSynchronize(cs_);
+    (void)hipStreamSynchronize(xs);
+    return static_cast<int>(e);
+  }
+  return DLA_OK;
+}
+
 int dla_shard_range(int dtype, int64_t n_elems, int n_shards, int shard, int64_t* start, int64_t* end) {
   g_last_error.clear();
   const int es = elem_size(dtype);
@@ -2029,8 +2275,8 @@ int dla_wsum_slab_tiled(int dtype, const void* base, int64_t tile_elems, int64_t
       cfg && cfg->variant
           ? cfg->variant
           : vec_store_policy(vec_variant(n_peers < kMaxPeersPerPass ? n_peers : kMaxPeersPerPass), n_elems * es);
-  if (variant != 9 && variant != 10 && variant != 12 && variant != 21)
-    return fail(DLA_E_CONFIG, "dla_wsum_slab_tiled: variant must be 0 (auto), 9, 10, 12 or 21");
+  if (variant != 9 && variant != 10 && variant != 12 && !(variant >= 21 && variant <= 24))
+    return fail(DLA_E_CONFIG, "dla_wsum_slab_tiled: variant must be 0 (auto), 9, 10, 12 or 21-24");
   const int64_t stride = slab_rows * tile_elems;
   hipStream_t s = static_cast<hipStream_t>(stream);
   hipError_t e;

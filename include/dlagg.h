@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define DLA_ABI_VERSION 6
+#define DLA_ABI_VERSION 7
 
 /* element dtypes of the peer buffers and of the output */
 #define DLA_F32 0
@@ -224,6 +224,26 @@ int dla_host_round_start(int dtype, int n_peers, int n_tensors, const void* cons
                          const double* weights, void* rows, int64_t pitch_elems, void* result, void* stream);
 int dla_host_round_finish(int dtype, int n_tensors, const int64_t* numels, const void* result, void* const* outs,
                           void* stream);
+
+/* A large round of CPU-resident models in one synchronous call — fedavg.py:20-25 at the reference's
+ * call sites when the models are large (the DFL aggregator's N models, accdfl/dfl/community.py:673;
+ * the simulators' averages, simulations/learning_simulation.py:335) — streamed through the GPU in
+ * element chunks of the flat (parameters()-order) vector.  For chunk c (buffer c & 1):
+ *   1. pack: elements [c*chunk, (c+1)*chunk) of every peer (HOST pointers tensors[k * n_tensors + t],
+ *      numels[t] elements of dtype each) into row k of h_stage[buf] (threaded memcpy);
+ *   2. one H2D DMA of the rows into d_stage[buf] on copy_stream;
+ *   3. the list-order reduce of the rows into d_out[buf] on stream, then a D2H into h_out[buf];
+ *   4. while chunk c+1 is packed and copied in: unpack chunk c into outs[t] (HOST pointers).
+ * Buffers (caller-owned, untouched by anything else during the call):
+ *   h_stage  page-locked host, 2 * n_peers * chunk_elems elements    d_stage device, same size
+ *   h_out    page-locked host, 2 * chunk_elems elements               d_out   device, same size
+ * chunk_elems * sizeof(dtype) must be a multiple of 256 bytes.  stream and copy_stream are streams of
+ * the current device (they may be the same stream).  Returns after every output has been written.
+ * Replaces one DMA per tensor per peer per chunk (14 080 per chunk for 128 google_speech ResNet-34
+ * models of 110 tensors) by one per chunk.  ABI v7. */
+int dla_host_reduce(int dtype, int n_peers, int n_tensors, const void* const* tensors, const int64_t* numels,
+                    const double* weights, void* const* outs, int64_t chunk_elems, void* h_stage, void* d_stage,
+                    void* h_out, void* d_out, void* stream, void* copy_stream);
 
 #ifdef __cplusplus
 }

@@ -4,7 +4,8 @@
  *   gcc -std=c11 -O2 -ffp-contract=off tests/c_abi_demo.c -Iinclude -I/opt/rocm/include \
  *       -D__HIP_PLATFORM_AMD__ -Ldecentralized-learning_amd/lib -ldlagg -L/opt/rocm/lib -lamdhip64 -o c_abi_demo
  * Runs FedAvg (dla_wsum, a dla_plan with changed weights, the bucket-sharded dla_wsum_sharded and
- * the tile-interleaved dla_wsum_slab_tiled, host-resident peers through dla_host_round_*) and the
+ * the tile-interleaved dla_wsum_slab_tiled, host-resident peers through dla_host_round_* and the
+ * chunked dla_host_reduce) and the
  * teacher-logit mean (dla_mean) on N peers and checks every element bit-for-bit against the reference's
  * sequential arithmetic written out in C (fedavg.py:21-25).  Exit status 0 = all equal.
  */
@@ -201,7 +202,53 @@ int main(void) {
     CHECK_HIP(hipHostFree(result));
   }
 
-  /* 7. errors come back as codes with a message */
+  /* 7. a large round of host peers streamed in chunks (dla_host_reduce): the same two tensors per
+   *    peer, 8 192-element chunks (the last one partial), two streams */
+  {
+    const int64_t split = 4099, numels[2] = {split, P - split}, chunk = 8192;
+    const void* tensors[2 * N];
+    void *h_stage, *d_stage, *h_out, *d_out2;
+    void* outs_host[2] = {out_host, out_host + split};
+    hipStream_t st, cst;
+    for (int k = 0; k < N; ++k) {
+      tensors[2 * k] = host[k];
+      tensors[2 * k + 1] = host[k] + split;
+    }
+    CHECK_HIP(hipStreamCreate(&st));
+    CHECK_HIP(hipStreamCreate(&cst));
+    CHECK_HIP(hipHostMalloc(&h_stage, sizeof(float) * (size_t)(2 * N * chunk), hipHostMallocDefault));
+    CHECK_HIP(hipHostMalloc(&h_out, sizeof(float) * (size_t)(2 * chunk), hipHostMallocDefault));
+    CHECK_HIP(hipMalloc(&d_stage, sizeof(float) * (size_t)(2 * N * chunk)));
+    CHECK_HIP(hipMalloc(&d_out2, sizeof(float) * (size_t)(2 * chunk)));
+    memset(out_host, 0xff, sizeof(float) * P);
+    CHECK_DLA(dla_host_reduce(DLA_F32, N, 2, tensors, numels, w, outs_host, chunk, h_stage, d_stage, h_out, d_out2,
+                              st, cst));
+    for (int64_t j = 0; j < P; ++j) {
+      volatile float acc = host[0][j] * 0.0f;
+      for (int k = 0; k < N; ++k) {
+        volatile float prod = (float)w[k] * host[k][j];
+        acc = acc + prod;
+      }
+      if (!same_f32(acc, out_host[j])) {
+        fprintf(stderr, "dla_host_reduce mismatch at %lld\n", (long long)j);
+        return 1;
+      }
+    }
+    /* a pageable staging buffer is refused before any copy */
+    if (dla_host_reduce(DLA_F32, N, 2, tensors, numels, w, outs_host, chunk, out_host, d_stage, h_out, d_out2, st,
+                        cst) != DLA_E_INVALID) {
+      fprintf(stderr, "expected DLA_E_INVALID for a pageable h_stage\n");
+      return 1;
+    }
+    CHECK_HIP(hipHostFree(h_stage));
+    CHECK_HIP(hipHostFree(h_out));
+    CHECK_HIP(hipFree(d_stage));
+    CHECK_HIP(hipFree(d_out2));
+    CHECK_HIP(hipStreamDestroy(st));
+    CHECK_HIP(hipStreamDestroy(cst));
+  }
+
+  /* 8. errors come back as codes with a message */
   if (dla_wsum(DLA_F32, (const void* const*)dev, w, 0, P, dev_out, NULL) != DLA_E_INVALID ||
       strlen(dla_last_error()) == 0) {
     fprintf(stderr, "expected DLA_E_INVALID for n_peers = 0\n");
@@ -214,7 +261,8 @@ int main(void) {
   }
   CHECK_HIP(hipFree(dev_out));
   free(out_host);
-  printf("c_abi_demo ok: dla_wsum, dla_plan, dla_mean, dla_wsum_sharded, dla_wsum_slab_tiled, dla_host_round "
+  printf("c_abi_demo ok: dla_wsum, dla_plan, dla_mean, dla_wsum_sharded, dla_wsum_slab_tiled, dla_host_round, "
+         "dla_host_reduce "
          "bit-exact on %d peers "
          "x %lld fp32\n", N, (long long)P);
   return 0;

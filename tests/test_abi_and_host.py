@@ -59,7 +59,7 @@ def test_library_version_and_argument_errors(lib_path):
     from accdfl_amd import _lib
 
     L = _lib.lib()
-    assert L.so.dla_version() == 6
+    assert L.so.dla_version() == 7
     assert L.build_id == _lib.source_build_id() == _lib.file_build_id(lib_path)
     assert L.max_peers_per_pass == 128
     # kernel selection by shape (host-only query): north star, configs[3] share, configs[4] share,
@@ -156,6 +156,33 @@ def test_host_round_argument_errors(lib_path):
         _lib.host_round_start(0, 2, ptrs, [10], [0.5, 0.5], rows.ctypes.data + 4, 64, res.ctypes.data, 0)
     with pytest.raises(_lib.DlaggError, match="bad tensor"):
         _lib.host_round_finish(0, [10], res.ctypes.data, [0], 0)
+
+
+def test_host_reduce_argument_errors(lib_path):
+    """dla_host_reduce refuses bad chunk sizes, tables, dtypes and pageable staging before any copy."""
+    import numpy as np
+
+    from accdfl_amd import _lib
+
+    st = np.zeros(4 * 64, dtype=np.float32)
+    a = np.ones(10, dtype=np.float32)
+    out = np.zeros(10, dtype=np.float32)
+    ptrs = [a.ctypes.data, a.ctypes.data]
+    buf = st.ctypes.data
+
+    def call(dtype=0, chunk=64, tensors=ptrs, outs=(out.ctypes.data,), h_stage=buf):
+        _lib.host_reduce(dtype, 2, tensors, [10], [0.5, 0.5], list(outs), chunk, h_stage, buf, buf, buf, 0, 0)
+
+    with pytest.raises(_lib.DlaggError, match="256 bytes"):
+        call(chunk=10)
+    with pytest.raises(_lib.DlaggError, match="dtype"):
+        call(dtype=9)
+    with pytest.raises(_lib.DlaggError, match="null tensor"):
+        call(tensors=[a.ctypes.data, 0])
+    with pytest.raises(_lib.DlaggError, match="null output"):
+        call(outs=(0,))
+    with pytest.raises(_lib.DlaggError, match="page-locked"):
+        call()
 
 
 class _OddModule(nn.Module):

@@ -456,12 +456,13 @@ def test_device_model_manager_never_averages_stale_rows():
         assert same_bits(p.detach().numpy(), q, "f32")
 
 
-@pytest.mark.parametrize("threads", [True, False])
+@pytest.mark.parametrize("mode", ["native", "pipelined", "packed"])
 @pytest.mark.parametrize("dtype", ["f32", "bf16"])
-def test_host_path_sharded_over_devices(dtype, threads):
+def test_host_path_sharded_over_devices(dtype, mode):
     """CPU models bucket-sharded over several devices (here three shards on cuda:0: the
     same code path as three GPUs) — buckets cut through parameter tensors, result bit-exact,
-    with one host thread per GPU and with the serial peer-major issue."""
+    through dla_host_reduce (one host thread per GPU), the per-tensor pipelined copies and the
+    serial peer-major issue."""
     from torch import nn
 
     from accdfl_amd.core.gradient_aggregation import fedavg as fa
@@ -474,15 +475,51 @@ def test_host_path_sharded_over_devices(dtype, threads):
         models.append(m)
     w = [0.3, 0.1, 0.2, 0.25, 0.15]
     fa.set_host_devices(["cuda:0", "cuda:0", "cuda:0"])
-    fa.set_shard_threads(threads)
+    fa.set_host_path(mode)
     try:
         out = fa.FedAvg.aggregate(models, w)
     finally:
         fa.set_host_devices([])
-        fa.set_shard_threads(True)
+        fa.set_host_path("native")
     for i, p in enumerate(out.parameters()):
         want = fedavg_bits([gc.as_float(_bits(m[i].detach().reshape(-1), dtype), dtype) for m in models], w, dtype)
         assert same_bits(gc.as_float(_bits(p.detach().reshape(-1), dtype), dtype), want, dtype), i
+
+
+@pytest.mark.parametrize("chunk_bytes", [1 << 16, 1 << 20, 32 << 20])
+@pytest.mark.parametrize("pinned", [False, True])
+@pytest.mark.parametrize("dtype", ["f32", "bf16", "f16", "f64"])
+def test_native_host_reduce_chunks(dtype, pinned, chunk_bytes):
+    """dla_host_reduce (the default path for large rounds of CPU models): chunk boundaries that cut
+    through tensors, a last partial chunk (2-D H2D), tensors smaller than a chunk and spanning many,
+    pageable and page-locked peers, 11 peers; bit-exact, buffers copied from models[0]."""
+    from torch import nn
+
+    from accdfl_amd.core.gradient_aggregation import fedavg as fa
+
+    shapes = [(700_001,), (3, 333_333), (5,), (1_200_000,), (64, 3, 3, 3), (77,)]
+    g = torch.Generator().manual_seed(47)
+    models = []
+    for k in range(11):
+        m = nn.ParameterList([nn.Parameter((torch.randn(s, generator=g) * 0.05).to(TDT[dtype])) for s in shapes])
+        if pinned:
+            for p in m:
+                p.data = p.data.pin_memory()
+        m.register_buffer("running_mean", torch.full((7,), float(k)))
+        models.append(m)
+    w = [float(x) for x in np.random.default_rng(11).dirichlet(np.ones(11))]
+    old = fa._NATIVE_CHUNK_BYTES
+    fa._NATIVE_CHUNK_BYTES = chunk_bytes
+    try:
+        assert fa.host_path() == "native"
+        out = fa.FedAvg.aggregate(models, w)
+    finally:
+        fa._NATIVE_CHUNK_BYTES = old
+        fa.release_staging()
+    for i, p in enumerate(out.parameters()):
+        want = fedavg_bits([gc.as_float(_bits(m[i].detach().reshape(-1), dtype), dtype) for m in models], w, dtype)
+        assert same_bits(gc.as_float(_bits(p.detach().reshape(-1), dtype), dtype), want, dtype), i
+    assert torch.equal(out.running_mean, models[0].running_mean)
 
 
 def _seq_mean(arrs, dtype):
