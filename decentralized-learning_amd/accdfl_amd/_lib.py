@@ -190,7 +190,8 @@ class _Lib:
         so.dla_host_round_finish.restype = ctypes.c_int
         so.dla_host_reduce.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(vp),
                                        ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_double),
-                                       ctypes.POINTER(vp), ctypes.c_int64, vp, vp, vp, vp, vp, vp]
+                                       ctypes.POINTER(vp), ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, vp, vp,
+                                       vp, vp, vp, vp]
         so.dla_host_reduce.restype = ctypes.c_int
         so.dla_plan_destroy.argtypes = [vp]
         so.dla_plan_destroy.restype = None
@@ -321,17 +322,21 @@ def host_round_start(dtype_code: int, n_peers: int, tensor_ptrs: Sequence[int], 
         L.check(rc, "dla_host_round_start")
 
 
-def host_reduce(dtype_code: int, n_peers: int, tensor_ptrs: Sequence[int], numels, weights: Sequence[float],
-                out_ptrs: Sequence[int], chunk_elems: int, h_stage: int, d_stage: int, h_out: int, d_out: int,
+def host_reduce(dtype_code: int, n_peers: int, tensor_ptrs, numels, weights: Sequence[float], out_ptrs,
+                begin: int, end: int, chunk_elems: int, h_stage: int, d_stage: int, h_out: int, d_out: int,
                 stream_ptr: int, copy_stream_ptr: int) -> None:
-    """dla_host_reduce: a large round of host tensors through the GPU in packed chunks (synchronous).
-    ``tensor_ptrs``: peer-major, n_peers * len(numels) host pointers; ``out_ptrs``: one per tensor."""
+    """dla_host_reduce: flat elements [begin, end) of a round of host tensors through the GPU in packed
+    chunks (synchronous).  ``tensor_ptrs``: peer-major, n_peers * len(numels) host pointers;
+    ``out_ptrs``: one per tensor.  Sequences or ctypes arrays (reused across the buckets of a round)."""
     L = lib()
     if not isinstance(numels, ctypes.Array):
         numels = (ctypes.c_int64 * len(numels))(*numels)
-    rc = L.so.dla_host_reduce(dtype_code, n_peers, len(numels), (ctypes.c_void_p * len(tensor_ptrs))(*tensor_ptrs),
-                              numels, _dbl_array(weights), (ctypes.c_void_p * len(out_ptrs))(*out_ptrs), chunk_elems,
-                              h_stage, d_stage, h_out, d_out, stream_ptr, copy_stream_ptr)
+    if not isinstance(tensor_ptrs, ctypes.Array):
+        tensor_ptrs = (ctypes.c_void_p * len(tensor_ptrs))(*tensor_ptrs)
+    if not isinstance(out_ptrs, ctypes.Array):
+        out_ptrs = (ctypes.c_void_p * len(out_ptrs))(*out_ptrs)
+    rc = L.so.dla_host_reduce(dtype_code, n_peers, len(numels), tensor_ptrs, numels, _dbl_array(weights), out_ptrs,
+                              begin, end, chunk_elems, h_stage, d_stage, h_out, d_out, stream_ptr, copy_stream_ptr)
     if rc != 0:
         L.check(rc, "dla_host_reduce")
 

@@ -230,34 +230,44 @@ def _reduce_host_small(device, dtype, center: List[torch.Tensor], peers: List[Li
         _lib.host_round_finish(code, hr.numels_arr, hr.h_out.data_ptr(), [c.data_ptr() for c in center], stream)
 
 
-def _small_round(models: List[nn.Module], weights) -> "nn.Module | None":
-    """The whole aggregate for a small round of same-layout, one-dtype, contiguous CPU
-    models (the reference's call sites: GL merges N=2 every round): one native call packs
-    every peer into page-locked rows and enqueues the reduce, which reads the rows and writes
-    the page-locked result across PCIe (no staging DMA, dla_host_round_start); the result
-    module is built on the host while it runs, then one call waits and unpacks into its
-    parameters (dla_host_round_finish).  None when the round does not qualify (the general
-    path handles it)."""
-    peers = [list(m.parameters()) for m in models]
-    p0 = peers[0]
+def _host_layout(models: List[nn.Module]):
+    """(dtype, numels, pointers) of a round whose models all have models[0]'s parameter shapes, one
+    supported dtype and contiguous CPU storage — the models at every reference call site — with the
+    parameters' host pointers peer-major, gathered in one pass without a tensor view per parameter
+    (a round of 128 ResNet-34 models has 14 080 parameters: a detach + reshape + slice of each costs
+    more than the GPU work); None when the round does not qualify (the general path handles it)."""
+    p0 = list(models[0].parameters())
     if not p0 or not torch.cuda.is_available():
         return None
     dtype = p0[0].dtype
     if dtype not in _wsum.SUPPORTED_DTYPES:
         return None
-    layout = [p.shape for p in p0]
+    shapes = [p.shape for p in p0]
+    n_t = len(shapes)
     ptrs = []
-    for pl in peers:
-        if len(pl) != len(layout):
+    add = ptrs.append
+    for m in models:
+        ps = list(m.parameters())
+        if len(ps) != n_t:
             return None
-        for p, shape in zip(pl, layout):
-            if p.shape != shape or p.dtype != dtype or p.device.type != "cpu" or not p.is_contiguous():
+        for p, shape in zip(ps, shapes):
+            if p.shape != shape or p.dtype is not dtype or not p.is_cpu or not p.is_contiguous():
                 return None
-            ptrs.append(p.data_ptr())
-    numels = [p.numel() for p in p0]
+            add(p.data_ptr())
+    return dtype, [p.numel() for p in p0], ptrs
+
+
+def _small_round(models: List[nn.Module], weights, layout) -> "nn.Module | None":
+    """The whole aggregate for a small round of same-layout, one-dtype, contiguous CPU
+    models (the reference's call sites: GL merges N=2 every round): one native call packs
+    every peer into page-locked rows and enqueues the reduce, which reads the rows and writes
+    the page-locked result across PCIe (no staging DMA, dla_host_round_start); the result
+    module is built on the host while it runs, then one call waits and unpacks into its
+    parameters (dla_host_round_finish).  None when the round is not small."""
+    dtype, numels, ptrs = layout
     total = sum(numels)
-    esize = p0[0].element_size()
-    n = len(peers)
+    esize = torch.empty((), dtype=dtype).element_size()
+    n = len(models)
     if not _is_small(n, total * esize):
         return None
     device = _wsum.require_device(None)
@@ -274,6 +284,56 @@ def _small_round(models: List[nn.Module], weights) -> "nn.Module | None":
             torch.cuda.current_stream(device).synchronize()
             return None
         _lib.host_round_finish(code, hr.numels_arr, hr.h_out.data_ptr(), [c.data_ptr() for c in params], stream)
+    return center
+
+
+def _large_round(models: List[nn.Module], weights, layout) -> "nn.Module | None":
+    """A large round of same-layout CPU models through dla_host_reduce from the pointer table of
+    _host_layout: every GPU of the host path (set_host_devices) streams its parameter bucket in
+    packed chunks (one DMA per chunk), one host thread per GPU; the averaged elements land in the
+    result's parameters.  None when the result's parameters are not dense CPU tensors."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from accdfl_amd.core.sharding import bucket_bounds
+
+    dtype, numels, ptrs = layout
+    n = len(models)
+    esize = torch.empty((), dtype=dtype).element_size()
+    total = sum(numels)
+    align = _ALIGN_BYTES // esize
+    device = _wsum.require_device(None)
+    devices = _devices_for(device)
+    devices = devices[:max(1, min(len(devices), (total * esize) // _MIN_SHARD_BYTES))]
+    center = _center_copy(models[0], large=n * total * esize >= _SMALL_ROUND_BYTES)
+    params = list(center.parameters())
+    if len(params) != len(numels) or not all(c.is_cpu and c.is_contiguous() for c in params):
+        return None
+    code = _wsum.dtype_code(dtype)
+    tensor_arr = (ctypes.c_void_p * len(ptrs))(*ptrs)
+    numel_arr = (ctypes.c_int64 * len(numels))(*numels)
+    out_arr = (ctypes.c_void_p * len(params))(*[c.data_ptr() for c in params])
+    with _staging_lock:
+        jobs = []
+        for i, (dev, (s, e)) in enumerate(zip(devices, bucket_bounds(total, len(devices), align))):
+            if s < e:
+                chunk = _native_chunk(n, esize, e - s, align)
+                jobs.append((_get_native_staging(dev, dtype, i if len(devices) > 1 else -1, n, chunk), dev, s, e,
+                             chunk))
+
+        def bucket(job):
+            st, dev, s, e, chunk = job
+            compute = torch.cuda.current_stream(dev)
+            st.copy_stream.wait_stream(compute)  # earlier users of the device staging are done
+            with torch.cuda.device(dev):
+                _lib.host_reduce(code, n, tensor_arr, numel_arr, weights, out_arr, s, e, chunk, st.h_stage.data_ptr(),
+                                 st.d_stage.data_ptr(), st.h_out.data_ptr(), st.d_out.data_ptr(),
+                                 compute.cuda_stream, st.copy_stream.cuda_stream)
+
+        if len(jobs) == 1:
+            bucket(jobs[0])
+        else:
+            with ThreadPoolExecutor(max_workers=len(jobs)) as pool:
+                list(pool.map(bucket, jobs))  # re-raises the first failure
     return center
 
 
@@ -405,9 +465,9 @@ def _bucket_native(st: _NativeStaging, dev, flats: List[List[torch.Tensor]], num
     compute = torch.cuda.current_stream(dev)
     st.copy_stream.wait_stream(compute)  # earlier users of the device staging are done
     with torch.cuda.device(dev):
-        _lib.host_reduce(_wsum.dtype_code(dtype), n, ptrs, sizes, weights, [o.data_ptr() for o in outs], chunk,
-                         st.h_stage.data_ptr(), st.d_stage.data_ptr(), st.h_out.data_ptr(), st.d_out.data_ptr(),
-                         compute.cuda_stream, st.copy_stream.cuda_stream)
+        _lib.host_reduce(_wsum.dtype_code(dtype), n, ptrs, sizes, weights, [o.data_ptr() for o in outs], 0, e - s,
+                         chunk, st.h_stage.data_ptr(), st.d_stage.data_ptr(), st.h_out.data_ptr(),
+                         st.d_out.data_ptr(), compute.cuda_stream, st.copy_stream.cuda_stream)
 
 
 # How the host-staged path moves a large round (ACCDFL_AMD_HOST_PATH):
@@ -681,9 +741,13 @@ class FedAvg(GradientAggregation):
 
         with torch.no_grad():
             if len(models) > 0:
-                small = _small_round(models, list(weights))
-                if small is not None:
-                    return small
+                layout = _host_layout(models)
+                if layout is not None:
+                    done = _small_round(models, list(weights), layout)
+                    if done is None and _HOST_PATH == "native":
+                        done = _large_round(models, list(weights), layout)
+                    if done is not None:
+                        return done
             params0 = list(models[0].parameters())
             nbytes = sum(p.numel() * p.element_size() for p in params0) * len(models)
             center_model = _center_copy(models[0], large=nbytes >= _SMALL_ROUND_BYTES)

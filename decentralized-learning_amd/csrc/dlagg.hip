@@ -2085,8 +2085,8 @@ struct Events {
 }  // namespace
 
 int dla_host_reduce(int dtype, int n_peers, int n_tensors, const void* const* tensors, const int64_t* numels,
-                    const double* weights, void* const* outs, int64_t chunk_elems, void* h_stage, void* d_stage,
-                    void* h_out, void* d_out, void* stream, void* copy_stream) {
+                    const double* weights, void* const* outs, int64_t begin, int64_t end, int64_t chunk_elems,
+                    void* h_stage, void* d_stage, void* h_out, void* d_out, void* stream, void* copy_stream) {
   g_last_error.clear();
   const int es = elem_size(dtype);
   if (es == 0) return fail(DLA_E_INVALID, "dla_host_reduce: unknown dtype");
@@ -2105,7 +2105,9 @@ int dla_host_reduce(int dtype, int n_peers, int n_tensors, const void* const* te
     if (!tensors[i] && numels[i % n_tensors] > 0)
       return fail(DLA_E_INVALID, "dla_host_reduce: null tensor pointer at " + std::to_string(i));
   const int64_t total = start[n_tensors];
-  if (total == 0) return DLA_OK;
+  if (begin < 0 || end < begin || end > total)
+    return fail(DLA_E_INVALID, "dla_host_reduce: need 0 <= begin <= end <= sum(numels)");
+  if (end == begin) return DLA_OK;
   if (!is_pinned_host(h_stage) || !is_pinned_host(h_out))
     return fail(DLA_E_INVALID, "dla_host_reduce: h_stage / h_out must be page-locked host memory (hipHostMalloc)");
   if (!is_device_mem(d_stage) || !is_device_mem(d_out))
@@ -2120,7 +2122,7 @@ int dla_host_reduce(int dtype, int n_peers, int n_tensors, const void* const* te
   hipEvent_t* d2h = ev.e + 4;
   const int64_t row_bytes = chunk_elems * es;
   const int64_t buf_bytes = row_bytes * n_peers;
-  const int64_t n_chunks = (total + chunk_elems - 1) / chunk_elems;
+  const int64_t n_chunks = (end - begin + chunk_elems - 1) / chunk_elems;
   std::vector<void*> dsts;
   std::vector<const void*> srcs;
   std::vector<int64_t> bytes;
@@ -2144,7 +2146,7 @@ int dla_host_reduce(int dtype, int n_peers, int n_tensors, const void* const* te
   auto unpack = [&](int64_t c) {
     const int buf = static_cast<int>(c & 1);
     if (!check(hipEventSynchronize(d2h[buf]), "D2H")) return;
-    const int64_t c0 = c * chunk_elems, c1 = c0 + chunk_elems < total ? c0 + chunk_elems : total;
+    const int64_t c0 = begin + c * chunk_elems, c1 = c0 + chunk_elems < end ? c0 + chunk_elems : end;
     dsts.clear(), srcs.clear(), bytes.clear();
     pieces(c0, c1, [&](int t, int64_t a, int64_t b) {
       dsts.push_back(static_cast<char*>(outs[t]) + (a - start[t]) * es);
@@ -2161,7 +2163,7 @@ int dla_host_reduce(int dtype, int n_peers, int n_tensors, const void* const* te
   const auto t_start = clk::now();
   for (int64_t c = 0; c < n_chunks && e == hipSuccess; ++c) {
     const int buf = static_cast<int>(c & 1);
-    const int64_t c0 = c * chunk_elems, c1 = c0 + chunk_elems < total ? c0 + chunk_elems : total;
+    const int64_t c0 = begin + c * chunk_elems, c1 = c0 + chunk_elems < end ? c0 + chunk_elems : end;
     const int64_t m = c1 - c0;
     const auto t0 = clk::now();
     char* hs = static_cast<char*>(h_stage) + buf * buf_bytes;
@@ -2212,9 +2214,9 @@ int dla_host_reduce(int dtype, int n_peers, int n_tensors, const void* const* te
     std::fprintf(stderr,
                  "dla_host_reduce: %d peers x %lld elems, %lld chunks of %lld: total %.2f ms, wait-h2d %.2f, "
                  "pack %.2f (%.1f GB/s), issue %.2f, unpack+wait-d2h %.2f\n",
-                 n_peers, static_cast<long long>(total), static_cast<long long>(n_chunks),
+                 n_peers, static_cast<long long>(end - begin), static_cast<long long>(n_chunks),
                  static_cast<long long>(chunk_elems), secs(t_start, clk::now()) * 1e3, t_wait * 1e3, t_pack * 1e3,
-                 t_pack > 0 ? double(total) * es * n_peers / t_pack / 1e9 : 0.0, t_issue * 1e3, t_unpack * 1e3);
+                 t_pack > 0 ? double(end - begin) * es * n_peers / t_pack / 1e9 : 0.0, t_issue * 1e3, t_unpack * 1e3);
   if (e != hipSuccess) {
     (void)hipStreamSynchronize(cs_);
     (void)hipStreamSynchronize(xs);

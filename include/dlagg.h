@@ -228,8 +228,10 @@ int dla_host_round_finish(int dtype, int n_tensors, const int64_t* numels, const
 /* A large round of CPU-resident models in one synchronous call — fedavg.py:20-25 at the reference's
  * call sites when the models are large (the DFL aggregator's N models, accdfl/dfl/community.py:673;
  * the simulators' averages, simulations/learning_simulation.py:335) — streamed through the GPU in
- * element chunks of the flat (parameters()-order) vector.  For chunk c (buffer c & 1):
- *   1. pack: elements [c*chunk, (c+1)*chunk) of every peer (HOST pointers tensors[k * n_tensors + t],
+ * element chunks of the flat (parameters()-order) vector.  Only the flat elements [begin, end) are
+ * reduced and written (one bucket per GPU when the round is sharded over several GPUs: one call per
+ * GPU, each from its own host thread, with that GPU current).  For chunk c (buffer c & 1):
+ *   1. pack: elements [begin + c*chunk, begin + (c+1)*chunk) of every peer (HOST pointers tensors[k * n_tensors + t],
  *      numels[t] elements of dtype each) into row k of h_stage[buf] (threaded memcpy);
  *   2. one H2D DMA of the rows into d_stage[buf] on copy_stream;
  *   3. the list-order reduce of the rows into d_out[buf] on stream, then a D2H into h_out[buf];
@@ -242,8 +244,8 @@ int dla_host_round_finish(int dtype, int n_tensors, const int64_t* numels, const
  * Replaces one DMA per tensor per peer per chunk (14 080 per chunk for 128 google_speech ResNet-34
  * models of 110 tensors) by one per chunk.  ABI v7. */
 int dla_host_reduce(int dtype, int n_peers, int n_tensors, const void* const* tensors, const int64_t* numels,
-                    const double* weights, void* const* outs, int64_t chunk_elems, void* h_stage, void* d_stage,
-                    void* h_out, void* d_out, void* stream, void* copy_stream);
+                    const double* weights, void* const* outs, int64_t begin, int64_t end, int64_t chunk_elems,
+                    void* h_stage, void* d_stage, void* h_out, void* d_out, void* stream, void* copy_stream);
 
 #ifdef __cplusplus
 }

@@ -221,8 +221,11 @@ int main(void) {
     CHECK_HIP(hipMalloc(&d_stage, sizeof(float) * (size_t)(2 * N * chunk)));
     CHECK_HIP(hipMalloc(&d_out2, sizeof(float) * (size_t)(2 * chunk)));
     memset(out_host, 0xff, sizeof(float) * P);
-    CHECK_DLA(dla_host_reduce(DLA_F32, N, 2, tensors, numels, w, outs_host, chunk, h_stage, d_stage, h_out, d_out2,
-                              st, cst));
+    /* in two calls over [0, 300 007) and [300 007, P): the buckets of a round sharded over two GPUs */
+    CHECK_DLA(dla_host_reduce(DLA_F32, N, 2, tensors, numels, w, outs_host, 0, 300007, chunk, h_stage, d_stage,
+                              h_out, d_out2, st, cst));
+    CHECK_DLA(dla_host_reduce(DLA_F32, N, 2, tensors, numels, w, outs_host, 300007, P, chunk, h_stage, d_stage,
+                              h_out, d_out2, st, cst));
     for (int64_t j = 0; j < P; ++j) {
       volatile float acc = host[0][j] * 0.0f;
       for (int k = 0; k < N; ++k) {
@@ -235,8 +238,8 @@ int main(void) {
       }
     }
     /* a pageable staging buffer is refused before any copy */
-    if (dla_host_reduce(DLA_F32, N, 2, tensors, numels, w, outs_host, chunk, out_host, d_stage, h_out, d_out2, st,
-                        cst) != DLA_E_INVALID) {
+    if (dla_host_reduce(DLA_F32, N, 2, tensors, numels, w, outs_host, 0, P, chunk, out_host, d_stage, h_out, d_out2,
+                        st, cst) != DLA_E_INVALID) {
       fprintf(stderr, "expected DLA_E_INVALID for a pageable h_stage\n");
       return 1;
     }

@@ -170,8 +170,9 @@ def test_host_reduce_argument_errors(lib_path):
     ptrs = [a.ctypes.data, a.ctypes.data]
     buf = st.ctypes.data
 
-    def call(dtype=0, chunk=64, tensors=ptrs, outs=(out.ctypes.data,), h_stage=buf):
-        _lib.host_reduce(dtype, 2, tensors, [10], [0.5, 0.5], list(outs), chunk, h_stage, buf, buf, buf, 0, 0)
+    def call(dtype=0, chunk=64, tensors=ptrs, outs=(out.ctypes.data,), h_stage=buf, begin=0, end=10):
+        _lib.host_reduce(dtype, 2, tensors, [10], [0.5, 0.5], list(outs), begin, end, chunk, h_stage, buf, buf, buf,
+                         0, 0)
 
     with pytest.raises(_lib.DlaggError, match="256 bytes"):
         call(chunk=10)
@@ -181,6 +182,10 @@ def test_host_reduce_argument_errors(lib_path):
         call(tensors=[a.ctypes.data, 0])
     with pytest.raises(_lib.DlaggError, match="null output"):
         call(outs=(0,))
+    with pytest.raises(_lib.DlaggError, match="begin"):
+        call(begin=4, end=11)
+    with pytest.raises(_lib.DlaggError, match="begin"):
+        call(begin=5, end=4)
     with pytest.raises(_lib.DlaggError, match="page-locked"):
         call()
 
