@@ -37,10 +37,15 @@ Extra objects on the JSON line:
   host_inclusive, host_inclusive_small, wire_ingress, dfl_round  (N = 1) FedAvg.aggregate on
                 CPU modules (PCIe-inclusive), the GNLeNet small rounds, one peer's wire bytes
                 into HBM, one DFL round from EVA blocks to outgoing bytes
+  host_inclusive_configs  (N = 1) every GPU config's whole model as CPU modules with the reference's
+                real layout (tests/golden/layouts.json) through FedAvg.aggregate, pageable and
+                page-locked peers
   cpu_baseline  (N = 1, rank 0) the reference's torch-CPU op sequence (oracle/fedavg_oracle.py,
-                kind "port") on this host's CPU share, bounded sample; every other CPU
-                comparison (per config, GNLeNet rounds, the reference-style DFL round) is
-                timed in this leg too, the only one that runs the oracle port
+                kind "port") on this host's CPU share, bounded sample, product temporary held
+                (value), and the literal sequence in a fresh process (cold_fresh_process); every
+                other CPU comparison (per config, the config layouts, GNLeNet rounds, the
+                reference-style DFL round) is timed in this leg too, the only one that runs the
+                oracle port
 """
 from __future__ import annotations
 
@@ -113,6 +118,8 @@ def parse():
                          "(what the CPU test of the multi-rank launch runs)")
     ap.add_argument("--sweep", action="store_true", help="interleaved A/B of launch variants, then exit")
     ap.add_argument("--host-breakdown", action="store_true", help="time the host-inclusive phases, then exit")
+    ap.add_argument("--no-numa-bind", action="store_true",
+                    help="do not restrict each rank's CPUs to its GPU's NUMA node (host_memory.bind_to_gpu_node)")
     ap.add_argument("--host-configs-only", action="store_true",
                     help="print the per-config host-inclusive table (CPU modules, real layouts), then exit")
     ap.add_argument("--configs-only", action="store_true",
@@ -297,13 +304,52 @@ def _cgroup_cpus():
         return None
 
 
+_COLD_SCRIPT = r"""
+import json, statistics, sys, time
+import numpy as np, torch
+sys.path.insert(0, sys.argv[1])
+from oracle.fedavg_oracle import fedavg_flat_torch
+n, p, th, budget = int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4]), float(sys.argv[5])
+torch.set_num_threads(th)
+gen = torch.Generator().manual_seed(1000)
+peers = [torch.randn(p, generator=gen) * 0.05 for _ in range(n)]
+w = [float(x) for x in np.random.default_rng(0).dirichlet(np.ones(n))]
+out = torch.empty(p)
+fedavg_flat_torch(peers, w, out)
+ts, start = [], time.perf_counter()
+while (time.perf_counter() - start < budget and len(ts) < 50) or len(ts) < 2:
+    t0 = time.perf_counter()
+    fedavg_flat_torch(peers, w, out)
+    ts.append(time.perf_counter() - t0)
+print(json.dumps({"median_ms": statistics.median(ts) * 1e3, "reduces": len(ts)}))
+"""
+
+
+def cpu_baseline_cold(n, p, threads, budget_s):
+    """The literal reference op sequence (a fresh ``w * p`` temporary per peer) in a FRESH
+    process: what a newly started reference process pays, page faults of every temporary
+    included (the in-process figure depends on what the allocator already holds)."""
+    try:
+        r = subprocess.run([sys.executable, "-c", _COLD_SCRIPT, ROOT, str(n), str(p), str(threads), str(budget_s)],
+                           capture_output=True, text=True, timeout=120 + 4 * budget_s,
+                           env=dict(os.environ, OMP_NUM_THREADS=str(threads)))
+        row = json.loads(r.stdout.strip().splitlines()[-1])
+    except (subprocess.SubprocessError, ValueError, IndexError) as exc:
+        return {"error": "%s: %s" % (type(exc).__name__, exc)}
+    return {"GB/s": round((n + 1) * p * 4 / (row["median_ms"] / 1e3) / 1e9, 3),
+            "median_ms": round(row["median_ms"], 1), "reduces": row["reduces"], "threads": threads}
+
+
 def cpu_baseline(n, p, budget_s):
-    """The reference op sequence (deepcopy -> mul_(0) -> add_(w*p)) on torch-CPU, timed on
-    a bounded sample of the same workload: repeated full NS reduces until ~budget_s, at the
+    """The reference op sequence (deepcopy -> mul_(0) -> add_(w*p)) on torch-CPU, timed on a
+    bounded sample of the same workload: repeated full NS reduces until ~budget_s, at the
     process's CPU share (cpu_threads), at every affinity CPU when that differs, and on one
-    thread.  ``value`` / ``cores`` is the fastest of these counts."""
+    thread, with the product temporary in a held buffer (fedavg_flat_torch_warm: same ops,
+    same bits, no page faults — the sequence at its best).  ``value`` / ``cores`` is the
+    fastest of these counts.  ``cold_fresh_process`` times the literal sequence (a fresh
+    temporary per peer) in a new process at the same thread count."""
     sys.path.insert(0, ROOT)
-    from oracle.fedavg_oracle import fedavg_flat_torch  # timed CPU baseline (kind "port")
+    from oracle.fedavg_oracle import fedavg_flat_torch_warm  # timed CPU baseline (kind "port")
 
     share, how = cpu_threads()
     aff = len(os.sched_getaffinity(0))
@@ -311,6 +357,7 @@ def cpu_baseline(n, p, budget_s):
     peers = [torch.randn(p, generator=gen) * 0.05 for _ in range(n)]
     w = [float(x) for x in np.random.default_rng(0).dirichlet(np.ones(n))]
     out = torch.empty(p)
+    tmp = torch.empty(p)
     byts = (n + 1) * p * 4
     quota = _cgroup_cpus()
     # every affinity CPU as well, unless the cgroup quota caps the job below that count (then
@@ -320,13 +367,13 @@ def cpu_baseline(n, p, budget_s):
     per = {}
     for th in counts:
         torch.set_num_threads(th)
-        fedavg_flat_torch(peers, w, out)  # warm-up
+        fedavg_flat_torch_warm(peers, w, out, tmp)  # warm-up
         times = []
         start = time.perf_counter()
         lim = budget_s if th != 1 else budget_s / 2
         while (time.perf_counter() - start < lim and len(times) < 200) or len(times) < 2:
             t0 = time.perf_counter()
-            fedavg_flat_torch(peers, w, out)
+            fedavg_flat_torch_warm(peers, w, out, tmp)
             times.append(time.perf_counter() - t0)
         med = statistics.median(times)
         per[th] = (med, len(times), sum(times))
@@ -334,19 +381,23 @@ def cpu_baseline(n, p, budget_s):
     torch.set_num_threads(share)
     best = min((v[0], th) for th, v in per.items())[1]
     med, cnt, tot = per[best]
+    del peers, out, tmp
+    log("cpu baseline: literal op sequence in a fresh process")
+    cold = cpu_baseline_cold(n, p, share, min(4.0, budget_s))
     return {
         "value": round(byts / med / 1e9, 3),
         "unit": "GB/s",
         "cores": best,
         "kind": "port",
-        "sample": "%d full reduces of %d peers x %d fp32 (torch-CPU op sequence of fedavg.py:20-25) on %d "
-                  "threads, median %.1f ms, %.1f s total" % (cnt, n, p, best, med * 1e3, tot),
+        "sample": "%d full reduces of %d peers x %d fp32 (torch-CPU op sequence of fedavg.py:20-25, product "
+                  "temporary held) on %d threads, median %.1f ms, %.1f s total" % (cnt, n, p, best, med * 1e3, tot),
         "threads_source": how,
         "affinity_cpus": aff,
         "cgroup_cpu_quota": quota,
         "by_threads": {str(th): {"GB/s": round(byts / v[0] / 1e9, 3), "median_ms": round(v[0] * 1e3, 1),
                                  "reduces": v[1]} for th, v in per.items()},
         "value_1thread": round(byts / per[1][0] / 1e9, 3),
+        "cold_fresh_process": cold,
         "cpu": _cpu_model(),
     }
 
@@ -808,12 +859,12 @@ def dfl_round_reference_style(msgs, p, reps=2):
 
 
 def _cpu_port_ms(n, share, dt, budget_s=1.5, max_elems=500_000_000):
-    """The reference op sequence (oracle/fedavg_oracle.py, torch-CPU) on the same share,
+    """The reference op sequence (oracle/fedavg_oracle.py, torch-CPU, product temporary held) on the same share,
     on this host's cores: median ms of a bounded sample, or None above max_elems."""
     if n * share > max_elems:
         return None, 0
     sys.path.insert(0, ROOT)
-    from oracle.fedavg_oracle import fedavg_flat_torch  # timed CPU baseline (kind "port")
+    from oracle.fedavg_oracle import fedavg_flat_torch_warm  # timed CPU baseline (kind "port")
 
     threads = cpu_threads()[0]
     torch.set_num_threads(threads)
@@ -821,12 +872,13 @@ def _cpu_port_ms(n, share, dt, budget_s=1.5, max_elems=500_000_000):
     peers = [(base * (1.0 + 0.01 * k)).to(dt) for k in range(n)]  # values do not change CPU time
     w = [float(1.0 / n)] * n
     out = torch.empty(share, dtype=dt)
-    fedavg_flat_torch(peers, w, out)
+    tmp = torch.empty(share, dtype=dt)
+    fedavg_flat_torch_warm(peers, w, out, tmp)
     ts = []
     start = time.perf_counter()
     while (time.perf_counter() - start < budget_s and len(ts) < 50) or len(ts) < 3:
         t0 = time.perf_counter()
-        fedavg_flat_torch(peers, w, out)
+        fedavg_flat_torch_warm(peers, w, out, tmp)
         ts.append(time.perf_counter() - t0)
     return statistics.median(ts) * 1e3, threads
 
@@ -1197,8 +1249,13 @@ def main():
         return
     from accdfl_amd import _lib
     from accdfl_amd.core import wsum
+    from accdfl_amd.core.host_memory import bind_to_gpu_node
 
     _lib.lib()  # fail loudly here if the HIP library is missing
+    # one process per GPU, bound to the GPU's NUMA node before any host buffer is allocated: the
+    # host-inclusive legs then pack and DMA node-local memory (configs[4] CPU modules: 159-177 ms
+    # unbound, 111-121 bound, profiles/r02zb)
+    numa_node = None if args.no_numa_bind else bind_to_gpu_node(device)
     if args.sweep:
         sweep(args, device)
         return
@@ -1275,7 +1332,7 @@ def main():
             "hbm_layout": ("PeerSlab tile-interleaved slab [n_tiles][%d peers][%d-element tiles]" % (n, inp.tile)
                            if inp.layout == "slab" else "one buffer per peer"),
         },
-        "launch": launch_info(world),
+        "launch": dict(launch_info(world), numa_node_bound=numa_node),
         "roofline": {
             "bound": "hbm",
             "kernel": inp.kernel if cfg is None else "forced launch cfg %s" % (tuple(args_cfg(args)),),

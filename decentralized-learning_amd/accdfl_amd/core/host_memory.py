@@ -118,3 +118,47 @@ def result_tensor(shape, dtype: torch.dtype) -> torch.Tensor:
 
 def pool_free_bytes() -> int:
     return _pool.free_bytes()
+
+
+def gpu_numa_node(device=None):
+    """NUMA node of the HIP device's PCIe root (sysfs), or None when unknown."""
+    if not torch.cuda.is_available():
+        return None
+    props = torch.cuda.get_device_properties(torch.device("cuda", 0) if device is None else device)
+    bus = "%04x:%02x:%02x.0" % (getattr(props, "pci_domain_id", 0), props.pci_bus_id, props.pci_device_id)
+    try:
+        node = int(open("/sys/bus/pci/devices/%s/numa_node" % bus).read())
+    except (OSError, ValueError):
+        return None
+    return node if node >= 0 else None
+
+
+def _cpulist(text: str):
+    cpus = set()
+    for part in text.strip().split(","):
+        if "-" in part:
+            a, b = part.split("-")
+            cpus.update(range(int(a), int(b) + 1))
+        elif part:
+            cpus.add(int(part))
+    return cpus
+
+
+def bind_to_gpu_node(device=None) -> "int | None":
+    """Restrict this process's CPUs to the device's NUMA node (within its current affinity), so the
+    host memory it allocates afterwards — peer models, page-locked staging — is local to the GPU's
+    PCIe root and the staging copies do not cross the socket link: the one-process-per-GPU
+    deployment with NUMA binding (what ``numactl --cpunodebind`` does).  Returns the node, or None
+    when it is unknown or would leave no CPU."""
+    node = gpu_numa_node(device)
+    if node is None:
+        return None
+    try:
+        cpus = _cpulist(open("/sys/devices/system/node/node%d/cpulist" % node).read())
+    except OSError:
+        return None
+    mine = cpus & os.sched_getaffinity(0)
+    if not mine:
+        return None
+    os.sched_setaffinity(0, mine)
+    return node

@@ -147,6 +147,24 @@ def fedavg_flat_torch(peers, weights, out=None):
         return acc
 
 
+def fedavg_flat_torch_warm(peers, weights, out, tmp):
+    """fedavg_flat_torch with the product temporary of ``c1.add_(w * p1)`` (fedavg.py:25) in a
+    caller-held buffer: the same op sequence and bits (``torch.mul(p, w, out=tmp)`` is ``w * p``),
+    without a fresh allocation per peer.  In a fresh process each ``w * p`` of a 25 M model maps and
+    page-faults 100 MB (glibc serves requests above its 32 MB mmap ceiling with a new mapping unless
+    its heap already holds a free region that large), which makes the literal sequence 5-30x
+    slower than its arithmetic; this is the sequence at its best, the stricter CPU baseline."""
+    import torch
+
+    with torch.no_grad():
+        out.copy_(peers[0])
+        out.mul_(0)
+        for p, w in zip(peers, weights):
+            torch.mul(p, w, out=tmp)
+            out.add_(tmp)
+        return out
+
+
 # ------------------------------------------------------------ comparison helper
 def same_bits(a: np.ndarray, b: np.ndarray, dtype: str) -> bool:
     """Bit equality, with every NaN equal to every NaN (payloads are not contract:

@@ -14,8 +14,12 @@ import torch  # noqa: E402
 
 from accdfl_amd.core.gradient_aggregation.fedavg import FedAvg, host_path, release_staging  # noqa: E402
 
+if os.environ.get("PROBE_BIND") == "gpu":
+    from accdfl_amd.core.host_memory import bind_to_gpu_node
+    print(json.dumps({"bound_to_numa_node": bind_to_gpu_node()}), flush=True)
 cfgs = sys.argv[1].split(",") if len(sys.argv) > 1 else ["ns", "configs[3']", "configs[4]"]
-env = {k: os.environ.get(k) for k in ("DLA_COPY_THREADS", "ACCDFL_AMD_HOST_CHUNK_MB", "ACCDFL_AMD_HOST_PATH")}
+env = {k: os.environ.get(k) for k in ("DLA_COPY_THREADS", "ACCDFL_AMD_HOST_CHUNK_MB", "ACCDFL_AMD_HOST_PATH",
+                                      "PROBE_BIND")}
 for c in cfgs:
     if c == "ns":
         row = bench.host_inclusive(8, 25_000_000)

@@ -98,3 +98,20 @@ def test_fma_would_break_parity():
     fma = acc.astype(np.float32)
     assert not np.array_equal(fma.view(np.uint32), want.view(np.uint32))
     assert n == 8
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_timed_flat_ports_match_the_bit_model(dtype):
+    """Both timed CPU baselines (bench.py cpu_baseline: the held-temporary sequence; the fresh-process
+    leg: the literal sequence) compute the reference's bits (fedavg.py:21-25)."""
+    from oracle.fedavg_oracle import fedavg_flat_torch, fedavg_flat_torch_warm
+
+    g = torch.Generator().manual_seed(5)
+    peers = [(torch.randn(100_003, generator=g) * 0.05).to(dtype) for _ in range(7)]
+    w = [float(x) for x in np.random.default_rng(7).dirichlet(np.ones(7))]
+    lit = fedavg_flat_torch(peers, w, torch.empty(100_003, dtype=dtype))
+    warm = fedavg_flat_torch_warm(peers, w, torch.empty(100_003, dtype=dtype), torch.empty(100_003, dtype=dtype))
+    name = "f32" if dtype == torch.float32 else "bf16"
+    want = fedavg_bits([gc.as_float(gc.from_torch(p, name), name) for p in peers], w, name)
+    assert same_bits(gc.from_torch(lit, name), gc.from_torch(warm, name), name)
+    assert same_bits(gc.as_float(gc.from_torch(warm, name), name), want, name)
