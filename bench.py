@@ -1265,6 +1265,8 @@ def main():
     if args.host_configs_only:
         print(json.dumps(dict(config="north star 8 x 25 M f32 (one tensor per peer)",
                               **host_inclusive(args.peers, args.params))), flush=True)
+        print(json.dumps(dict(config="GNLeNet small rounds", numa_node_bound=numa_node, **host_inclusive_small())),
+              flush=True)
         for name, row in host_inclusive_configs().items():
             print(json.dumps(dict(config=name, **row)), flush=True)
         return

@@ -810,11 +810,8 @@ __device__ __attribute__((always_inline)) inline void vec_tail(
 // p[k] + (i >> tshift_v) * tstride_v + (i & (2^tshift_v - 1)); the output stays contiguous.
 // PLAIN_ST: plain (L2 write-back) output stores instead of sc1 — faster when the output is small
 // and many peers are read per element, slower for large outputs (vec_store_policy).
-// BS: threads per workgroup (one lane per vector either way); XCD: remap workgroup ids so each of
-// the 8 XCDs (which take workgroups round-robin) walks one contiguous eighth of the vectors.
-template <int DT, int KMAX, int G, int VW, bool ACC_IN, bool TILED = false, bool PLAIN_ST = false, int BS = 64,
-          bool XCD = false>
-__global__ __launch_bounds__(BS) void wsum_vec_kernel(
+template <int DT, int KMAX, int G, int VW, bool ACC_IN, bool TILED = false, bool PLAIN_ST = false>
+__global__ __launch_bounds__(64) void wsum_vec_kernel(
     const PeerTable<typename Ops<DT>::w_t, KMAX> tab, int n_peers, int64_t n_vecs,
     int64_t n_elems, void* __restrict__ out_v, int tshift_v = 0, int64_t tstride_v = 0, int tshift_e = -1,
     int64_t tstride_e = 0) {
@@ -823,18 +820,13 @@ __global__ __launch_bounds__(BS) void wsum_vec_kernel(
   using acc_t = typename O::acc_t;
   using V = typename VecOf<VW>::T;
   constexpr int WE = O::WE;               // elements per dword
-  const int64_t main_grid = (n_vecs + BS - 1) / BS;
+  const int64_t main_grid = (n_vecs + 63) / 64;
   if (blockIdx.x >= main_grid) {  // the ragged-tail workgroup (< VW * WE elements)
     fold_tail<DT, ACC_IN>(tab.p, tab.w, n_peers, n_vecs * VW * WE, n_elems, out_v, TILED ? tshift_e : -1,
                           tstride_e);
     return;
   }
-  int64_t b = blockIdx.x;
-  if constexpr (XCD) {
-    const int64_t q = main_grid >> 3;
-    if (b < (q << 3)) b = (b & 7) * q + (b >> 3);
-  }
-  const int64_t j = b * BS + threadIdx.x;
+  const int64_t j = static_cast<int64_t>(blockIdx.x) * 64 + threadIdx.x;
   const bool live = j < n_vecs;
   const int64_t i = live ? j : n_vecs - 1;  // clamped: loads stay unpredicated
   const int64_t a = TILED ? (i >> tshift_v) * tstride_v + (i & ((int64_t{1} << tshift_v) - 1)) : i;
@@ -1213,7 +1205,7 @@ hipError_t launch_vec_tiled(const PeerTable<typename Ops<DT>::w_t, KMAX>& tab, i
     return hipErrorInvalidValue;
   } else {
     constexpr int WE = Ops<DT>::WE;
-#define DLA_VECT(G_, VW_, PST_, BS_, XCD_)                                                                          \
+#define DLA_VECT(G_, VW_, PST_)                                                                                     \
   do {                                                                                                        \
     constexpr int G = KMAX < (G_) ? KMAX : (G_);                                                              \
     constexpr int per_vec = (VW_) * WE;                                                                       \
@@ -1221,21 +1213,18 @@ hipError_t launch_vec_tiled(const PeerTable<typename Ops<DT>::w_t, KMAX>& tab, i
     while ((1 << vs) < per_vec) ++vs;                                                                         \
     if (tshift_e < vs) return hipErrorInvalidValue;                                                           \
     const int64_t n_vecs = n_elems / per_vec;                                                                 \
-    int64_t grid = (n_vecs + (BS_) - 1) / (BS_);                                                              \
+    int64_t grid = (n_vecs + 63) / 64;                                                                        \
     if (n_elems > n_vecs * per_vec) ++grid;                                                                   \
     if (grid < 1 || grid > 0x7fffffff) return hipErrorInvalidValue;                                           \
-    hipLaunchKernelGGL((wsum_vec_kernel<DT, KMAX, G, VW_, ACC_IN, true, PST_, BS_, XCD_>),                    \
-                       dim3(static_cast<unsigned>(grid)), dim3(BS_), 0, s, tab, n, n_vecs, n_elems, out,       \
-                       tshift_e - vs, tstride_e / per_vec, tshift_e, tstride_e);                              \
+    hipLaunchKernelGGL((wsum_vec_kernel<DT, KMAX, G, VW_, ACC_IN, true, PST_>), dim3(static_cast<unsigned>(grid)),   \
+                       dim3(64), 0, s, tab, n, n_vecs, n_elems, out, tshift_e - vs, tstride_e / per_vec, tshift_e, \
+                       tstride_e);                                                                            \
   } while (0)
     switch (variant) {
-      case 12: DLA_VECT(16, 2, false, 64, false); break;
-      case 10: DLA_VECT(16, 4, false, 64, false); break;
-      case 21: DLA_VECT(32, 2, true, 64, false); break;
-      case 22: DLA_VECT(32, 2, false, 256, false); break;
-      case 23: DLA_VECT(32, 2, false, 64, true); break;
-      case 24: DLA_VECT(32, 2, false, 256, true); break;
-      default: DLA_VECT(32, 2, false, 64, false); break;
+      case 12: DLA_VECT(16, 2, false); break;
+      case 10: DLA_VECT(16, 4, false); break;
+      case 21: DLA_VECT(32, 2, true); break;
+      default: DLA_VECT(32, 2, false); break;
     }
 #undef DLA_VECT
     return hipGetLastError();
@@ -2277,8 +2266,8 @@ int dla_wsum_slab_tiled(int dtype, const void* base, int64_t tile_elems, int64_t
       cfg && cfg->variant
           ? cfg->variant
           : vec_store_policy(vec_variant(n_peers < kMaxPeersPerPass ? n_peers : kMaxPeersPerPass), n_elems * es);
-  if (variant != 9 && variant != 10 && variant != 12 && !(variant >= 21 && variant <= 24))
-    return fail(DLA_E_CONFIG, "dla_wsum_slab_tiled: variant must be 0 (auto), 9, 10, 12 or 21-24");
+  if (variant != 9 && variant != 10 && variant != 12 && variant != 21)
+    return fail(DLA_E_CONFIG, "dla_wsum_slab_tiled: variant must be 0 (auto), 9, 10, 12 or 21");
   const int64_t stride = slab_rows * tile_elems;
   hipStream_t s = static_cast<hipStream_t>(stream);
   hipError_t e;
