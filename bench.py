@@ -470,7 +470,7 @@ def host_inclusive_sharded(n, p, n_devices, reps=3):
             fa.set_shard_threads(True)
             fa.release_staging()
         med = statistics.median(times)
-        key = "%d_gpu" % g + ("" if g == 1 else ("_pipelined" if threads else "_packed"))
+        key = "%d_gpu" % g + ("" if g == 1 else ("_native" if threads else "_packed"))
         res[key] = {"ms": round(med * 1e3, 2), "GB/s": round((n + 1) * p * 4 / med / 1e9, 2)}
     res["path"] = ("FedAvg.aggregate(CPU nn.Modules), %d x %d fp32, bucket-sharded over the GPUs of one "
                    "process (fedavg.set_host_devices)" % (n, p))
