@@ -433,8 +433,9 @@ def host_inclusive(n, p, reps=5):
         times.append(time.perf_counter() - t0)
     med = statistics.median(times)
     return {"value": round((n + 1) * p * 4 / med / 1e9, 3), "unit": "GB/s", "ms": round(med * 1e3, 2),
-            "path": "FedAvg.aggregate(CPU nn.Modules): deepcopy (params uninitialised, pinned) + chunked H2D straight "
-                    "from the parameters + reduce + D2H into the result, chunk c's D2H overlapping chunk c+1's H2D"}
+            "path": "FedAvg.aggregate(CPU nn.Modules): deepcopy (params uninitialised, pooled pageable) + "
+                    "dla_host_reduce (threaded pack of each 32 MiB chunk into page-locked rows, one H2D DMA per "
+                    "chunk, reduce, D2H and unpack into the result, two chunks in flight)"}
 
 
 def host_inclusive_sharded(n, p, n_devices, reps=3):
