@@ -50,6 +50,8 @@
 #include <utility>
 #include <vector>
 
+#include <unistd.h>
+
 #include "dlagg.h"
 
 // Hash of this file, include/dlagg.h and the compile flags, set by the build
@@ -1713,6 +1715,8 @@ class CopyPool {
   // fn(0) on the calling thread and fn(1..n-1) on workers; false if another round holds the pool.
   template <typename F>
   bool try_run(int n, F& fn) {
+    // a forked child has the pool's bookkeeping but none of its threads: it spawns its own
+    if (getpid() != pid_) return false;
     std::unique_lock<std::mutex> busy(run_mu_, std::try_to_lock);
     if (!busy.owns_lock()) return false;
     std::function<void(int)> task = [&fn](int t) { fn(t); };
@@ -1750,6 +1754,7 @@ class CopyPool {
       }
     }
   }
+  const pid_t pid_ = getpid();
   std::mutex run_mu_, mu_;
   std::condition_variable cv_, done_cv_;
   std::vector<std::thread> workers_;

@@ -4,6 +4,7 @@ product path refuses to run without a HIP device (no CPU fallback)."""
 import ctypes
 import os
 import re
+import time
 
 import pytest
 import torch
@@ -398,3 +399,47 @@ def test_host_copy_batch_threaded_ranges(lib_path):
     offs = np.cumsum([0] + sizes[:-1])
     _lib.host_copy_batch([dst.ctypes.data + int(o) for o in offs], [a.ctypes.data for a in src], sizes)
     assert np.array_equal(dst[: sum(sizes)], np.concatenate(src)) and not dst[sum(sizes):].any()
+
+
+def test_copy_pool_after_fork(lib_path):
+    """dla_host_copy_batch runs large batches on a persistent thread pool; a forked child (the
+    pool's threads do not exist there) must still complete its copies instead of waiting on them."""
+    import numpy as np
+
+    from accdfl_amd import _lib
+
+    src = np.arange(6 << 20, dtype=np.uint8)   # 6 MiB: threaded
+    dst = np.zeros_like(src)
+    _lib.host_copy_batch([dst.ctypes.data], [src.ctypes.data], [src.nbytes])  # creates the pool
+    assert np.array_equal(dst, src)
+    pid = os.fork()
+    if pid == 0:  # child: copy again through the (absent) pool, exit 0 on success
+        code = 1
+        try:
+            out = np.zeros_like(src)
+            _lib.host_copy_batch([out.ctypes.data], [src.ctypes.data], [src.nbytes])
+            code = 0 if np.array_equal(out, src) else 2
+        finally:
+            os._exit(code)
+    deadline = time.time() + 60
+    while True:
+        done, status = os.waitpid(pid, os.WNOHANG)
+        if done:
+            break
+        if time.time() > deadline:
+            os.kill(pid, 9)
+            os.waitpid(pid, 0)
+            pytest.fail("forked child hung in dla_host_copy_batch")
+        time.sleep(0.05)
+    assert os.WIFEXITED(status) and os.WEXITSTATUS(status) == 0
+
+
+def test_numa_cpulist_and_binding_without_gpu():
+    from accdfl_amd.core import host_memory
+
+    assert host_memory._cpulist("0-3,8,10-11\n") == {0, 1, 2, 3, 8, 10, 11}
+    assert host_memory._cpulist("") == set()
+    if not torch.cuda.is_available():
+        before = os.sched_getaffinity(0)
+        assert host_memory.gpu_numa_node() is None and host_memory.bind_to_gpu_node() is None
+        assert os.sched_getaffinity(0) == before
