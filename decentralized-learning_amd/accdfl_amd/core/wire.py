@@ -125,7 +125,7 @@ def _block_address(block) -> int:
 
 def _gather(addrs, lens, dst: torch.Tensor) -> None:
     """Copy the pieces back to back into the host uint8 tensor ``dst`` (one native batched
-    memcpy, threaded above 8 MiB: libdlagg's dla_host_copy_batch)."""
+    memcpy, threaded from 4 MiB: libdlagg's dla_host_copy_batch)."""
     from accdfl_amd import _lib
 
     if not lens:

@@ -1768,7 +1768,7 @@ CopyPool& copy_pool() {
   return *pool;
 }
 
-// dsts[i] <- srcs[i], bytes[i] each (validated by the caller); threaded above 8 MiB.
+// dsts[i] <- srcs[i], bytes[i] each (validated by the caller); threaded from 4 MiB.
 void copy_batch(void* const* dsts, const void* const* srcs, const int64_t* bytes, int n) {
   int64_t total = 0;
   for (int i = 0; i < n; ++i) total += bytes[i];

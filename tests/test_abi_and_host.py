@@ -386,7 +386,7 @@ def test_result_memory_pool_reuses_blocks_only_after_release():
 
 
 def test_host_copy_batch_threaded_ranges(lib_path):
-    """dla_host_copy_batch splits batches above 8 MiB into equal byte ranges over threads (a
+    """dla_host_copy_batch splits batches of 4 MiB and more into equal byte ranges over threads (a
     range may start and end inside a segment): every byte lands exactly once."""
     import numpy as np
 
@@ -443,3 +443,39 @@ def test_numa_cpulist_and_binding_without_gpu():
         before = os.sched_getaffinity(0)
         assert host_memory.gpu_numa_node() is None and host_memory.bind_to_gpu_node() is None
         assert os.sched_getaffinity(0) == before
+
+
+def test_copy_batch_concurrent_callers(lib_path):
+    """Several host threads in dla_host_copy_batch at once (the bucket-sharded host path runs one per
+    GPU): one holds the persistent pool, the others spawn their own threads; every byte lands."""
+    import threading
+
+    import numpy as np
+
+    from accdfl_amd import _lib
+
+    rng = np.random.default_rng(3)
+    srcs = [rng.integers(0, 255, size=(9 << 20) + 7 * k, dtype=np.uint8) for k in range(6)]
+    dsts = [np.zeros_like(s) for s in srcs]
+    errors = []
+
+    def work(k):
+        try:
+            for _ in range(5):
+                dsts[k][:] = 0
+                half = srcs[k].nbytes // 2
+                _lib.host_copy_batch([dsts[k].ctypes.data, dsts[k].ctypes.data + half],
+                                     [srcs[k].ctypes.data, srcs[k].ctypes.data + half],
+                                     [half, srcs[k].nbytes - half])
+                if not np.array_equal(dsts[k], srcs[k]):
+                    errors.append(k)
+        except Exception as exc:  # noqa: BLE001 — reported below
+            errors.append(exc)
+
+    threads = [threading.Thread(target=work, args=(k,)) for k in range(6)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(timeout=120)
+    assert not any(t.is_alive() for t in threads), "a copy hung"
+    assert not errors, errors
