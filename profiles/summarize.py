@@ -64,8 +64,11 @@ if trace:
     kmax = 8 if bench_peers <= 8 else 32 if bench_peers <= 32 else 128
     lead = "%d, %d," % (dtype_code, bench_peers if bench_kernel == "wsum_bigtile_kernel" else kmax)
     ns = {k: v for k, v in groups.items() if k[0].split(bench_kernel + "<")[1].startswith(lead)}
-    if bench_kernel == "wsum_vec_kernel":  # the TILED template flag: the headline, not separate_buffers
-        ns = {k: v for k, v in ns.items() if (", true>(" in k[0]) == bench_tiled}
+    if bench_kernel == "wsum_vec_kernel":  # the TILED template flag (6th argument): the headline, not separate_buffers
+        def tiled(name):
+            targs = name.split(bench_kernel + "<", 1)[1].split(">(", 1)[0].split(",")
+            return len(targs) > 5 and targs[5].strip() == "true"
+        ns = {k: v for k, v in ns.items() if tiled(k[0]) == bench_tiled}
     groups = ns or groups
     if groups:
         (kname, kgrid), durs = max(groups.items(), key=lambda kv: sum(kv[1]))
