@@ -2116,16 +2116,7 @@ int dla_host_reduce(int dtype, int n_peers, int n_tensors, const void* const* te
   hipEvent_t* d2h = ev.e + 4;
   const int64_t row_bytes = chunk_elems * es;
   const int64_t buf_bytes = row_bytes * n_peers;
-  // chunk boundaries: a first chunk of 1/8 (the DMA starts after a short pack instead of a full
-  // one), then full chunks
-  std::vector<int64_t> cut{begin};
-  {
-    const int64_t gran = 256 / es;
-    const int64_t first = ((chunk_elems / 8 + gran - 1) / gran) * gran;
-    for (int64_t x = begin + (first < chunk_elems ? first : chunk_elems); x < end; x += chunk_elems) cut.push_back(x);
-    cut.push_back(end);
-  }
-  const int64_t n_chunks = static_cast<int64_t>(cut.size()) - 1;
+  const int64_t n_chunks = (end - begin + chunk_elems - 1) / chunk_elems;
   std::vector<void*> dsts;
   std::vector<const void*> srcs;
   std::vector<int64_t> bytes;
@@ -2149,7 +2140,7 @@ int dla_host_reduce(int dtype, int n_peers, int n_tensors, const void* const* te
   auto unpack = [&](int64_t c) {
     const int buf = static_cast<int>(c & 1);
     if (!check(hipEventSynchronize(d2h[buf]), "D2H")) return;
-    const int64_t c0 = cut[c], c1 = cut[c + 1];
+    const int64_t c0 = begin + c * chunk_elems, c1 = c0 + chunk_elems < end ? c0 + chunk_elems : end;
     dsts.clear(), srcs.clear(), bytes.clear();
     pieces(c0, c1, [&](int t, int64_t a, int64_t b) {
       dsts.push_back(static_cast<char*>(outs[t]) + (a - start[t]) * es);
@@ -2166,7 +2157,7 @@ int dla_host_reduce(int dtype, int n_peers, int n_tensors, const void* const* te
   const auto t_start = clk::now();
   for (int64_t c = 0; c < n_chunks && e == hipSuccess; ++c) {
     const int buf = static_cast<int>(c & 1);
-    const int64_t c0 = cut[c], c1 = cut[c + 1];
+    const int64_t c0 = begin + c * chunk_elems, c1 = c0 + chunk_elems < end ? c0 + chunk_elems : end;
     const int64_t m = c1 - c0;
     const auto t0 = clk::now();
     char* hs = static_cast<char*>(h_stage) + buf * buf_bytes;
