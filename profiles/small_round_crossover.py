@@ -1,6 +1,8 @@
 """r02: FedAvg.aggregate of CPU-resident models, small-round path (dla_host_round_*: pack into
-page-locked rows, the kernel reads them across PCIe) against the pipelined path (chunked H2D
-straight from the parameters overlapping the D2H), forced by _SMALL_ROW_BYTES / _SMALL_ROUND_BYTES, per input size."""
+page-locked rows, the kernel reads them across PCIe) against the large-round paths — native
+(dla_host_reduce: packed chunks, one DMA per chunk) and pipelined (chunked H2D straight from the
+parameters overlapping the D2H) — forced by _SMALL_ROW_BYTES / _SMALL_ROUND_BYTES, per input size.
+The process is bound to the GPU's NUMA node first (as bench.py does)."""
 import json
 import os
 import statistics
@@ -27,9 +29,12 @@ def med(fn, reps):
 
 
 def main():
+    from accdfl_amd.core.host_memory import bind_to_gpu_node
+
+    print(json.dumps({"numa_node_bound": bind_to_gpu_node()}), flush=True)
     default = F._SMALL_ROW_BYTES, F._SMALL_ROUND_BYTES
-    for n, numel in ((2, 256 << 10), (2, 1 << 20), (2, 1_690_046), (2, 4_932_344), (8, 256 << 10), (8, 512 << 10),
-                     (8, 1 << 20), (4, 3_900_000)):
+    for n, numel in ((2, 256 << 10), (2, 512 << 10), (2, 1 << 20), (2, 1_690_046), (2, 4_932_344), (8, 128 << 10),
+                     (8, 256 << 10), (8, 512 << 10), (8, 1 << 20), (4, 3_900_000), (32, 256 << 10)):
         g = torch.Generator().manual_seed(n)
         ms = [nn.ParameterList([nn.Parameter(torch.randn(numel, generator=g))]) for _ in range(n)]
         w = [1.0 / n] * n
@@ -38,7 +43,10 @@ def main():
         F._SMALL_ROW_BYTES = F._SMALL_ROUND_BYTES = 1 << 40
         r["small_us"] = med(lambda: F.FedAvg.aggregate(ms, w), reps)
         F._SMALL_ROUND_BYTES = 0
+        r["native_us"] = med(lambda: F.FedAvg.aggregate(ms, w), reps)
+        F.set_host_path("pipelined")
         r["pipelined_us"] = med(lambda: F.FedAvg.aggregate(ms, w), reps)
+        F.set_host_path("native")
         F._SMALL_ROW_BYTES, F._SMALL_ROUND_BYTES = default
         r["default_us"] = med(lambda: F.FedAvg.aggregate(ms, w), reps)
         print(json.dumps(r), flush=True)
