@@ -278,7 +278,7 @@ def _small_round(models: List[nn.Module], weights, layout) -> "nn.Module | None"
         stream = torch.cuda.current_stream(device).cuda_stream
         _lib.host_round_start(code, n, ptrs, hr.numels_arr, weights, hr.h_in.data_ptr(), pitch, hr.h_out.data_ptr(),
                               stream)
-        center = _center_copy(models[0], large=False)  # overlaps the reduce
+        center = _center_copy(models[0])  # overlaps the reduce
         params = list(center.parameters())
         if len(params) != len(numels) or not all(c.is_contiguous() for c in params):
             torch.cuda.current_stream(device).synchronize()
@@ -304,7 +304,7 @@ def _large_round(models: List[nn.Module], weights, layout) -> "nn.Module | None"
     device = _wsum.require_device(None)
     devices = _devices_for(device)
     devices = devices[:max(1, min(len(devices), (total * esize) // _MIN_SHARD_BYTES))]
-    center = _center_copy(models[0], large=n * total * esize >= _SMALL_ROUND_BYTES)
+    center = _center_copy(models[0])
     params = list(center.parameters())
     if len(params) != len(numels) or not all(c.is_cpu and c.is_contiguous() for c in params):
         return None
@@ -433,8 +433,16 @@ _native_staging: Dict[Tuple[torch.device, torch.dtype, int], _NativeStaging] = {
 _NATIVE_CHUNK_BYTES = int(float(os.environ.get("ACCDFL_AMD_HOST_CHUNK_MB", "32")) * (1 << 20))
 
 
+_NATIVE_MIN_CHUNK_BYTES = 2 << 20
+
+
 def _native_chunk(n: int, esize: int, bucket: int, align: int) -> int:
-    chunk = max(align, _NATIVE_CHUNK_BYTES // (n * esize) // align * align)
+    """Elements per peer row of a dla_host_reduce chunk: 32 MiB of rows, but at least 8 chunks per
+    bucket down to 2 MiB — nothing crosses PCIe until the first chunk is packed, so a round of one
+    or two full chunks waits a whole pack before its DMA starts (2 x 4.9 M fp32: 1.58 ms in 32 MiB
+    chunks against 1.48 for per-tensor DMAs, profiles/r02zk_crossover.log)."""
+    target = min(_NATIVE_CHUNK_BYTES, max(_NATIVE_MIN_CHUNK_BYTES, n * bucket * esize // 8))
+    chunk = max(align, target // (n * esize) // align * align)
     return min(chunk, _round_up(bucket, align))
 
 
@@ -710,8 +718,10 @@ def _center_copy(model0: nn.Module, large: bool = True) -> nn.Module:
     uninitialised tensors of the same shape, strides, dtype, device and
     ``requires_grad``: the reduce overwrites every one of them, so copying models[0]'s
     values first (and page-faulting P fresh elements: 16 ms of a 35 ms host-inclusive
-    8 x 25 M reduce) is wasted.  For a ``large`` round the contiguous CPU parameters come
-    from core/host_memory.result_tensor (pre-faulted pooled pageable memory by default).
+    8 x 25 M reduce) is wasted.  Contiguous CPU parameters come from
+    core/host_memory.result_tensor (tensors of 1 MiB and more: pre-faulted pooled pageable memory
+    by default — a fresh 19.7 MB result costs 1.65 ms of page faults, as much as the PCIe transfer
+    of a 2-model ResNet-8 round; ``large=False`` allocates every parameter fresh).
     Buffers and every other attribute are deep-copied exactly as in the reference (the module
     tree through _clone_value, deepcopy's protocol without its per-object dispatch: the GL
     merge of two GNLeNet models builds this copy every round)."""
@@ -748,9 +758,7 @@ class FedAvg(GradientAggregation):
                         done = _large_round(models, list(weights), layout)
                     if done is not None:
                         return done
-            params0 = list(models[0].parameters())
-            nbytes = sum(p.numel() * p.element_size() for p in params0) * len(models)
-            center_model = _center_copy(models[0], large=nbytes >= _SMALL_ROUND_BYTES)
+            center_model = _center_copy(models[0])
             reduce_parameters(list(center_model.parameters()), [list(m.parameters()) for m in models],
                               list(weights))
             return center_model

@@ -109,10 +109,11 @@ def result_tensor(shape, dtype: torch.dtype) -> torch.Tensor:
     """An uninitialised contiguous CPU tensor for a result parameter, per the mode."""
     numel = int(np.prod(shape)) if len(shape) else 1
     nbytes = numel * torch.empty((), dtype=dtype).element_size()
-    if _mode == "pooled" and nbytes >= POOL_MIN_BYTES and dtype in _NP:
-        return _pool.take(tuple(shape), dtype)
-    if _mode == "pinned" and torch.cuda.is_available():
-        return torch.empty(tuple(shape), dtype=dtype, pin_memory=True)
+    if nbytes >= POOL_MIN_BYTES:  # smaller tensors: plain torch.empty in every mode
+        if _mode == "pooled" and dtype in _NP:
+            return _pool.take(tuple(shape), dtype)
+        if _mode == "pinned" and torch.cuda.is_available():
+            return torch.empty(tuple(shape), dtype=dtype, pin_memory=True)
     return torch.empty(tuple(shape), dtype=dtype)
 
 

@@ -20,7 +20,7 @@ import torch.nn as nn
 
 from accdfl_amd.core.gradient_aggregation import GradientAggregationMethod
 from accdfl_amd.core import wire
-from accdfl_amd.core.gradient_aggregation.fedavg import _SMALL_ROUND_BYTES, FedAvg, _center_copy
+from accdfl_amd.core.gradient_aggregation.fedavg import FedAvg, _center_copy
 
 
 class ModelManager:
@@ -203,18 +203,17 @@ class DeviceModelManager(ModelManager):
             weights = [float(1. / n) for _ in range(n)]
         else:
             assert len(weights) == n
-        large = n * self.slab.total * self.slab.buf.element_size() >= _SMALL_ROUND_BYTES
         with torch.no_grad():
             first = entries[0]
             if isinstance(first, WirePeer):
                 # deepcopy(models[0]) of the module unserialize_model would have built:
                 # the template's structure with the first arrival's buffers.
-                center = _center_copy(self.template, large=large)
+                center = _center_copy(self.template)
                 for name, buf in center.named_buffers():
                     if name in first.state_dict:
                         buf.copy_(first.state_dict[name])
             else:
-                center = _center_copy(first, large=large)  # deepcopy(models[0]) minus the parameter values
+                center = _center_copy(first)  # deepcopy(models[0]) minus the parameter values
             self.slab.reduce_into(list(center.parameters()), weights)
         return center
 
