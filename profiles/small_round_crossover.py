@@ -44,6 +44,10 @@ def main():
         r["small_us"] = med(lambda: F.FedAvg.aggregate(ms, w), reps)
         F._SMALL_ROUND_BYTES = 0
         r["native_us"] = med(lambda: F.FedAvg.aggregate(ms, w), reps)
+        prev_min = F._NATIVE_MIN_CHUNK_BYTES
+        F._NATIVE_MIN_CHUNK_BYTES = F._NATIVE_CHUNK_BYTES  # full 32 MiB chunks only
+        r["native_32MiB_chunks_us"] = med(lambda: F.FedAvg.aggregate(ms, w), reps)
+        F._NATIVE_MIN_CHUNK_BYTES = prev_min
         F.set_host_path("pipelined")
         r["pipelined_us"] = med(lambda: F.FedAvg.aggregate(ms, w), reps)
         F.set_host_path("native")
