@@ -167,15 +167,17 @@ def _flat_slices(tensors: List[torch.Tensor], numels: List[int], start: int, end
     return out
 
 
-# Small rounds are latency-bound: below these sizes a round goes through dla_host_round_*
-# (one native call packs every peer into page-locked rows and enqueues the reduce, which reads
-# them across PCIe; one call waits and unpacks) instead of the chunked H2D/D2H pipeline.  The
-# crossover is per peer row (profiles/r02s_small_round_crossover.log, us small / pipelined):
-# 2 x 1 MiB 140.6 / 269.5, 8 x 1 MiB 403.4 / 478.2, 8 x 2 MiB 619.4 / 639.2, but 2 x 4 MiB
-# 492.6 / 408.9, 2 x 6.8 MB 874.4 / 535.8, 8 x 4 MiB 1228.4 / 981.8.  GNLeNet (configs[1], the
-# GL merge of N=2 every round) is 341 KB per row.
-_SMALL_ROW_BYTES = 2 << 20
-_SMALL_ROUND_BYTES = 64 << 20
+# Small rounds go through dla_host_round_* (one native call packs every peer into page-locked rows
+# and enqueues the reduce, which reads them across PCIe; one call waits and unpacks) instead of the
+# chunked dla_host_reduce: below ~96 MB of input the kernel's own PCIe reads beat the chunked DMAs
+# (no pack-before-DMA fill, no per-chunk round trips).  Measured on the reference layouts, us
+# small / dla_host_reduce (profiles/r02zo_layout_paths.log): FEMNIST 2 peers 619 / 828, 4 peers
+# 943 / 1343, 8 peers (54 MB) 1644-1882 / 1759-1979, 32 peers (216 MB) 6152 / 4704; ResNet-8 2 peers
+# 1393-2496 / 2290-2780, 3 peers 1895 / 2587, 4 peers (79 MB) 2497 / 2966, 8 peers (158 MB)
+# 4951 / 4213; GNLeNet 8 peers 257 / 367, 64 peers 1084 / 1528.  (Round 2 first bounded it at
+# 2 MiB per row against the per-tensor pipelined path, profiles/r02s_small_round_crossover.log.)
+_SMALL_ROW_BYTES = 64 << 20
+_SMALL_ROUND_BYTES = 96 << 20
 
 
 def _is_small(n: int, row_bytes: int) -> bool:

@@ -476,9 +476,12 @@ def test_host_path_sharded_over_devices(dtype, mode):
     w = [0.3, 0.1, 0.2, 0.25, 0.15]
     fa.set_host_devices(["cuda:0", "cuda:0", "cuda:0"])
     fa.set_host_path(mode)
+    small = fa._SMALL_ROUND_BYTES
+    fa._SMALL_ROUND_BYTES = 0  # the large-round paths (the bf16 round would be a small round)
     try:
         out = fa.FedAvg.aggregate(models, w)
     finally:
+        fa._SMALL_ROUND_BYTES = small
         fa.set_host_devices([])
         fa.set_host_path("native")
     for i, p in enumerate(out.parameters()):
@@ -508,13 +511,14 @@ def test_native_host_reduce_chunks(dtype, pinned, chunk_bytes):
         m.register_buffer("running_mean", torch.full((7,), float(k)))
         models.append(m)
     w = [float(x) for x in np.random.default_rng(11).dirichlet(np.ones(11))]
-    old = fa._NATIVE_CHUNK_BYTES
+    old, small = fa._NATIVE_CHUNK_BYTES, fa._SMALL_ROUND_BYTES
     fa._NATIVE_CHUNK_BYTES = chunk_bytes
+    fa._SMALL_ROUND_BYTES = 0  # dla_host_reduce even where the round would be a small one
     try:
         assert fa.host_path() == "native"
         out = fa.FedAvg.aggregate(models, w)
     finally:
-        fa._NATIVE_CHUNK_BYTES = old
+        fa._NATIVE_CHUNK_BYTES, fa._SMALL_ROUND_BYTES = old, small
         fa.release_staging()
     for i, p in enumerate(out.parameters()):
         want = fedavg_bits([gc.as_float(_bits(m[i].detach().reshape(-1), dtype), dtype) for m in models], w, dtype)
