@@ -732,7 +732,7 @@ def _center_copy(model0: nn.Module, large: bool = True) -> nn.Module:
         if id(p) in memo or type(p) is not nn.Parameter:
             continue  # Parameter subclasses keep the stock deepcopy
         if p.device.type == "cpu":
-            if large and p.is_contiguous():
+            if large and p.is_contiguous() and p.numel() * p.element_size() >= _host_memory.POOL_MIN_BYTES:
                 data = _host_memory.result_tensor(p.shape, p.dtype)
             else:
                 data = torch.empty_strided(p.size(), p.stride(), dtype=p.dtype)
