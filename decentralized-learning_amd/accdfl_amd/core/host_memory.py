@@ -12,7 +12,7 @@ by ``ACCDFL_AMD_RESULT_MEMORY`` or ``set_result_memory``:
   taken from a pool of already-faulted blocks (anonymous mmaps, transparent huge pages
   requested).  A block returns to the pool when the last tensor using it is freed, and the
   pool keeps at most ``POOL_FREE_BYTES`` of free blocks.  Nothing is page-locked.
-* ``pinned``: the result tensors of a large round are allocated page-locked
+* ``pinned``: the result tensors of >= 1 MiB are allocated page-locked
   (``is_pinned()``).  As fast, but they stay page-locked for the model's lifetime and
   torch's caching host allocator keeps freed blocks page-locked too, so page-locked host
   memory grows with the number of results kept.
