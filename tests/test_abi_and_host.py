@@ -479,3 +479,22 @@ def test_copy_batch_concurrent_callers(lib_path):
         t.join(timeout=120)
     assert not any(t.is_alive() for t in threads), "a copy hung"
     assert not errors, errors
+
+
+def test_host_round_routing_and_chunks():
+    """The CPU-module round sizes the host paths are chosen by (fedavg.py: _is_small, _native_chunk)."""
+    from accdfl_amd.core.gradient_aggregation import fedavg as fa
+
+    mb = 1 << 20
+    assert fa._is_small(2, 341_416)                       # GL merge of two GNLeNet models
+    assert fa._is_small(2, 19_729_376)                    # GL merge of two ResNet-8 models (19.7 MB rows)
+    assert fa._is_small(4, 19_729_376)                    # 79 MB
+    assert not fa._is_small(8, 19_729_376)                # 158 MB: dla_host_reduce
+    assert not fa._is_small(32, 6_760_184)                # configs[2], 216 MB
+    assert not fa._is_small(1, 65 * mb) and not fa._is_small(2, 0)
+    for n, esize, bucket in ((8, 4, 25_000_000), (128, 2, 21_296_355), (2, 4, 4_932_344), (11, 8, 3_000_000)):
+        align = 256 // esize
+        c = fa._native_chunk(n, esize, bucket, align)
+        assert c % align == 0 and c <= -(-bucket // align) * align
+        assert n * c * esize <= fa._NATIVE_CHUNK_BYTES
+        assert n * c * esize >= min(fa._NATIVE_MIN_CHUNK_BYTES, n * bucket * esize) - n * align * esize
