@@ -126,10 +126,10 @@ def gpu_numa_node(device=None):
     if not torch.cuda.is_available():
         return None
     props = torch.cuda.get_device_properties(torch.device("cuda", 0) if device is None else device)
-    bus = "%04x:%02x:%02x.0" % (getattr(props, "pci_domain_id", 0), props.pci_bus_id, props.pci_device_id)
     try:
+        bus = "%04x:%02x:%02x.0" % (getattr(props, "pci_domain_id", 0), props.pci_bus_id, props.pci_device_id)
         node = int(open("/sys/bus/pci/devices/%s/numa_node" % bus).read())
-    except (OSError, ValueError):
+    except (AttributeError, TypeError, OSError, ValueError):
         return None
     return node if node >= 0 else None
 
