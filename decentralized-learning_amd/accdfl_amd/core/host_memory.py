@@ -161,5 +161,8 @@ def bind_to_gpu_node(device=None) -> "int | None":
     mine = cpus & os.sched_getaffinity(0)
     if not mine:
         return None
-    os.sched_setaffinity(0, mine)
+    try:
+        os.sched_setaffinity(0, mine)
+    except OSError:
+        return None
     return node
