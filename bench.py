@@ -50,12 +50,14 @@ Extra objects on the JSON line:
 from __future__ import annotations
 
 import argparse
+import datetime
 import json
 import os
 import socket
 import statistics
 import subprocess
 import sys
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -113,9 +115,15 @@ def parse():
                     help="HBM layout of the headline's peers: the PeerSlab tile-interleaved slab (default) or "
                          "one buffer per peer")
     ap.add_argument("--strong-steps", type=int, default=20)
+    ap.add_argument("--leg-timeout", type=float, default=300.0,
+                    help="seconds any one leg (the headline included) may take on any rank; past it the run "
+                         "ends at once with a non-zero exit, rank 0 printing the line measured so far")
+    ap.add_argument("--dist-timeout", type=float, default=0.0,
+                    help="torch.distributed timeout in seconds (default: --leg-timeout + 120, so the leg "
+                         "watchdog fires first)")
     ap.add_argument("--dry-run", action="store_true",
-                    help="launch + rendezvous + rank-count check + bucket split only, no GPU work "
-                         "(what the CPU test of the multi-rank launch runs)")
+                    help="launch + rendezvous + rank-count check + bucket split + a gloo all-gather leg with its "
+                         "parity check, no GPU work (what the CPU tests of the multi-rank launch run)")
     ap.add_argument("--sweep", action="store_true", help="interleaved A/B of launch variants, then exit")
     ap.add_argument("--host-breakdown", action="store_true", help="time the host-inclusive phases, then exit")
     ap.add_argument("--no-numa-bind", action="store_true",
@@ -165,15 +173,163 @@ def setup_dist(args):
         torch.cuda.set_device(dev)
     cpu_group = None
     if world > 1:
+        # every collective of the run has a deadline: no leg can wait out a 10-minute default
+        # (the Legs watchdog, at --leg-timeout, ends a stuck run before this one fires)
+        timeout = datetime.timedelta(seconds=args.dist_timeout or args.leg_timeout + 120)
         if backend == "nccl" and not args.dry_run:
-            dist.init_process_group("nccl", device_id=dev)
+            dist.init_process_group("nccl", device_id=dev, timeout=timeout)
         else:
-            dist.init_process_group("gloo" if args.dry_run else backend)
-        cpu_group = dist.new_group(backend="gloo")
+            dist.init_process_group("gloo" if args.dry_run else backend, timeout=timeout)
+        cpu_group = dist.new_group(backend="gloo", timeout=timeout)
         world = dist.get_world_size()
     if world != args.gpus:
         raise SystemExit("bench.py: --gpus %d but the process group has %d rank(s)" % (args.gpus, world))
     return rank, world, dev, cpu_group
+
+
+class LegAbort(Exception):
+    """Some rank failed this leg before its collectives: every rank skips it."""
+
+
+def _injected(leg, rank):
+    """BENCH_INJECT_FAIL=<leg>:<rank>:<mode> (tests only): make `leg` fail on `rank` —
+    raise_prepare (before its collectives), raise_run (right after every rank agreed to start
+    them) or hang (block forever there)."""
+    spec = os.environ.get("BENCH_INJECT_FAIL", "")
+    if not spec:
+        return None
+    name, r, mode = spec.rsplit(":", 2)
+    return mode if name == leg and int(r) == rank else None
+
+
+class Legs:
+    """Runs the legs of one bench process so that a failure or a hang on one rank never leaves the
+    other ranks waiting in a collective:
+
+    * a leg calls ``go()`` right before its first collective: a gloo all-reduce (MIN) of a ready
+      flag.  A rank that failed while preparing contributes 0 there, and every rank skips the leg
+      together (its row says "skipped");
+    * a rank that fails AFTER ``go()`` (its peers may sit in a collective it will never join) ends
+      the run at once with a non-zero exit, rank 0 printing the line measured so far
+      ("aborted_leg"); ``settled()`` marks the end of a leg's collectives, after which a local
+      failure is only recorded;
+    * a watchdog thread ends the run the same way when a leg outlives ``timeout_s``;
+    * after each leg the ranks agree (gloo, MIN) on its status and its parity flag, so a row's
+      ``parity_ok`` is the verdict of every rank (None where no rank checked anything).
+    At world 1 the agreements are no-ops and only the watchdog remains."""
+
+    def __init__(self, rank, world, group, timeout_s, result):
+        self.rank, self.world, self.group = rank, world, group
+        self.timeout_s = timeout_s
+        self.result = result  # the JSON line so far (printed by rank 0 if the run is cut short)
+        self.failed = []
+        self._name = None
+        self._deadline = None
+        self._went = self._go_done = False
+        threading.Thread(target=self._watch, daemon=True).start()
+
+    # ------------------------------------------------------------------ agreement / abort
+    def _agree(self, vals):
+        t = torch.tensor(vals, dtype=torch.int64)
+        if self.world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MIN, group=self.group)
+        return [int(x) for x in t]
+
+    def go(self):
+        """Every rank is ready for this leg's collectives (else LegAbort on every rank)."""
+        if self._go_done:
+            return
+        self._go_done = True
+        if not self._agree([1])[0]:
+            raise LegAbort()
+        self._went = True
+        mode = _injected(self._name, self.rank)
+        if mode == "raise_run":
+            raise RuntimeError("injected failure after go() on rank %d" % self.rank)
+        if mode == "hang":
+            log("injected hang in leg %s on rank %d" % (self._name, self.rank), every_rank=True)
+            while True:
+                time.sleep(1)
+
+    def settled(self):
+        """This leg's collectives are over: a later local failure is recorded, not fatal."""
+        self._went = False
+
+    def fatal(self, leg, reason, code=1):
+        log("FATAL in leg %s on rank %d: %s — ending the run" % (leg, self.rank, reason), every_rank=True)
+        if self.rank == 0:
+            for _ in range(3):
+                try:
+                    res = dict(self.result, aborted_leg={"leg": leg, "rank": 0, "reason": str(reason)[:500],
+                                                         "exit_code": code})
+                    print(json.dumps(res), flush=True)
+                    break
+                except (RuntimeError, TypeError, ValueError):  # the main thread was mutating the dict
+                    time.sleep(0.05)
+        sys.stdout.flush()
+        sys.stderr.flush()
+        os._exit(code)
+
+    def _watch(self):
+        while True:
+            time.sleep(0.25)
+            d = self._deadline
+            if d is not None and time.monotonic() > d:
+                self.fatal(self._name, "leg exceeded its %.0f s deadline (--leg-timeout)" % self.timeout_s, 124)
+
+    def arm(self, name, timeout_s=None):
+        self._name = name
+        self._deadline = time.monotonic() + (timeout_s or self.timeout_s)
+
+    def disarm(self):
+        self._deadline = None
+
+    # ------------------------------------------------------------------ one leg
+    def run(self, name, fn, *a, timeout_s=None, **kw):
+        """Row of leg `name` (fn(self, *a, **kw) returns a dict; may set "parity_ok")."""
+        self._went = self._go_done = False
+        self.arm(name, timeout_s)
+        log("leg %s" % name)
+        row, ok = None, 1
+        try:
+            if _injected(name, self.rank) == "raise_prepare":
+                raise RuntimeError("injected failure before the collectives on rank %d" % self.rank)
+            row = fn(self, *a, **kw)
+            if not self._go_done:
+                self.go()
+        except LegAbort:
+            self.disarm()
+            self.failed.append(name)
+            return {"skipped": "a rank failed before this leg's collectives"}
+        except Exception as exc:  # noqa: BLE001 — every failure of a leg is reported on its row
+            if self._went:
+                self.fatal(name, "%s: %s" % (type(exc).__name__, exc))
+            msg = "%s: %s" % (type(exc).__name__, exc)
+            log("leg %s failed on rank %d: %s" % (name, self.rank, msg), every_rank=True)
+            if not self._go_done:  # the others are (or will be) in go(): tell them, skip together
+                self._go_done = True
+                try:
+                    self._agree([0])
+                except Exception as exc2:  # noqa: BLE001
+                    self.fatal(name, "agreement failed: %s" % exc2)
+                self.disarm()
+                self.failed.append(name)
+                return {"skipped": "failed on rank %d before its collectives" % self.rank, "error": msg}
+            row, ok = {"error": msg}, 0
+        par = row.get("parity_ok") if isinstance(row, dict) else None
+        try:
+            ok_all, par_all = self._agree([ok, 2 if par is None else int(bool(par))])
+        except Exception as exc:  # noqa: BLE001 — a peer died: nothing can be agreed any more
+            self.fatal(name, "final agreement failed: %s" % exc)
+        self.disarm()
+        if isinstance(row, dict):
+            if par_all != 2:
+                row["parity_ok"] = bool(par_all)
+            if not ok_all and ok:
+                row["error_on_another_rank"] = True
+        if not ok_all or par_all == 0:
+            self.failed.append(name)
+        return row
 
 
 def launch_info(world):
@@ -183,10 +339,11 @@ def launch_info(world):
                            "torch.distributed.run" if "WORLD_SIZE" in os.environ else "single process")}
 
 
-def log(msg):
+def log(msg, every_rank=False):
     """Progress on stderr (one line per phase), so a long run visibly advances."""
-    if os.environ.get("RANK", "0") == "0":
-        print("[bench %.1fs] %s" % (time.perf_counter() - _T0, msg), file=sys.stderr, flush=True)
+    rank = os.environ.get("RANK", "0")
+    if rank == "0" or every_rank:
+        print("[bench %.1fs r%s] %s" % (time.perf_counter() - _T0, rank, msg), file=sys.stderr, flush=True)
 
 
 _T0 = time.perf_counter()
@@ -453,14 +610,23 @@ def host_inclusive_sharded(n, p, n_devices, reps=3):
         m = nn.Module()
         m.w = nn.Parameter(torch.randn(p, generator=gen) * 0.05)
         models.append(m)
-    w = [float(1.0 / n)] * n
+    w = [float(x) for x in np.random.default_rng(3).dirichlet(np.ones(n))]
     res = {}
-    runs = [(1, True)] + ([(n_devices, True), (n_devices, False)] if n_devices > 1 else [])
-    for g, threads in runs:
-        fa.set_host_devices(list(range(g)))
+    # one visible GPU (the several-ranks rehearsal): the buckets repeat GPU 0, the same code path
+    devices = list(range(n_devices)) if n_devices <= torch.cuda.device_count() else [0] * n_devices
+    runs = [([0], True)] + ([(devices, True), (devices, False)] if n_devices > 1 else [])
+    ref = None
+    ok = True
+    for devs, threads in runs:
+        fa.set_host_devices(devs)
         fa.set_shard_threads(threads)
         try:
-            fa.FedAvg.aggregate(models, w)
+            out = fa.FedAvg.aggregate(models, w)
+            if ref is None:
+                ref = out.w.detach().clone()  # the one-GPU result: every sharded result must equal it
+            good = same_bits(out.w.detach(), ref)
+            ok = ok and good
+            del out
             times = []
             for _ in range(reps):
                 t0 = time.perf_counter()
@@ -471,10 +637,13 @@ def host_inclusive_sharded(n, p, n_devices, reps=3):
             fa.set_shard_threads(True)
             fa.release_staging()
         med = statistics.median(times)
-        key = "%d_gpu" % g + ("" if g == 1 else ("_native" if threads else "_packed"))
-        res[key] = {"ms": round(med * 1e3, 2), "GB/s": round((n + 1) * p * 4 / med / 1e9, 2)}
+        key = "%d_gpu" % len(devs) + ("" if len(devs) == 1 else ("_native" if threads else "_packed"))
+        res[key] = {"ms": round(med * 1e3, 2), "GB/s": round((n + 1) * p * 4 / med / 1e9, 2), "devices": devs,
+                    "parity_ok": good}
     res["path"] = ("FedAvg.aggregate(CPU nn.Modules), %d x %d fp32, bucket-sharded over the GPUs of one "
-                   "process (fedavg.set_host_devices)" % (n, p))
+                   "process (fedavg.set_host_devices); each sharded result checked bit for bit against the "
+                   "one-GPU result" % (n, p))
+    res["parity_ok"] = ok
     return res
 
 
@@ -539,19 +708,110 @@ def host_breakdown(n, p, device):
     return res
 
 
-def collectives(n, p, dt, es, world, device, slab, w, iters=10):
-    """RCCL over xGMI, reported beside (never inside) `value`, N > 1 only:
-    * allgather: every rank's averaged bucket -> the whole model on every rank;
-    * peer_sharded_exact: peers arrive whole on different ranks (n / world each) ->
-      all-to-all transpose -> the same bit-exact bucket reduce -> all-gather;
-    * peer_sharded_reduce_scatter: local partial fold -> reduce-scatter -> all-gather
-      (stated-tolerance mode)."""
+def _comm_device(device):
+    """Where the collectives' tensors live: the GPU over RCCL, the host over gloo (the
+    several-ranks-on-one-GPU rehearsal)."""
+    return device if dist.get_backend() == "nccl" else torch.device("cpu")
+
+
+def _bits(t):
+    return t.view({8: torch.int64, 4: torch.int32, 2: torch.int16}[t.element_size()])
+
+
+def same_bits(a, b):
+    """Bit-for-bit equality of two float tensors (NaN-free synthetic data), on a's device."""
+    a = a.contiguous()
+    b = b.to(a.device).contiguous()
+    return a.shape == b.shape and a.dtype == b.dtype and bool(torch.equal(_bits(a), _bits(b)))
+
+
+def gather_all(local, max_len, cdev):
+    """all_gather of `local` (padded to max_len elements) -> one tensor per rank, on every rank."""
+    buf = torch.zeros(max_len, dtype=local.dtype, device=cdev)
+    if local.numel():
+        buf[: local.numel()].copy_(local)
+    outs = [torch.empty_like(buf) for _ in range(dist.get_world_size())]
+    dist.all_gather(outs, buf)
+    return outs
+
+
+def _seeded_rows(ks, length, dt, device, seed_base):
+    """Rows k in ks of a seeded peer set (row k = normal(0, 0.05) of `length` elements from
+    seed seed_base + k): every rank and the rank-0 reference build the same rows."""
+    out = torch.empty((len(ks), length), dtype=dt, device=device)
+    for i, k in enumerate(ks):
+        out[i].normal_(0.0, 0.05, generator=torch.Generator(device=device).manual_seed(seed_base + k))
+    return out
+
+
+def _rank_content(r, length, dt, cdev):
+    """A rank's deterministic all-gather payload (cheap to rebuild on every rank)."""
+    i = torch.arange(length, dtype=torch.int64, device=cdev)
+    return ((i * 7 + r * 1_000_003) % 65521).to(dt)
+
+
+def leg_headline_parity(legs, inp, n, p, dt, w, rank, world, device):
+    """The weak headline's per-rank buckets, reassembled by an all-gather, against ONE single-GPU
+    reduce of the whole n x (world * p) model rebuilt on rank 0 from the same seeds (rank r's
+    bucket of peer k = seed 1000 + 97 r + k) — bit for bit."""
+    from accdfl_amd.core import wsum
+
+    cdev = _comm_device(device)
+    ref = None
+    if rank == 0:
+        pitch = max(128, (p + 127) // 128 * 128)
+        full = torch.empty((n, world * p), dtype=dt, device=device)
+        for r in range(world):
+            full[:, r * p:(r + 1) * p].copy_(make_slab(n, pitch, dt, device, 1000 + 97 * r)[:, :p])
+        ref = wsum.wsum(list(full), w)
+        del full
+    legs.go()
+    got = gather_all(inp.out[:p], p, cdev)
+    legs.settled()
+    row = {"check": "all-gathered buckets of every rank == one reduce of the whole %d x %d model on rank 0's GPU"
+                    % (n, world * p)}
+    if rank == 0:
+        row["parity_ok"] = same_bits(torch.cat(got).to(device), ref)
+    return row
+
+
+def leg_allgather(legs, p, dt, es, world, rank, device, iters=10):
+    """RCCL all-gather of every rank's averaged bucket into the whole model on every rank (the
+    reassembly step, never inside `value`); every rank checks the gathered model against the
+    buckets it can rebuild (_rank_content)."""
+    from accdfl_amd.core.sharding import BucketShardedFedAvg
+
+    cdev = _comm_device(device)
+    sh = BucketShardedFedAvg(p * world, dt, device=cdev)
+    bucket = _rank_content(rank, sh.bucket_len, dt, cdev)
+    full = torch.empty(p * world, dtype=dt, device=cdev)
+    want = torch.cat([_rank_content(r, sh.bucket_len, dt, cdev) for r in range(world)])[: p * world]
+    legs.go()
+    wall, _ = time_kernel(lambda: sh.all_gather(bucket, full), iters, 2, world, settle_s=0)
+    legs.settled()
+    return {"ms": round(wall / iters * 1e3, 3), "bytes_out_per_rank": p * world * es,
+            "GBps_per_rank_in": round((world - 1) * sh.bucket_len * es / (wall / iters) / 1e9, 1),
+            "parity_ok": same_bits(full, want)}
+
+
+def leg_peer_sharded(legs, exact, n, p, dt, world, rank, device, w, iters=10):
+    """Peers arriving whole on different ranks (rank r holds peers r*m .. r*m+m-1, m = n / world,
+    each of world * p elements, seed 6000 + k):
+    * exact: all-to-all transpose -> the same list-order bucket reduce -> all-gather, checked bit
+      for bit against one single-GPU reduce of all n peers on rank 0;
+    * reduce-scatter (exact=False): local partial fold -> reduce-scatter -> all-gather, checked
+      against the same reference within its stated bound |err| <= N 2^-23 sum_k |w_k p_k|."""
     from accdfl_amd.core import wsum
     from accdfl_amd.core.sharding import BucketShardedFedAvg
 
-    res = {}
-    on_gpu = dist.get_backend() == "nccl"
-    cdev = device if on_gpu else torch.device("cpu")  # gloo rehearsal: CPU tensors, GPU reduce
+    if n % world:
+        return {"skipped": "%d peers do not split evenly over %d ranks" % (n, world)}
+    if not exact and dt not in (torch.float32, torch.float64):
+        return {"skipped": "the reduce-scatter mode states its bound for fp32 / fp64 only"}
+    cdev = _comm_device(device)
+    on_gpu = cdev.type == "cuda"
+    m = n // world
+    L = p * world
 
     def reducer(peers, weights, out):
         if on_gpu:
@@ -559,23 +819,78 @@ def collectives(n, p, dt, es, world, device, slab, w, iters=10):
         out.copy_(wsum.wsum([t.to(device) for t in peers], weights).cpu())
         return out
 
-    sh = BucketShardedFedAvg(p * world, dt, device=cdev, reducer=reducer)
-    bucket = torch.zeros(sh.bucket_len, dtype=dt, device=cdev)
-    full = torch.empty(p * world, dtype=dt, device=cdev)
-    wall, _ = time_kernel(lambda: sh.all_gather(bucket, full), iters, 2, world, settle_s=0)
-    res["allgather"] = {"ms": round(wall / iters * 1e3, 3), "bytes_out_per_rank": p * world * es,
-                        "GBps_per_rank_in": round((world - 1) * sh.bucket_len * es / (wall / iters) / 1e9, 1)}
-    if n % world == 0:
-        m = n // world
-        local = torch.empty((m, p * world), dtype=dt, device=cdev).normal_(0.0, 0.05)
-        for exact in (True, False):
-            fn = lambda: sh.aggregate_peer_sharded(local, w, exact=exact)  # noqa: E731
-            wall, _ = time_kernel(fn, iters, 2, world, settle_s=0)
-            key = "peer_sharded_exact" if exact else "peer_sharded_reduce_scatter"
-            res[key] = {"ms": round(wall / iters * 1e3, 3), "peers_per_rank": m,
-                        "model_params": p * world, "bit_exact": exact}
-        del local
-    return res
+    local = _seeded_rows(range(rank * m, (rank + 1) * m), L, dt, device, 6000).to(cdev)
+    ref = bound = None
+    if rank == 0:
+        allp = _seeded_rows(range(n), L, dt, device, 6000)
+        ref = wsum.wsum(list(allp), w)
+        if not exact:
+            bound = torch.zeros(L, dtype=torch.float64, device=device)
+            for k in range(n):
+                bound.add_(allp[k].double().abs_().mul_(abs(w[k])))
+            bound.mul_(n * 2.0 ** -23)
+        del allp
+    sh = BucketShardedFedAvg(L, dt, device=cdev, reducer=reducer)
+    fn = lambda: sh.aggregate_peer_sharded(local, w, exact=exact)  # noqa: E731
+    legs.go()
+    wall, _ = time_kernel(fn, iters, 2, world, settle_s=0)
+    out = fn()
+    legs.settled()
+    row = {"ms": round(wall / iters * 1e3, 3), "peers_per_rank": m, "model_params": L, "bit_exact": exact}
+    if rank == 0:
+        got = out.to(device)
+        if exact:
+            row["parity_ok"] = same_bits(got, ref)
+        else:
+            err = (got.double() - ref.double()).abs_()
+            row["parity_ok"] = bool(torch.all(err <= bound))
+            row["max_err_over_bound"] = float((err / bound.clamp_min(1e-300)).max())
+            row["tolerance"] = "N * 2^-23 * sum_k |w_k p_k| (DESIGN.md §2)"
+    return row
+
+
+def leg_xgmi_sharded(legs, n, p, world, rank, device, w, reps=10):
+    """dla_wsum_sharded (ONE process, several GPUs): n peers of p fp32 placed
+    round-robin on GPUs 0..G-1 of rank 0's process, G = min(world, visible GPUs); shard s reduces
+    bucket s of every peer on GPU s, reading the peers held elsewhere over xGMI; "direct" writes
+    every bucket straight into the result on GPU 0, "gather" writes locally then copies
+    peer-to-peer.  Checked bit for bit against wsum on GPU 0.  With one visible GPU (the
+    several-ranks rehearsal) the shards repeat GPU 0.  The other ranks idle on the CPU."""
+    from accdfl_amd.core import wsum
+
+    legs.go()
+    if rank != 0:
+        return {}
+    g = min(world, torch.cuda.device_count())
+    devs = [torch.device("cuda", i) for i in range(g)] if g > 1 else [torch.device("cuda", 0)] * world
+    uniq = sorted({d.index for d in devs})
+    pitch = max(128, (p + 127) // 128 * 128)
+    rows = make_slab(n, pitch, torch.float32, device, 7000)
+    ref = wsum.wsum([rows[k, :p] for k in range(n)], w)
+    peers = [rows[k, :p].to(devs[k % len(devs)]) for k in range(n)]
+    torch.cuda.synchronize()
+
+    def sync():
+        for d in uniq:
+            torch.cuda.synchronize(d)
+
+    row = {"devices": [d.index for d in devs], "peer_devices": [t.device.index for t in peers],
+           "peers": n, "params": p, "modes": {}}
+    ok = True
+    for mode in ("direct", "gather"):
+        out = wsum.wsum_sharded(peers, w, devs, mode=mode)
+        sync()
+        good = same_bits(out, ref)
+        ok = ok and good
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            wsum.wsum_sharded(peers, w, devs, out=out, mode=mode)
+        sync()
+        t = (time.perf_counter() - t0) / reps
+        row["modes"][mode] = {"ms": round(t * 1e3, 3), "GB/s": round((n + 1) * p * 4 / t / 1e9, 1),
+                              "parity_ok": good}
+    row["parity_ok"] = ok
+    return row
 
 
 GNLENET = [(32, 3, 5, 5), (32,), (32,), (32,), (32, 32, 5, 5), (32,), (32,), (32,), (64, 32, 5, 5), (64,),
@@ -955,6 +1270,34 @@ def cpu_per_config():
     return res
 
 
+def cpu_baseline_all(args, result, n, p):
+    """The cpu_baseline object: the reference op sequence on the host cores (the only leg that runs
+    the oracle port), plus every other CPU comparison, each ratio filled into the GPU row it
+    belongs to."""
+    cb = cpu_baseline(n, p, args.cpu_seconds)
+    if not args.no_small:
+        cb["per_config"] = cpu_per_config()
+        for name, row in cb["per_config"].items():
+            g = result.get("baseline_configs", {}).get(name)
+            if g:
+                g["gpu_over_cpu"] = round(row["cpu_port_ms"] * 1e3 / g["us_per_reduce"], 1)
+    if not args.no_host_inclusive:
+        cb["gnlenet_small"] = cpu_gnlenet_small()
+        for key, row in cb["gnlenet_small"].items():
+            result.get("host_inclusive_small", {}).get(key, {})["cpu_port_ms"] = row["cpu_port_ms"]
+        msgs = dfl_messages(n, p)
+        cb["dfl_round_reference_style"] = dfl_round_reference_style(msgs, p)
+        del msgs
+        log("cpu baseline: reference op sequence on the config layouts")
+        cb["layout_configs"] = cpu_layout_configs()
+        for name, row in cb["layout_configs"].items():
+            g = result.get("host_inclusive_configs", {}).get(name)
+            if g and "pageable_ms" in g:
+                g["cpu_port_ms"] = row["cpu_port_ms"]
+                g["pageable_over_cpu"] = round(row["cpu_port_ms"] / g["pageable_ms"], 1)
+    return cb
+
+
 def cpu_gnlenet_small(reps=50):
     """The torch-CPU op sequence (oracle port of fedavg.py:13-26) on the GNLeNet rounds of
     host_inclusive_small."""
@@ -980,89 +1323,124 @@ _MALL_BYTES = 256 << 20
 _ROTATE_BYTES = 1 << 30
 
 
-def strong_scaling(rank, world, device, steps, warmup):
-    """Each STRONG model split into ``world`` contiguous 256-B-aligned parameter buckets
+def strong_line(legs, name, rank, world, device, steps, warmup):
+    """STRONG model `name` split into ``world`` contiguous 256-B-aligned parameter buckets
     (core/sharding.bucket_bounds, the bucket-sharded layout of SURVEY.md §8e); rank r reduces
     bucket r of every peer.  Whole-model algorithmic bytes / max-over-ranks step time.  Each
     rank cycles through enough copies of its bucket that the working set is >= 1 GiB, so a
     small bucket cannot be served from the 256 MiB Infinity Cache step after step
-    ("cache_warm" repeats one copy, for comparison).  The all-gather that reassembles the
-    whole averaged model on every rank (RCCL) is timed separately, never inside the line."""
-    from accdfl_amd import _lib
+    ("cache_warm" repeats one copy, for comparison).  At N > 1 the all-gather that reassembles
+    the whole averaged model on every rank (RCCL) is timed separately (never inside the line),
+    on the ranks' real averaged buckets, and the reassembled model is checked bit for bit on rank 0
+    against ONE reduce of the whole model rebuilt from the same seeds (copy 0 of rank r's bucket:
+    seed 1000 + 7 r + k)."""
     from accdfl_amd.core import wsum
     from accdfl_amd.core.sharding import BucketShardedFedAvg, bucket_bounds
 
-    res = {}
-    for name, (n, params, dts) in STRONG.items():
-        log("strong: " + name)
-        dt = torch.float32 if dts == "f32" else torch.bfloat16
-        es = 4 if dts == "f32" else 2
-        bounds = bucket_bounds(params, world, 256 // es)
-        s0, e0 = bounds[rank]
-        m = max(e0 - s0, 0)
-        pitch = max(128, (m + 127) // 128 * 128)
-        set_bytes = (n + 1) * pitch * es
-        copies = 1 if set_bytes >= _ROTATE_BYTES else min(64, -(-_ROTATE_BYTES // set_bytes))
-        w = [float(x) for x in np.random.default_rng(0).dirichlet(np.ones(n))]
-        inputs = [SlabInput(n, m, dt, device, 1000 + 131 * c + 7 * rank, w) for c in range(copies)] if m else []
-        sp = torch.cuda.current_stream().cuda_stream
-        ctr = [0]
-
-        def step_rot():
-            if inputs:
-                inputs[ctr[0] % len(inputs)].launch(sp)
-            ctr[0] += 1
-
-        def step_warm():
-            if inputs:
-                inputs[0].launch(sp)
-
-        wall, ev = time_kernel(step_rot, steps, warmup, world)
-        wall_w, _ = time_kernel(step_warm, steps, warmup, world)
-        total = (n + 1) * params * es
-        row = {"peers": n, "params": params, "dtype": dts, "buckets": world,
-               "bucket_params_max": max(e - s for s, e in bounds),
-               "ms_per_step": round(wall / steps * 1e3, 5),
-               "value": round(total / (wall / steps) / 1e9, 2), "unit": "GB/s",
-               "kernel_us_max_rank": round(ev / steps * 1e6, 2),
-               "input_copies_rotated": copies,
-               "cache_warm_value": round(total / (wall_w / steps) / 1e9, 2),
-               "regime": "HBM" if (n + 1) * (bounds[0][1] - bounds[0][0]) * es > _MALL_BYTES
-               else "bucket fits the Infinity Cache; rotated copies keep it HBM-resident",
-               "kernel": inputs[0].kernel if inputs else None}
-        if world > 1:
-            try:
-                cdev = device if dist.get_backend() == "nccl" else torch.device("cpu")  # gloo: host tensors
-                sh = BucketShardedFedAvg(params, dt, device=cdev)
-                bucket = torch.zeros(sh.bucket_len, dtype=dt, device=cdev)
-                full = torch.empty(params, dtype=dt, device=cdev)
-                wall_g, _ = time_kernel(lambda: sh.all_gather(bucket, full), 10, 2, world, settle_s=0)
-                row["allgather_ms"] = round(wall_g / 10 * 1e3, 4)
-                row["with_allgather_value"] = round(total / (wall / steps + wall_g / 10) / 1e9, 2)
-                del bucket, full
-            except Exception as exc:  # never lose the line to the auxiliary leg
-                row["allgather_error"] = "%s: %s" % (type(exc).__name__, exc)
-        res[name] = row
-        del inputs
+    n, params, dts = STRONG[name]
+    dt = torch.float32 if dts == "f32" else torch.bfloat16
+    es = 4 if dts == "f32" else 2
+    bounds = bucket_bounds(params, world, 256 // es)
+    s0, e0 = bounds[rank]
+    m = max(e0 - s0, 0)
+    pitch = max(128, (m + 127) // 128 * 128)
+    set_bytes = (n + 1) * pitch * es
+    copies = 1 if set_bytes >= _ROTATE_BYTES else min(64, -(-_ROTATE_BYTES // set_bytes))
+    w = [float(x) for x in np.random.default_rng(0).dirichlet(np.ones(n))]
+    ref = None
+    if world > 1 and rank == 0:  # the single-GPU reference of the whole model (built before the timing)
+        full = torch.empty((n, params), dtype=dt, device=device)
+        for r, (s, e) in enumerate(bounds):
+            if e > s:
+                pr = max(128, (e - s + 127) // 128 * 128)
+                full[:, s:e].copy_(make_slab(n, pr, dt, device, 1000 + 7 * r)[:, : e - s])
+        ref = wsum.wsum(list(full), w)
+        del full
         torch.cuda.empty_cache()
-    return res
+    inputs = [SlabInput(n, m, dt, device, 1000 + 131 * c + 7 * rank, w) for c in range(copies)] if m else []
+    sp = torch.cuda.current_stream().cuda_stream
+    ctr = [0]
+
+    def step_rot():
+        if inputs:
+            inputs[ctr[0] % len(inputs)].launch(sp)
+        ctr[0] += 1
+
+    def step_warm():  # last: leaves copy 0's average in inputs[0].out
+        if inputs:
+            inputs[0].launch(sp)
+
+    legs.go()
+    wall, ev = time_kernel(step_rot, steps, warmup, world)
+    wall_w, _ = time_kernel(step_warm, steps, warmup, world)
+    total = (n + 1) * params * es
+    row = {"peers": n, "params": params, "dtype": dts, "buckets": world,
+           "bucket_params_max": max(e - s for s, e in bounds),
+           "ms_per_step": round(wall / steps * 1e3, 5),
+           "value": round(total / (wall / steps) / 1e9, 2), "unit": "GB/s",
+           "kernel_us_max_rank": round(ev / steps * 1e6, 2),
+           "input_copies_rotated": copies,
+           "cache_warm_value": round(total / (wall_w / steps) / 1e9, 2),
+           "regime": "HBM" if (n + 1) * (bounds[0][1] - bounds[0][0]) * es > _MALL_BYTES
+           else "bucket fits the Infinity Cache; rotated copies keep it HBM-resident",
+           "kernel": inputs[0].kernel if inputs else None}
+    if world > 1:
+        cdev = _comm_device(device)
+        sh = BucketShardedFedAvg(params, dt, device=cdev)
+        bucket = torch.zeros(sh.bucket_len, dtype=dt, device=cdev)
+        if m:
+            bucket[:m].copy_(inputs[0].out[:m])
+        full = torch.empty(params, dtype=dt, device=cdev)
+        wall_g, _ = time_kernel(lambda: sh.all_gather(bucket, full), 10, 2, world, settle_s=0)
+        legs.settled()
+        row["allgather_ms"] = round(wall_g / 10 * 1e3, 4)
+        row["with_allgather_value"] = round(total / (wall / steps + wall_g / 10) / 1e9, 2)
+        if rank == 0:
+            row["parity_ok"] = same_bits(full.to(device), ref)
+    del inputs
+    torch.cuda.empty_cache()
+    return row
 
 
-def dry_run(args, rank, world):
-    """No GPU: the launch, the rendezvous, the rank-count check and the bucket split the
-    strong-scaling lines use; rank 0 prints one JSON line (checked by the CPU tests)."""
+def dry_run(args, rank, world, cpu_group):
+    """No GPU: the launch, the rendezvous, the rank-count check, the bucket split the
+    strong-scaling lines use and a gloo all-gather leg with its parity check, all through the
+    Legs runner (agreed skips, fatal exits, the watchdog); rank 0 prints one JSON line (checked by
+    the CPU tests, which also inject failures with BENCH_INJECT_FAIL)."""
     from accdfl_amd.core.sharding import bucket_bounds
 
-    mine = {name: list(bucket_bounds(params, world, 256 // (4 if dts == "f32" else 2))[rank])
-            for name, (_, params, dts) in STRONG.items()}
-    got = [None] * world
-    if world > 1:
-        dist.all_gather_object(got, mine)
-    else:
+    result = {"dry_run": True, "n_gpus": world, "launch": launch_info(world)}
+    legs = Legs(rank, world, cpu_group, args.leg_timeout, result)
+
+    def rendezvous(L):
+        mine = {name: list(bucket_bounds(params, world, 256 // (4 if dts == "f32" else 2))[rank])
+                for name, (_, params, dts) in STRONG.items()}
         got = [mine]
+        L.go()
+        if world > 1:
+            got = [None] * world
+            dist.all_gather_object(got, mine)
+        L.settled()
+        buckets = {name: [g[name] for g in got] for name in STRONG}
+        cover = all(b[0][0] == 0 and b[-1][1] == STRONG[name][1] and all(x[1] == y[0] for x, y in zip(b, b[1:]))
+                    for name, b in buckets.items())
+        return {"buckets": buckets, "parity_ok": cover}
+
+    def gloo_allgather(L, length=100_003):
+        mine = _rank_content(rank, length, torch.float32, torch.device("cpu"))
+        L.go()
+        got = gather_all(mine, length, torch.device("cpu")) if world > 1 else [mine]
+        L.settled()
+        want = [_rank_content(r, length, torch.float32, torch.device("cpu")) for r in range(world)]
+        return {"elems_per_rank": length, "parity_ok": all(same_bits(a, b) for a, b in zip(got, want))}
+
+    rows = {"rendezvous": legs.run("rendezvous", rendezvous), "gloo_allgather": legs.run("gloo_allgather",
+                                                                                          gloo_allgather)}
+    result["buckets"] = rows["rendezvous"].pop("buckets", None)
+    result["legs"] = rows
+    result["legs_failed"] = legs.failed
     if rank == 0:
-        print(json.dumps({"dry_run": True, "n_gpus": world, "launch": launch_info(world),
-                          "buckets": {name: [g[name] for g in got] for name in STRONG}}), flush=True)
+        print(json.dumps(result), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
@@ -1246,7 +1624,7 @@ def main():
         sys.exit(spawn_ranks(args))  # nothing has touched a GPU in this process
     rank, world, device, cpu_group = setup_dist(args)
     if args.dry_run:
-        dry_run(args, rank, world)
+        dry_run(args, rank, world, cpu_group)
         return
     from accdfl_amd import _lib
     from accdfl_amd.core import wsum
@@ -1285,6 +1663,10 @@ def main():
     if args.variant or args.chunks or args.grid or args.block:
         cfg = _lib.LaunchCfg(args.variant, args.chunks, args.grid, args.block)
     code = wsum.dtype_code(dt)
+    result = {"metric": METRIC, "value": None, "unit": "GB/s", "n_gpus": world, "steps": args.steps,
+              "warmup": args.warmup, "launch": dict(launch_info(world), numa_node_bound=numa_node)}
+    legs = Legs(rank, world, cpu_group, args.leg_timeout, result)
+    legs.arm("headline (setup)")
     inp = SlabInput(n, p, dt, device, 1000 + 97 * rank, w, layout="rows" if cfg is not None else args.layout)
     if cfg is not None:
         ptrs = [inp.buf[k].data_ptr() for k in range(n)]
@@ -1296,7 +1678,9 @@ def main():
             inp.launch(torch.cuda.current_stream().cuda_stream)
 
     log("headline: %d peers x %d %s, %d ranks" % (n, p, args.dtype, world))
+    legs.arm("headline")
     wall, ev = time_kernel(step, args.steps, args.warmup, world)
+    legs.disarm()
     bytes_step = (n + 1) * p * es
     ms_per_step = wall / args.steps * 1e3
     value = world * bytes_step / (wall / args.steps) / 1e9
@@ -1312,7 +1696,7 @@ def main():
         except (OSError, ValueError):
             traffic = None
 
-    result = {
+    result.update({
         "metric": METRIC,
         "value": round(value, 2),
         "unit": "GB/s",
@@ -1347,75 +1731,78 @@ def main():
             "bytes_per_launch": bytes_step,
             "us_per_launch": round(kern_s * 1e6, 2),
         },
-    }
+    })
+    parity = result["parity"] = {}
+    if world > 1:
+        row = legs.run("headline_parity", leg_headline_parity, inp, n, p, dt, w, rank, world, device)
+        parity["headline (all-gathered buckets vs one-GPU reduce of the whole model)"] = row.get("parity_ok")
+        result["headline_parity"] = row
+    head_out = inp.out[:p].clone()
     del inp
     torch.cuda.empty_cache()
     if cfg is None and args.layout == "slab":
-        # the same peers as separate buffers (what FedAvg.aggregate on device modules reduces)
-        rows = SlabInput(n, p, dt, device, 1000 + 97 * rank, w, layout="rows")
-        _, ev_r = time_kernel(lambda: rows.launch(torch.cuda.current_stream().cuda_stream), args.steps,
-                              args.warmup, world)
-        result["separate_buffers"] = {"kernel": rows.kernel, "us_per_launch": round(ev_r / args.steps * 1e6, 2),
-                                      "GB/s": round(bytes_step / (ev_r / args.steps) / 1e9, 1)}
-        del rows
-        torch.cuda.empty_cache()
+        def separate(L):
+            # the same peers as separate buffers (what FedAvg.aggregate on device modules reduces)
+            rows = SlabInput(n, p, dt, device, 1000 + 97 * rank, w, layout="rows")
+            L.go()
+            _, ev_r = time_kernel(lambda: rows.launch(torch.cuda.current_stream().cuda_stream), args.steps,
+                                  args.warmup, world)
+            L.settled()
+            row = {"kernel": rows.kernel, "us_per_launch": round(ev_r / args.steps * 1e6, 2),
+                   "GB/s": round(bytes_step / (ev_r / args.steps) / 1e9, 1),
+                   "parity_ok": same_bits(rows.out[:p], head_out),
+                   "check": "same peers, row-major kernel == the headline's tiled-slab kernel, bit for bit"}
+            del rows
+            torch.cuda.empty_cache()
+            return row
+        result["separate_buffers"] = legs.run("separate_buffers", separate)
+        parity["separate_buffers == headline"] = result["separate_buffers"].get("parity_ok")
+    del head_out
     if not args.no_strong and args.dtype == "f32" and (n, p) == (NS_PEERS, NS_PARAMS):
-        log("strong-scaling lines")
-        result["strong_scaling"] = {"scaling": "strong",
-                                    "lines": strong_scaling(rank, world, device, args.strong_steps, 3)}
+        lines = {}
+        for name in STRONG:
+            lines[name] = legs.run("strong: " + name, strong_line, name, rank, world, device, args.strong_steps, 3)
+            if world > 1:
+                parity["strong: " + name] = lines[name].get("parity_ok")
+        result["strong_scaling"] = {"scaling": "strong", "lines": lines}
     if world > 1 and not args.no_collectives:
-        try:  # same shapes on every rank: a failure raises on all of them, nothing waits
-            result["collectives"] = collectives(n, args.coll_params or p, dt, es, world, device, None, w)
-        except Exception as exc:  # never lose the headline line to an auxiliary leg
-            result["collectives"] = {"error": "%s: %s" % (type(exc).__name__, exc)}
+        coll_p = args.coll_params or (p if dist.get_backend() == "nccl" else min(p, 1 << 21))
+        coll = result["collectives"] = {}
+        coll["allgather"] = legs.run("allgather", leg_allgather, coll_p, dt, es, world, rank, device)
+        for exact, key in ((True, "peer_sharded_exact"), (False, "peer_sharded_reduce_scatter")):
+            coll[key] = legs.run(key, leg_peer_sharded, exact, n, coll_p, dt, world, rank, device, w)
+        if args.dtype == "f32":
+            coll["xgmi_sharded"] = legs.run("xgmi_sharded", leg_xgmi_sharded, n, p, world, rank, device, w)
+        for key, row in coll.items():
+            parity["collectives: " + key] = row.get("parity_ok")
     if world > 1 and not args.no_host_inclusive and args.dtype == "f32":
         # rank 0 alone drives GPUs 0..G-1 from one process (the reference's CPU-module call
         # sites); the other ranks wait on the CPU (gloo), so no RCCL kernel sits on a GPU
-        if rank == 0:
-            try:
-                g = min(world, torch.cuda.device_count())
-                result["host_inclusive_sharded"] = host_inclusive_sharded(n, p, g)
-            except Exception as exc:  # never lose the headline line to an auxiliary leg
-                result["host_inclusive_sharded"] = {"error": "%s: %s" % (type(exc).__name__, exc)}
-        dist.barrier(group=cpu_group)
+        def sharded_host(L):
+            L.go()
+            return host_inclusive_sharded(n, p, world) if rank == 0 else {}
+        result["host_inclusive_sharded"] = legs.run("host_inclusive_sharded", sharded_host)
+        parity["host_inclusive_sharded"] = result["host_inclusive_sharded"].get("parity_ok")
     if rank == 0 and world == 1:
         if not args.no_small:
-            log("baseline configs")
-            result["baseline_configs"] = baseline_configs(device)
+            result["baseline_configs"] = legs.run("baseline_configs", lambda L: baseline_configs(device))
         if not args.no_host_inclusive and args.dtype == "f32":
-            log("host-inclusive legs")
-            result["host_inclusive"] = host_inclusive(n, p)
-            result["wire_ingress"] = wire_ingress(p, device)
-            result["host_inclusive_small"] = host_inclusive_small()
-            result["host_inclusive_configs"] = host_inclusive_configs()
-            log("DFL round from EVA blocks")
-            msgs = dfl_messages(n, p)
-            result["dfl_round"] = dfl_round(msgs, p, device)
-            del msgs
-        if not args.no_cpu_baseline and args.dtype == "f32":
-            log("cpu baseline")
-            cb = result["cpu_baseline"] = cpu_baseline(n, p, args.cpu_seconds)
-            # every CPU comparison lives in this leg (the only one that runs the oracle port)
-            if not args.no_small:
-                cb["per_config"] = cpu_per_config()
-                for name, row in cb["per_config"].items():
-                    g = result.get("baseline_configs", {}).get(name)
-                    if g:
-                        g["gpu_over_cpu"] = round(row["cpu_port_ms"] * 1e3 / g["us_per_reduce"], 1)
-            if not args.no_host_inclusive:
-                cb["gnlenet_small"] = cpu_gnlenet_small()
-                for key, row in cb["gnlenet_small"].items():
-                    result.get("host_inclusive_small", {}).get(key, {})["cpu_port_ms"] = row["cpu_port_ms"]
+            result["host_inclusive"] = legs.run("host_inclusive", lambda L: host_inclusive(n, p))
+            result["wire_ingress"] = legs.run("wire_ingress", lambda L: wire_ingress(p, device))
+            result["host_inclusive_small"] = legs.run("host_inclusive_small", lambda L: host_inclusive_small())
+            result["host_inclusive_configs"] = legs.run("host_inclusive_configs", lambda L: host_inclusive_configs())
+
+            def dfl(L):
                 msgs = dfl_messages(n, p)
-                cb["dfl_round_reference_style"] = dfl_round_reference_style(msgs, p)
-                del msgs
-                log("cpu baseline: reference op sequence on the config layouts")
-                cb["layout_configs"] = cpu_layout_configs()
-                for name, row in cb["layout_configs"].items():
-                    g = result.get("host_inclusive_configs", {}).get(name)
-                    if g:
-                        g["cpu_port_ms"] = row["cpu_port_ms"]
-                        g["pageable_over_cpu"] = round(row["cpu_port_ms"] / g["pageable_ms"], 1)
+                return dfl_round(msgs, p, device)
+            result["dfl_round"] = legs.run("dfl_round", dfl)
+        if not args.no_cpu_baseline and args.dtype == "f32":
+            result["cpu_baseline"] = legs.run("cpu_baseline", lambda L: cpu_baseline_all(args, result, n, p),
+                                              timeout_s=max(args.leg_timeout, 600))
+    parity = {k: v for k, v in parity.items() if v is not None}
+    result["parity"] = parity
+    result["parity_ok"] = all(parity.values()) if parity else None
+    result["legs_failed"] = legs.failed
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

@@ -25,9 +25,11 @@ keeps them page-locked for good; "pageable" allocates them fresh).
 Where the arithmetic runs: always on the HIP device (libdlagg.so).  Models already
 on the device are reduced in place of their parameters with no copies; models on several
 GPUs are bucket-sharded over those GPUs (dla_wsum_sharded).  CPU models (every reference
-call site): small rounds (peer rows <= 2 MiB, the GL merge of two GNLeNet models) are packed
-into page-locked rows that the kernel reads across PCIe (dla_host_round_start / _finish)
-while the result module is built; larger rounds stream element chunks through the GPU in one
+call site): small rounds (_is_small: rows of at most _SMALL_ROW_BYTES = 64 MiB and under
+_SMALL_ROUND_BYTES = 96 MB of input in all, e.g. the GL merge of two models of any BASELINE
+layout) are packed into page-locked rows that the kernel reads across PCIe
+(dla_host_round_start / _finish) while the result module is built; larger rounds stream element
+chunks through the GPU in one
 native call (dla_host_reduce: a threaded pack of every peer's chunk into page-locked rows, one
 DMA per chunk, the reduce, the D2H and the unpack into the result, two chunks in flight),
 optionally bucket-sharded over several GPUs.  The host-staged paths are synchronous like the reference;
@@ -280,9 +282,16 @@ def _small_round(models: List[nn.Module], weights, layout) -> "nn.Module | None"
         stream = torch.cuda.current_stream(device).cuda_stream
         _lib.host_round_start(code, n, ptrs, hr.numels_arr, weights, hr.h_in.data_ptr(), pitch, hr.h_out.data_ptr(),
                               stream)
-        center = _center_copy(models[0])  # overlaps the reduce
-        params = list(center.parameters())
-        if len(params) != len(numels) or not all(c.is_contiguous() for c in params):
+        # the kernel now reads hr.h_in / writes hr.h_out across PCIe: every way out of this block
+        # waits for it, so the next round cannot repack those rows under a running kernel
+        try:
+            center = _center_copy(models[0])  # overlaps the reduce
+            params = list(center.parameters())
+            ok = len(params) == len(numels) and all(c.is_contiguous() for c in params)
+        except BaseException:
+            torch.cuda.current_stream(device).synchronize()
+            raise
+        if not ok:
             torch.cuda.current_stream(device).synchronize()
             return None
         _lib.host_round_finish(code, hr.numels_arr, hr.h_out.data_ptr(), [c.data_ptr() for c in params], stream)
@@ -416,14 +425,21 @@ class _NativeStaging:
         self.copy_stream = torch.cuda.Stream(device)
 
     def ensure(self, rows: int, chunk: int):
-        if rows <= self.rows and chunk <= self.chunk:
-            return
-        rows, chunk = max(rows, self.rows), max(chunk, self.chunk)
-        self.h_stage = self.d_stage = self.h_out = self.d_out = None
-        self.h_stage = torch.empty(2 * rows * chunk, dtype=self.dtype, pin_memory=True)
-        self.d_stage = torch.empty(2 * rows * chunk, dtype=self.dtype, device=self.device)
-        self.h_out = torch.empty(2 * chunk, dtype=self.dtype, pin_memory=True)
-        self.d_out = torch.empty(2 * chunk, dtype=self.dtype, device=self.device)
+        """Room for two chunks of ``rows`` rows of ``chunk`` elements.  The staging grows with the
+        byte footprint rows * chunk, not with the two maxima apart: the chunk shrinks as the peer
+        count grows (_native_chunk), so a 2-peer round of a 25 M model (chunk 3.1 M) followed by a
+        64-peer round (chunk 131 K) needs 2 x 8.4 M elements, not 2 x 64 x 3.1 M (1.6 GB of
+        page-locked host memory plus as much HBM).  dla_host_reduce lays the rows out from the
+        call's own (n_peers, chunk_elems), so any buffer of at least that size serves."""
+        stage = 2 * rows * chunk
+        if self.h_stage is None or self.h_stage.numel() < stage:
+            self.h_stage = self.d_stage = None
+            self.h_stage = torch.empty(stage, dtype=self.dtype, pin_memory=True)
+            self.d_stage = torch.empty(stage, dtype=self.dtype, device=self.device)
+        if self.h_out is None or self.h_out.numel() < 2 * chunk:
+            self.h_out = self.d_out = None
+            self.h_out = torch.empty(2 * chunk, dtype=self.dtype, pin_memory=True)
+            self.d_out = torch.empty(2 * chunk, dtype=self.dtype, device=self.device)
         self.rows, self.chunk = rows, chunk
 
 

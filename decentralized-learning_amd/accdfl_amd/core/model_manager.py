@@ -93,11 +93,18 @@ class DeviceModelManager(ModelManager):
         # models that arrive as EVA block lists are gathered here instead of b''.join'ed
         self._ingress: List[Optional[torch.Tensor]] = []
         self._ingress_ev: List[Optional[torch.cuda.Event]] = []
+        # next ingress slot of this round: only ever increases within a round (reset with the
+        # registry), so a registry entry removed mid-round never hands its slot — still viewed by
+        # a live WirePeer — to the next arrival
+        self._ingress_next = 0
 
     @staticmethod
     def _fingerprint(model) -> tuple:
         """Identity and in-place version of every parameter (torch bumps ``_version`` on each
-        in-place write, so a model changed after it arrived no longer matches)."""
+        in-place write, so a model changed after it arrived no longer matches).  Writes through
+        ``p.data`` (``p.data.copy_(...)``, ``p.data += ...``) bypass the version counter and are
+        NOT detected: a caller that edits a registered model that way after it arrived must
+        re-register it (or call ``reset_incoming_trained_models``)."""
         if isinstance(model, WirePeer):
             return ()
         return tuple((id(p), p.data_ptr(), p._version) for p in model.parameters())
@@ -151,9 +158,13 @@ class DeviceModelManager(ModelManager):
             return
         if self.template is None:
             raise ValueError("DeviceModelManager needs a template module to decode wire payloads")
-        pos = len(self.incoming_trained_models)
         alloc = None
+        pos = -1
+        if not self.incoming_trained_models:
+            self._ingress_next = 0  # a new round (also when the caller replaced the registry dict)
         if isinstance(data, (list, tuple)):
+            pos = self._ingress_next
+            self._ingress_next += 1
             n_tensors = len(self.template.state_dict())
             alloc = self._ingress_alloc(pos, sum(len(b) for b in data) + 256 * (n_tensors + 1))
         sd = wire.loads_state_dict(data, copy=False, alloc=alloc)  # views of `data` / the ingress buffer
@@ -173,6 +184,7 @@ class DeviceModelManager(ModelManager):
     def reset_incoming_trained_models(self):
         super().reset_incoming_trained_models()
         self._staged = []
+        self._ingress_next = 0
         if self.slab is not None:
             self.slab.reset()
 

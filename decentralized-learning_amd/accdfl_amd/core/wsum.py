@@ -184,11 +184,22 @@ def wsum_sharded(peers: Sequence[torch.Tensor], weights: Sequence[float], device
                            gather, [int(st.cuda_stream) for st in shard_streams])
     # out's device waits for every shard's writes (direct) / its own copies (gather: already ordered)
     o_stream = shard_streams[0]
-    for st in shard_streams[1:]:
+    done = []
+    for st in shard_streams:
+        ev = torch.cuda.Event()
+        ev.record(st)
+        done.append((st, ev))
         if st.cuda_stream != o_stream.cuda_stream:
-            ev = torch.cuda.Event()
-            ev.record(st)
             o_stream.wait_event(ev)
+    # every peer-owning device's current stream waits for the shards that read its memory over
+    # xGMI: the caching allocator reuses a freed peer (or a .contiguous() temporary of one) only for
+    # later work on that stream, so a caller that drops the peers right after this call cannot have
+    # their memory rewritten while a remote shard still reads it
+    for pd in peer_devs:
+        cur = torch.cuda.current_stream(pd)
+        for st, ev in done:
+            if st.cuda_stream != cur.cuda_stream:
+                cur.wait_event(ev)
     for t, st in zip(keep[1:], shard_streams[1:]):
         t.record_stream(st)
         t.record_stream(o_stream)

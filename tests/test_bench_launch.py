@@ -7,6 +7,7 @@ import json
 import os
 import subprocess
 import sys
+import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
@@ -32,6 +33,52 @@ def test_gpus_2_self_spawns_two_ranks():
         es = 2 if "bf16" in name else 4
         assert buckets[1][0] * es % 256 == 0
     assert res["buckets"]["north star, 8 peers x 25 M f32"][1][1] == 25_000_000
+
+
+def test_dry_run_legs_agree_and_check_parity():
+    """Every leg of the dry run goes through the Legs runner: agreed start, a parity flag agreed by
+    both ranks (the gloo all-gather's payload rebuilt and compared on every rank)."""
+    p, res = _run("--gpus", "2", "--dist-backend", "gloo", "--dry-run")
+    assert p.returncode == 0, p.stderr[-2000:]
+    assert res["legs"]["rendezvous"]["parity_ok"] is True
+    assert res["legs"]["gloo_allgather"]["parity_ok"] is True
+    assert res["legs_failed"] == []
+
+
+def test_failure_before_collectives_skips_the_leg_on_every_rank():
+    """A leg that fails on rank 1 before its collectives is skipped by BOTH ranks together (the
+    gloo agreement in go()); the run goes on to the next leg and prints its line."""
+    p, res = _run("--gpus", "2", "--dist-backend", "gloo", "--dry-run",
+                  env={"BENCH_INJECT_FAIL": "rendezvous:1:raise_prepare"})
+    assert p.returncode == 0, p.stderr[-2000:]
+    assert "skipped" in res["legs"]["rendezvous"]
+    assert res["legs"]["gloo_allgather"]["parity_ok"] is True
+    assert res["legs_failed"] == ["rendezvous"]
+
+
+def test_failure_inside_collectives_ends_the_run_nonzero_quickly():
+    """A rank failing after every rank agreed to enter the collectives cannot resynchronise: it
+    ends the run at once with a non-zero exit (no 10-minute collective timeout)."""
+    t0 = time.monotonic()
+    p, _ = _run("--gpus", "2", "--dist-backend", "gloo", "--dry-run", "--leg-timeout", "60",
+                env={"BENCH_INJECT_FAIL": "gloo_allgather:1:raise_run"})
+    assert p.returncode != 0
+    assert time.monotonic() - t0 < 90, "the failing run took too long to end"
+    assert "FATAL in leg gloo_allgather" in p.stderr
+
+
+def test_hung_rank_hits_the_leg_deadline():
+    """A rank that hangs inside a leg: the watchdog ends the run with a non-zero exit shortly after
+    --leg-timeout; rank 0 prints the line measured so far, naming the leg."""
+    t0 = time.monotonic()
+    p, res = _run("--gpus", "2", "--dist-backend", "gloo", "--dry-run", "--leg-timeout", "8",
+                  env={"BENCH_INJECT_FAIL": "gloo_allgather:1:hang"})
+    elapsed = time.monotonic() - t0
+    assert p.returncode != 0
+    assert elapsed < 75, elapsed
+    assert "gloo_allgather" in p.stderr
+    if res is not None:  # rank 0 got to print before the launcher stopped it
+        assert res["aborted_leg"]["leg"] == "gloo_allgather"
 
 
 def test_single_process_default_is_one_rank():

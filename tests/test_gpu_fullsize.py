@@ -105,6 +105,65 @@ def test_configs4_whole_model_bf16_every_lane_position():
     assert same_bits(_bits(out[idx], "bf16"), want, "bf16")
 
 
+def _tiled(slab, n, numel, tile):
+    """The PeerSlab tile-interleaved layout [n_tiles][n][tile] of the first numel elements of
+    each row of a row-major slab (core/peer_slab.py; include/dlagg.h dla_wsum_slab_tiled)."""
+    n_t = -(-numel // tile)
+    buf = torch.zeros((n_t, n, tile), dtype=slab.dtype, device=slab.device)
+    full = numel // tile
+    for k in range(n):
+        if full:
+            buf[:full, k, :].copy_(slab[k, : full * tile].view(full, tile))
+        if numel > full * tile:
+            buf[full, k, : numel - full * tile].copy_(slab[k, full * tile: numel])
+    return buf
+
+
+def test_north_star_tiled_slab_dirichlet_every_element():
+    """The headline's own kernel and layout at full size: 8 peers x 25 M fp32 in the
+    tile-interleaved slab with 16 KiB tiles (what dla_slab_tile_elems picks for it), reduced by
+    dla_wsum_slab_tiled with NON-uniform (Dirichlet) weights — every element against the C oracle
+    (the only full-size check of this path used uniform 1/8 weights)."""
+    from accdfl_amd import _lib
+
+    n, numel = 8, 25_000_000
+    tile = _lib.slab_tile_elems(_lib.DLA_F32, n, numel)
+    assert tile * 4 == 16384
+    slab = _slab(n, numel, "f32", 8100)
+    buf = _tiled(slab, n, numel, tile)
+    host = slab[:, :numel].cpu()
+    del slab
+    w = [float(x) for x in np.random.default_rng(81).dirichlet(np.ones(n))]
+    out = torch.empty(numel, device="cuda")
+    _lib.wsum_slab_tiled_ptr(_lib.DLA_F32, buf.data_ptr(), tile, n, w, numel, out.data_ptr(),
+                             torch.cuda.current_stream().cuda_stream)
+    want = c_wsum([host[k].numpy() for k in range(n)], w, "f32")
+    assert same_bits(out.cpu().numpy(), want, "f32")
+
+
+def test_configs4_whole_model_tiled_4k_bf16_every_lane_position():
+    """configs[4]'s whole model (128 x 21,296,355 bf16) in the tile-interleaved slab with 4 KiB
+    tiles (dla_slab_tile_elems for it), on the chunk-covering sample: every bf16 position of a
+    chunk, the first and last tiles and the ragged tail."""
+    from accdfl_amd import _lib
+
+    n, numel = 128, 21_296_355
+    tile = _lib.slab_tile_elems(_lib.DLA_BF16, n, numel)
+    assert tile * 2 == 4096
+    slab = _slab(n, numel, "bf16", 1300)
+    buf = _tiled(slab, n, numel, tile)
+    idx_np = _chunk_covering_sample(numel, 8, 13)
+    idx = torch.from_numpy(idx_np).cuda()
+    sample = slab[:, :numel].index_select(1, idx).cpu()
+    del slab
+    w = [float(x) for x in np.random.default_rng(128).dirichlet(np.ones(n))]
+    out = torch.empty(numel, dtype=torch.bfloat16, device="cuda")
+    _lib.wsum_slab_tiled_ptr(_lib.DLA_BF16, buf.data_ptr(), tile, n, w, numel, out.data_ptr(),
+                             torch.cuda.current_stream().cuda_stream)
+    want = c_wsum([_bits(sample[k].contiguous(), "bf16") for k in range(n)], w, "bf16")
+    assert same_bits(_bits(out[idx], "bf16"), want, "bf16")
+
+
 class _LayoutModel(nn.Module):
     """A module with a reference model's parameter and buffer layout (names flattened)."""
 

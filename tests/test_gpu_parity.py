@@ -526,6 +526,71 @@ def test_native_host_reduce_chunks(dtype, pinned, chunk_bytes):
     assert torch.equal(out.running_mean, models[0].running_mean)
 
 
+def test_native_staging_grows_with_the_footprint():
+    """the chunk staging of dla_host_reduce grows with rows x chunk, not with the two
+    maxima apart — a 2-peer round of a 25 M fp32 model (big chunks) followed by a 64-peer round
+    (small chunks) keeps ~2 x max(rows x chunk) elements, not 2 x 64 x the 2-peer chunk (1.6 GB)."""
+    from accdfl_amd.core.gradient_aggregation import fedavg as fa
+
+    dev = torch.device("cuda", 0)
+    fa.release_staging()
+    try:
+        align = 256 // 4
+        c2 = fa._native_chunk(2, 4, 25_000_000, align)
+        c64 = fa._native_chunk(64, 4, 25_000_000, align)
+        assert c2 > 8 * c64  # the shape of the problem: the chunk shrinks as peers grow
+        st = fa._get_native_staging(dev, torch.float32, -1, 2, c2)
+        st = fa._get_native_staging(dev, torch.float32, -1, 64, c64)
+        need = max(2 * 2 * c2, 2 * 64 * c64)
+        assert st.h_stage.numel() == need and st.d_stage.numel() == need
+        assert st.h_out.numel() == 2 * c2
+        assert st.h_stage.numel() * 4 < 128 << 20
+        # and the round through it is still bit-exact (2 then 64 peers of a 1 M model, small chunks)
+        old, small = fa._NATIVE_CHUNK_BYTES, fa._SMALL_ROUND_BYTES
+        fa._NATIVE_CHUNK_BYTES, fa._SMALL_ROUND_BYTES = 1 << 20, 0
+        try:
+            for n in (2, 64, 3):
+                peers = _random_peers(n, 1_000_003, "f32", seed=n)
+                models = []
+                for t in peers:
+                    m = torch.nn.Module()
+                    m.w = torch.nn.Parameter(t)
+                    models.append(m)
+                w = [float(x) for x in np.random.default_rng(n).dirichlet(np.ones(n))]
+                out = fa.FedAvg.aggregate(models, w)
+                assert same_bits(out.w.detach().numpy(), fedavg_bits([t.numpy() for t in peers], w, "f32"), "f32"), n
+        finally:
+            fa._NATIVE_CHUNK_BYTES, fa._SMALL_ROUND_BYTES = old, small
+    finally:
+        fa.release_staging()
+
+
+def test_small_round_waits_for_its_kernel_when_the_copy_fails(monkeypatch):
+    """if building the result module raises after the small-round kernel was queued,
+    the stream is drained before the page-locked rows are released to the next round."""
+    from accdfl_amd.core.gradient_aggregation import fedavg as fa
+
+    c = gc.load("gnlenet_n8_dirichlet")
+    models = gc.build_models(c, "cpu")
+    calls = []
+    real = torch.cuda.Stream.synchronize
+
+    def boom(model0, large=True):
+        raise RuntimeError("copy failed")
+
+    def sync(self):
+        calls.append(1)
+        return real(self)
+
+    monkeypatch.setattr(fa, "_center_copy", boom)
+    monkeypatch.setattr(torch.cuda.Stream, "synchronize", sync)
+    with pytest.raises(RuntimeError, match="copy failed"):
+        fa.FedAvg.aggregate(models, c.weights)
+    assert calls, "the stream was not synchronised on the error path"
+    monkeypatch.undo()
+    _check_case_output(c, fa.FedAvg.aggregate(models, c.weights), "cpu")
+
+
 def _seq_mean(arrs, dtype):
     acc = np.zeros_like(arrs[0])
     for a in arrs:

@@ -113,6 +113,36 @@ def test_fedavg_multi_device_path_bit_exact():
         assert same_bits(gc.from_torch(p, c.dtype), want, c.dtype), i
 
 
+def _freed_peers_case(devs, peer_dev):
+    """Peers dropped right after the sharded call and their memory reused at once on the peers'
+    device: the result must still be the average of the ORIGINAL values (the peer
+    device's current stream waits for the shards that read it)."""
+    from accdfl_amd.core import wsum
+
+    n, numel = 8, 4_000_037
+    host = _peers(n, numel, "f32", 77)
+    w = [float(x) for x in np.random.default_rng(77).dirichlet(np.ones(n))]
+    want = c_wsum([p.numpy() for p in host], w, "f32")
+    side = torch.cuda.Stream(peer_dev)
+    with torch.cuda.stream(side):  # the caller works on a side stream of the peers' device
+        peers = [p.to(peer_dev) for p in host]
+        out = wsum.wsum_sharded(peers, w, devs)
+        del peers
+        junk = [torch.full((numel,), float("nan"), device=peer_dev) for _ in range(n)]  # reuses the blocks
+    torch.cuda.synchronize()
+    del junk
+    assert same_bits(out.cpu().numpy(), want, "f32")
+
+
+def test_sharded_peers_freed_right_after_on_one_gpu():
+    _freed_peers_case([torch.device("cuda", 0)] * 3, torch.device("cuda", 0))
+
+
+@pytest.mark.skipif(torch.cuda.device_count() < 2, reason="needs two GPUs (xGMI peer reads)")
+def test_sharded_peers_freed_right_after_across_gpus():
+    _freed_peers_case([torch.device("cuda", 0), torch.device("cuda", 1)], torch.device("cuda", 1))
+
+
 @pytest.mark.skipif(torch.cuda.device_count() < 2, reason="needs two GPUs (xGMI peer reads)")
 def test_models_on_two_gpus_through_fedavg():
     """Peers really on two GPUs: FedAvg.aggregate takes the sharded multi-device path (peer

@@ -101,6 +101,39 @@ def test_device_model_manager_wire_round():
         assert same_bits(back[name].numpy(), want[name].numpy(), "f32"), name
 
 
+@pytest.mark.gpu
+def test_ingress_slot_is_never_reused_within_a_round():
+    """a registry entry removed mid-round must not hand its page-locked ingress buffer
+    to the next arrival while a live WirePeer still views another slot — slots only advance
+    within a round (the old choice, len(registry), reused the buffer of the last live peer)."""
+    from types import SimpleNamespace
+
+    from accdfl_amd.core import wire
+    from accdfl_amd.core.gradient_aggregation import GradientAggregationMethod
+    from accdfl_amd.core.model_manager import DeviceModelManager
+
+    template = nn.Linear(300, 200)
+    payloads = []
+    for k in range(4):
+        torch.manual_seed(k)
+        payloads.append(wire.serialize_model(nn.Linear(300, 200)))
+    mm = DeviceModelManager(None, SimpleNamespace(gradient_aggregation=GradientAggregationMethod.FEDAVG),
+                            template=template, capacity=4)
+    for k in range(3):
+        mm.process_incoming_serialized(b"peer%d" % k, wire.payload_blocks(payloads[k], 1000))
+    live = mm.incoming_trained_models[b"peer2"]
+    before = {k: v.clone() for k, v in live.state_dict.items()}
+    del mm.incoming_trained_models[b"peer1"]  # removed mid-round
+    mm.process_incoming_serialized(b"peer3", wire.payload_blocks(payloads[3], 1000))
+    torch.cuda.synchronize()
+    for k, v in before.items():
+        assert torch.equal(live.state_dict[k], v), k
+    # the next round starts over at slot 0 (the buffers are reused, not grown without bound)
+    mm.reset_incoming_trained_models()
+    mm.process_incoming_serialized(b"peer0", wire.payload_blocks(payloads[0], 1000))
+    assert mm._ingress_next == 1 and len(mm._ingress) == 4
+
+
 @pytest.mark.filterwarnings("ignore:TypedStorage is deprecated")
 def test_storage_blob_fast_path_and_fallback():
     """The nested storage blobs are parsed in place (no torch.load pass); a blob in any
