@@ -130,6 +130,8 @@ def parse():
                     help="do not restrict each rank's CPUs to its GPU's NUMA node (host_memory.bind_to_gpu_node)")
     ap.add_argument("--host-configs-only", action="store_true",
                     help="print the per-config host-inclusive table (CPU modules, real layouts), then exit")
+    ap.add_argument("--device-configs-only", action="store_true",
+                    help="print the device-resident module rounds (FedAvg.aggregate on HBM modules), then exit")
     ap.add_argument("--configs-only", action="store_true",
                     help="print the per-BASELINE-config device-resident table (no CPU legs), then exit")
     ap.add_argument("--sweep-cfgs", default="", help="variant,chunks,grid;... (default: built-in list)")
@@ -991,6 +993,108 @@ def host_inclusive_configs(reps=3):
     return res
 
 
+# (layout, peers, dtype) of the device-resident module rounds: FedAvg.aggregate on modules that live in
+# HBM (models trained on the GPU; the simulators' averages), the reference layouts at their peer counts
+DEVICE_CONFIGS = {
+    "configs[1] CIFAR-10 GNLeNet, 8 peers": ("gnlenet", 8, "f32"),
+    "configs[2] FEMNIST CNN, 32 peers": ("femnist_cnn", 32, "f32"),
+    "configs[3] CIFAR-10 GNLeNet, 64 peers (whole model)": ("gnlenet", 64, "f32"),
+    "configs[3'] CIFAR-10 ResNet-8, 64 peers (whole model)": ("cifar10_resnet8", 64, "f32"),
+    "configs[4] google_speech ResNet-34, 16 peers, bf16": ("google_speech_resnet34", 16, "bf16"),
+    "configs[4] google_speech ResNet-34, 128 peers, bf16 (whole model)": ("google_speech_resnet34", 128, "bf16"),
+}
+
+
+def _device_layout_models(name, n, dt, device, seed=4100):
+    """n device-resident modules with the layout `name` (one tensor per parameter, allocated apart
+    as .to(device) of a trained model leaves them), BN buffers as the reference models carry them."""
+    from torch import nn
+
+    shapes, bufs = _layout(name)
+    numels = [int(np.prod(s)) if s else 1 for s in shapes]
+    base = torch.randn(sum(numels), generator=torch.Generator().manual_seed(seed)).to(device) * 0.05
+    models = []
+    for k in range(n):
+        flat = (base * (1.0 + 0.001 * k)).to(dt)
+        m = nn.Module()
+        m.ps = nn.ParameterList([nn.Parameter(t.view(s).clone()) for t, s in zip(flat.split(numels), shapes)])
+        for j, (s, bdt) in enumerate(bufs):
+            m.register_buffer("b%d" % j, torch.zeros(s, dtype=getattr(torch, bdt), device=device))
+        models.append(m)
+        del flat
+    return models, sum(numels)
+
+
+def device_module_configs(device, reps=10):
+    """FedAvg.aggregate on DEVICE-resident modules of the reference layouts (the
+    reference walks every parameter of every model, fedavg.py:24; the simulators average many
+    models, simulations/gl/gl_simulation.py:96-105), beside the flat PeerSlab reduce of the same
+    bytes.  Per config:
+      * end_to_end_ms: the whole FedAvg.aggregate call (parameter walk, deepcopy of models[0], pointer
+        table, reduce) until the result is ready (synchronised);
+      * layout_walk_ms: of which the one-pass walk over every parameter of every model
+        (fedavg._device_layout: shapes, dtype, device, contiguity, pointers);
+      * reduce_us: the device reduce alone, back to back on the walked layout (HIP events over the
+        timed region): the table's H2D copy + one wsum_multi_vec_kernel launch per 128-peer pass;
+      * per_tensor_reduce_us: the same reduce through the round-2 path (dla_wsum_multi: tensors packed
+        32 per launch up to 32 peers, one launch per tensor above);
+      * flat_slab_us: the tile-interleaved PeerSlab reduce of the same (N + 1) x P x s bytes
+        (what DeviceModelManager reduces), HIP events over a prepared launch."""
+    import ctypes
+
+    from accdfl_amd.core import wsum
+    from accdfl_amd.core.gradient_aggregation import fedavg as fa
+
+    res = {}
+    for name, (lay, n, dts) in DEVICE_CONFIGS.items():
+        log("device modules: " + name)
+        dt = torch.float32 if dts == "f32" else torch.bfloat16
+        es = 4 if dts == "f32" else 2
+        models, p = _device_layout_models(lay, n, dt, device)
+        w = [float(x) for x in np.random.default_rng(n).dirichlet(np.ones(n))]
+        byts = (n + 1) * p * es
+
+        def e2e():
+            fa.FedAvg.aggregate(models, w)
+            torch.cuda.synchronize()
+
+        row = {"peers": n, "params": p, "dtype": dts, "tensors": len(list(models[0].parameters())),
+               "bytes": byts, "end_to_end_ms": _median_ms(e2e, reps),
+               "layout_walk_ms": _median_ms(lambda: fa._device_layout(models), reps)}
+        dtype_, dev_, numels, table = fa._device_layout(models)
+        center = fa._center_copy(models[0])
+        outs = (ctypes.c_void_p * len(numels))(*[c.data_ptr() for c in center.parameters()])
+        nums = (ctypes.c_int64 * len(numels))(*numels)
+        ptrs = (ctypes.c_void_p * table.size).from_buffer(table)
+        steps = 20 if byts > (256 << 20) else 100
+
+        def reduce_once():
+            wsum.wsum_multi_ptrs(dt, ptrs, outs, nums, w, device)
+
+        ev = statistics.median(time_kernel(reduce_once, steps, 5, 1, settle_s=0.05)[1] for _ in range(3))
+        row["reduce_us"] = round(ev / steps * 1e6, 2)
+        row["reduce_GB/s"] = round(byts / (ev / steps) / 1e9, 1)
+        old = wsum.MULTI_TABLE_MIN_PEERS, wsum.MULTI_TABLE_MIN_BYTES
+        wsum.MULTI_TABLE_MIN_PEERS = wsum.MULTI_TABLE_MIN_BYTES = 1 << 62
+        try:
+            ev = statistics.median(time_kernel(reduce_once, steps, 5, 1, settle_s=0.05)[1] for _ in range(3))
+        finally:
+            wsum.MULTI_TABLE_MIN_PEERS, wsum.MULTI_TABLE_MIN_BYTES = old
+        row["per_tensor_reduce_us"] = round(ev / steps * 1e6, 2)
+        del models, center
+        torch.cuda.empty_cache()
+        inp = SlabInput(n, p, dt, device, 1000, w)
+        sp = torch.cuda.current_stream().cuda_stream
+        ev = statistics.median(time_kernel(lambda: inp.launch(sp), steps, 5, 1, settle_s=0.05)[1] for _ in range(3))
+        row["flat_slab_us"] = round(ev / steps * 1e6, 2)
+        row["reduce_over_flat_slab"] = round(row["reduce_us"] / row["flat_slab_us"], 3)
+        row["regime"] = "HBM" if byts > (256 << 20) else "Infinity-Cache / launch-latency"
+        del inp
+        torch.cuda.empty_cache()
+        res[name] = row
+    return res
+
+
 def cpu_layout_configs(budget_s=2.0):
     """The reference op sequence (oracle port of fedavg.py:13-26, torch-CPU, T tensors per
     model) on the pageable modules of host_inclusive_configs."""
@@ -1649,6 +1753,10 @@ def main():
         for name, row in host_inclusive_configs().items():
             print(json.dumps(dict(config=name, **row)), flush=True)
         return
+    if args.device_configs_only:
+        for name, row in device_module_configs(device).items():
+            print(json.dumps(dict(config=name, **row)), flush=True)
+        return
     if args.configs_only:
         for name, row in baseline_configs(device).items():
             print(json.dumps(dict(config=name, **row)))
@@ -1786,6 +1894,8 @@ def main():
     if rank == 0 and world == 1:
         if not args.no_small:
             result["baseline_configs"] = legs.run("baseline_configs", lambda L: baseline_configs(device))
+            result["device_module_configs"] = legs.run("device_module_configs",
+                                                       lambda L: device_module_configs(device))
         if not args.no_host_inclusive and args.dtype == "f32":
             result["host_inclusive"] = legs.run("host_inclusive", lambda L: host_inclusive(n, p))
             result["wire_ingress"] = legs.run("wire_ingress", lambda L: wire_ingress(p, device))

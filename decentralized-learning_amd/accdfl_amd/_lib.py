@@ -23,7 +23,7 @@ LIB_PATH = os.environ.get("DLAGG_LIB", os.path.join(PKG_ROOT, "lib", "libdlagg.s
 
 # dtype codes (include/dlagg.h)
 DLA_F32, DLA_BF16, DLA_F16, DLA_F64 = 0, 1, 2, 3
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 HIPCC_FLAGS = [
     "--offload-arch=gfx950",
@@ -59,6 +59,8 @@ EXPORTED = (
     "dla_host_round_start",
     "dla_host_round_finish",
     "dla_host_reduce",
+    "dla_wsum_multi_table_bytes",
+    "dla_wsum_multi_table",
 )
 
 
@@ -193,6 +195,12 @@ class _Lib:
                                        ctypes.POINTER(vp), ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, vp, vp,
                                        vp, vp, vp, vp]
         so.dla_host_reduce.restype = ctypes.c_int
+        so.dla_wsum_multi_table_bytes.argtypes = [ctypes.c_int, ctypes.c_int]
+        so.dla_wsum_multi_table_bytes.restype = ctypes.c_int64
+        so.dla_wsum_multi_table.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(vp), ctypes.POINTER(vp),
+                                            ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_double),
+                                            ctypes.c_int, vp, vp, vp]
+        so.dla_wsum_multi_table.restype = ctypes.c_int
         so.dla_plan_destroy.argtypes = [vp]
         so.dla_plan_destroy.restype = None
         v = so.dla_version()
@@ -287,15 +295,42 @@ def wsum_slab_ptr(dtype_code: int, base_ptr: int, pitch_elems: int, weights: Seq
 
 def wsum_multi_ptrs(dtype_code: int, peer_ptrs: Sequence[int], out_ptrs: Sequence[int], numels: Sequence[int],
                     weights: Sequence[float], stream_ptr: int) -> None:
-    """peer_ptrs is [n_tensors * n_peers] (tensor-major)."""
+    """peer_ptrs is [n_tensors * n_peers] (tensor-major); sequences or ctypes arrays."""
     L = lib()
     t = len(out_ptrs)
     n = len(weights)
-    assert len(peer_ptrs) == t * n
-    num = (ctypes.c_int64 * t)(*[int(x) for x in numels])
-    rc = L.so.dla_wsum_multi(dtype_code, t, _ptr_array(peer_ptrs), _ptr_array(out_ptrs), num, _dbl_array(weights),
-                             n, stream_ptr)
+    if len(peer_ptrs) != t * n:
+        raise ValueError("peer_ptrs must hold n_tensors * n_peers pointers")
+    num = numels if isinstance(numels, ctypes.Array) else (ctypes.c_int64 * t)(*[int(x) for x in numels])
+    pa = peer_ptrs if isinstance(peer_ptrs, ctypes.Array) else _ptr_array(peer_ptrs)
+    oa = out_ptrs if isinstance(out_ptrs, ctypes.Array) else _ptr_array(out_ptrs)
+    rc = L.so.dla_wsum_multi(dtype_code, t, pa, oa, num, _dbl_array(weights), n, stream_ptr)
     L.check(rc, "dla_wsum_multi")
+
+
+def wsum_multi_table_bytes(n_tensors: int, n_peers: int) -> int:
+    """dla_wsum_multi_table_bytes: size of the device table of a dla_wsum_multi_table call."""
+    return int(lib().so.dla_wsum_multi_table_bytes(n_tensors, n_peers))
+
+
+def wsum_multi_table_ptrs(dtype_code: int, peer_ptrs, out_ptrs, numels, weights: Sequence[float], table_host: int,
+                          table_dev: int, stream_ptr: int) -> None:
+    """dla_wsum_multi_table: peer_ptrs is [n_tensors * n_peers] (tensor-major); sequences or ctypes arrays."""
+    L = lib()
+    n = len(weights)
+    if not isinstance(out_ptrs, ctypes.Array):
+        out_ptrs = _ptr_array(out_ptrs)
+    t = len(out_ptrs)
+    if not isinstance(peer_ptrs, ctypes.Array):
+        peer_ptrs = (ctypes.c_void_p * len(peer_ptrs))(*peer_ptrs)
+    if len(peer_ptrs) != t * n:
+        raise ValueError("peer_ptrs must hold n_tensors * n_peers pointers")
+    if not isinstance(numels, ctypes.Array):
+        numels = (ctypes.c_int64 * t)(*[int(x) for x in numels])
+    rc = L.so.dla_wsum_multi_table(dtype_code, t, peer_ptrs, out_ptrs, numels, _dbl_array(weights), n, table_host,
+                                   table_dev, stream_ptr)
+    if rc != 0:
+        L.check(rc, "dla_wsum_multi_table")
 
 
 def host_copy_batch(dst_ptrs: Sequence[int], src_ptrs: Sequence[int], nbytes: Sequence[int]) -> None:

@@ -261,6 +261,57 @@ def _host_layout(models: List[nn.Module]):
     return dtype, [p.numel() for p in p0], ptrs
 
 
+def _device_layout(models: List[nn.Module]):
+    """(dtype, device, numels, tensor-major pointer table) of a round whose models all have models[0]'s
+    parameter shapes, one supported dtype and contiguous storage on ONE HIP device (models trained on
+    the GPU, the simulator's device-resident averages), gathered in one pass; None otherwise (the
+    general path handles it).  The table is [n_tensors x n_peers] uint64, as dla_wsum_multi takes it."""
+    import numpy as np
+
+    p0 = list(models[0].parameters())
+    if not p0 or not p0[0].is_cuda:
+        return None
+    dtype = p0[0].dtype
+    if dtype not in _wsum.SUPPORTED_DTYPES:
+        return None
+    dev = p0[0].get_device()
+    shapes = [p.shape for p in p0]
+    n_t = len(shapes)
+    rows = []
+    for m in models:
+        ps = p0 if m is models[0] else list(m.parameters())
+        if len(ps) != n_t:
+            return None
+        row = []
+        add = row.append
+        for p, shape in zip(ps, shapes):
+            if p.shape != shape or p.dtype is not dtype or p.get_device() != dev or not p.is_contiguous():
+                return None
+            add(p.data_ptr())
+        rows.append(row)
+    table = np.ascontiguousarray(np.array(rows, dtype=np.uint64).T)
+    return dtype, torch.device("cuda", dev), [p.numel() for p in p0], table
+
+
+def _device_round(models: List[nn.Module], weights, layout) -> "nn.Module | None":
+    """The whole aggregate for device-resident models of one layout: deepcopy(models[0]) with fresh
+    parameters (fedavg.py:20), then every parameter of every model folded straight into them by
+    dla_wsum_multi(_table) from one pointer table — one launch per 128-peer pass for rounds of many
+    peers, whatever the tensor count (fedavg.py:23-25).  Stream-ordered like any torch op."""
+    dtype, device, numels, table = layout
+    # the result's parameters first, the reduce into them next, the module tree last: the table's
+    # copy and the kernel run while the host clones the module (deepcopy of models[0], fedavg.py:20)
+    memo = _fresh_params(models[0])
+    params = [memo[id(p)] for p in models[0].parameters()] if len(memo) == len(numels) else []
+    if len(params) != len(numels) or not all(c.is_contiguous() and c.device == device for c in params):
+        return None
+    ptrs = (ctypes.c_void_p * table.size).from_buffer(table)
+    outs = (ctypes.c_void_p * len(params))(*[c.data_ptr() for c in params])
+    nums = (ctypes.c_int64 * len(numels))(*numels)
+    _wsum.wsum_multi_ptrs(dtype, ptrs, outs, nums, weights, device)
+    return _clone_value(models[0], memo)
+
+
 def _small_round(models: List[nn.Module], weights, layout) -> "nn.Module | None":
     """The whole aggregate for a small round of same-layout, one-dtype, contiguous CPU
     models (the reference's call sites: GL merges N=2 every round): one native call packs
@@ -743,6 +794,13 @@ def _center_copy(model0: nn.Module, large: bool = True) -> nn.Module:
     Buffers and every other attribute are deep-copied exactly as in the reference (the module
     tree through _clone_value, deepcopy's protocol without its per-object dispatch: the GL
     merge of two GNLeNet models builds this copy every round)."""
+    return _clone_value(model0, _fresh_params(model0, large))
+
+
+def _fresh_params(model0: nn.Module, large: bool = True) -> dict:
+    """The deepcopy memo _center_copy seeds: id(parameter) -> a fresh, uninitialised nn.Parameter of
+    the same shape, strides, dtype, device and requires_grad (nn.Parameter subclasses are left to
+    the stock deepcopy)."""
     memo = {}
     for p in model0.parameters():
         if id(p) in memo or type(p) is not nn.Parameter:
@@ -755,7 +813,7 @@ def _center_copy(model0: nn.Module, large: bool = True) -> nn.Module:
         else:
             data = torch.empty_strided(p.size(), p.stride(), dtype=p.dtype, device=p.device)
         memo[id(p)] = nn.Parameter(data, p.requires_grad)
-    return _clone_value(model0, memo)
+    return memo
 
 
 class FedAvg(GradientAggregation):
@@ -776,6 +834,12 @@ class FedAvg(GradientAggregation):
                         done = _large_round(models, list(weights), layout)
                     if done is not None:
                         return done
+                else:
+                    dev_layout = _device_layout(models)
+                    if dev_layout is not None:
+                        done = _device_round(models, list(weights), dev_layout)
+                        if done is not None:
+                            return done
             center_model = _center_copy(models[0])
             reduce_parameters(list(center_model.parameters()), [list(m.parameters()) for m in models],
                               list(weights))

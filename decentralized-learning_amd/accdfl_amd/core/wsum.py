@@ -8,6 +8,7 @@ tensors' device and is NOT synchronised (torch stream semantics).
 """
 from __future__ import annotations
 
+import os
 from typing import List, Optional, Sequence
 
 import torch
@@ -119,7 +120,6 @@ def wsum_multi(peer_params: Sequence[Sequence[torch.Tensor]], weights: Sequence[
         return
     n = len(peer_params)
     device = require_device(outs[0].device)
-    code = dtype_code(outs[0].dtype)
     ptrs: List[int] = []
     for i, o in enumerate(outs):
         _check_dev(o, device, "out %d" % i)
@@ -131,8 +131,79 @@ def wsum_multi(peer_params: Sequence[Sequence[torch.Tensor]], weights: Sequence[
             if p.numel() != o.numel() or p.dtype != o.dtype:
                 raise ValueError("peer %d tensor %d: numel/dtype mismatch" % (k, i))
             ptrs.append(p.data_ptr())
-    _lib.wsum_multi_ptrs(code, ptrs, [o.data_ptr() for o in outs], [o.numel() for o in outs], weights,
-                         _stream_ptr(device, stream))
+    wsum_multi_ptrs(outs[0].dtype, ptrs, [o.data_ptr() for o in outs], [o.numel() for o in outs], weights, device,
+                    stream)
+
+
+# Rounds of at least MULTI_TABLE_MIN_PEERS peers — or of more than 8 peers moving at least
+# MULTI_TABLE_MIN_BYTES — reduce every aligned tensor in one launch per 128-peer pass through a
+# device-side pointer table (dla_wsum_multi_table); other rounds pack up to 32 small tensors per
+# launch with the pointers in the kernel arguments (dla_wsum_multi), which needs no table copy.
+# Interleaved A/B on MI355X (profiles/r03e/, us, table / kernel-argument path, flat slab beside):
+# 128 x ResNet-34 bf16 865 / 1851 (813); 64 x ResNet-8 f32 219 / 310 (192); 64 x GNLeNet 14 / 48
+# (4.3); 16 x ResNet-34 bf16 (724 MB) 134 / 165 (106); but 32 x FEMNIST (223 MB) 41.3 / 35.2 (32.1)
+# and 8 x GNLeNet 13.0 / 6.3 (3.3), where the table's copy costs more than it saves.
+MULTI_TABLE_MIN_PEERS = int(os.environ.get("ACCDFL_AMD_MULTI_TABLE_MIN_PEERS", "33"))
+MULTI_TABLE_MIN_BYTES = 256 << 20
+
+
+class _TableRing:
+    """Page-locked host + device buffers for dla_wsum_multi_table's table, a few slots per device
+    used round-robin; a slot is refilled only after the stream that last read it has passed that
+    call (its event), so back-to-back rounds never overwrite a table still being copied or read."""
+
+    SLOTS = 4
+
+    def __init__(self, device: torch.device):
+        self.device = device
+        self.slots = [None] * self.SLOTS  # (host uint8, device uint8, event or None)
+        self.i = 0
+
+    def take(self, nbytes: int):
+        self.i = (self.i + 1) % self.SLOTS
+        slot = self.slots[self.i]
+        if slot is not None and slot[2] is not None:
+            slot[2].synchronize()
+        if slot is None or slot[0].numel() < nbytes:
+            size = max(nbytes, 64 << 10)
+            size = 1 << (size - 1).bit_length()
+            slot = (torch.empty(size, dtype=torch.uint8, pin_memory=True),
+                    torch.empty(size, dtype=torch.uint8, device=self.device), None)
+            self.slots[self.i] = slot
+        return slot
+
+    def done(self, stream: torch.cuda.Stream):
+        h, d, _ = self.slots[self.i]
+        ev = torch.cuda.Event()
+        ev.record(stream)
+        self.slots[self.i] = (h, d, ev)
+
+
+_rings = {}
+
+
+def wsum_multi_ptrs(dtype: torch.dtype, ptrs, out_ptrs, numels, weights: Sequence[float], device: torch.device,
+                    stream: Optional[torch.cuda.Stream] = None) -> None:
+    """wsum_multi on raw pointers the caller has validated (device-resident, contiguous, one dtype,
+    numels[i] elements each; ptrs tensor-major [n_tensors * n_peers]).  Rounds of more than
+    MULTI_TABLE_MIN_PEERS - 1 peers go through dla_wsum_multi_table (one launch per 128-peer pass)."""
+    code = dtype_code(dtype)
+    n = len(weights)
+    s = stream if stream is not None else torch.cuda.current_stream(device)
+    table = n >= MULTI_TABLE_MIN_PEERS or (
+        n > 8 and (n + 1) * sum(numels) * torch.empty((), dtype=dtype).element_size() >= MULTI_TABLE_MIN_BYTES)
+    if table and dtype != torch.float64:
+        ring = _rings.get(device)
+        if ring is None:
+            ring = _rings[device] = _TableRing(device)
+        h, d, _ = ring.take(_lib.wsum_multi_table_bytes(len(out_ptrs), n))
+        try:
+            _lib.wsum_multi_table_ptrs(code, ptrs, out_ptrs, numels, weights, h.data_ptr(), d.data_ptr(),
+                                       int(s.cuda_stream))
+        finally:
+            ring.done(s)
+        return
+    _lib.wsum_multi_ptrs(code, ptrs, out_ptrs, numels, weights, int(s.cuda_stream))
 
 
 def wsum_sharded(peers: Sequence[torch.Tensor], weights: Sequence[float], devices: Sequence[torch.device],

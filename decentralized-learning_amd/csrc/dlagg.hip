@@ -762,9 +762,19 @@ __device__ inline void store_vec_sc1(u32x4* p, u32x4 v) {
   asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
 }
 
-template <int DT, int KMAX, int G, int VW, bool FULL, bool ACC_IN>
+// A peer pointer as a global-address-space pointer: global_load (not flat_load) whatever the pointer
+// came from (the kernel-argument table is promoted to global by the backend; a pointer read from a
+// device-side table is not).
+template <class T>
+__device__ __attribute__((always_inline)) inline const __attribute__((address_space(1))) T* gptr(const void* p) {
+  return (const __attribute__((address_space(1))) T*)(p);
+}
+
+// TAB: anything with tab.p[k] (peer pointers) and tab.w[k] (op-math weights): the kernel-argument
+// PeerTable, or a PeerRef into a device-side pointer table (wsum_multi_vec_kernel).
+template <int DT, int KMAX, int G, int VW, bool FULL, bool ACC_IN, class TAB>
 __device__ __attribute__((always_inline)) inline void vec_round(
-    const PeerTable<typename Ops<DT>::w_t, KMAX>& tab, int k0, int m, bool first_round, int64_t a,
+    const TAB& tab, int k0, int m, bool first_round, int64_t a,
     typename Ops<DT>::acc_t (&acc)[VW][Ops<DT>::WE]) {
   using V = typename VecOf<VW>::T;
   V v[G];
@@ -772,7 +782,7 @@ __device__ __attribute__((always_inline)) inline void vec_round(
   for (int g = 0; g < G; ++g) {
     // partial round: slots past the last peer reload it (cached; branch-free issue)
     const int k = FULL || g < m ? k0 + g : k0 + m - 1;
-    v[g] = __builtin_nontemporal_load(static_cast<const V*>(tab.p[k]) + a);
+    v[g] = __builtin_nontemporal_load(gptr<V>(tab.p[k]) + a);
   }
   typename Ops<DT>::w_t wk[G];
 #pragma unroll
@@ -792,9 +802,9 @@ __device__ __attribute__((always_inline)) inline void vec_round(
 // profiles/r02v_ab_tail.log, tiled slab, us): 2 x 25 M f32 72.4 -> 44.5, 4 x 25 M f32 82.3 ->
 // 73.8, 12 x 11.2 M f32 88.5 -> 84.8, 20 x 5 M f32 73.1 -> 61.0, 48 x 1.23 M f32 39.0 -> 35.0,
 // 100 x 2.66 M bf16 83.3 -> 79.6, 3 x 50 M bf16 77.4 -> 64.0 (separate buffers alike).
-template <int DT, int KMAX, int G, int VW, bool ACC_IN>
+template <int DT, int KMAX, int G, int VW, bool ACC_IN, class TAB>
 __device__ __attribute__((always_inline)) inline void vec_tail(
-    const PeerTable<typename Ops<DT>::w_t, KMAX>& tab, int k0, int m, bool first_round, int64_t a,
+    const TAB& tab, int k0, int m, bool first_round, int64_t a,
     typename Ops<DT>::acc_t (&acc)[VW][Ops<DT>::WE]) {
   if constexpr (G > 1) {
     constexpr int H = G / 2;
@@ -856,6 +866,131 @@ __global__ __launch_bounds__(64) void wsum_vec_kernel(
     for (int d = 0; d < VW; ++d) o[d] = O::pack_w(acc[d]);
     if constexpr (PLAIN_ST)
       out[i] = o;
+    else
+      store_vec_sc1(out + i, o);
+  }
+}
+
+// ------------------------------------------------ many-peer multi-tensor kernel
+// dla_wsum_multi_table: every 16-byte aligned parameter tensor of a round (fedavg.py:24 walks them
+// one by one) over a pass of up to 128 peers in ONE launch.  The (tensor x peer) pointer table does
+// not fit the kernel-argument block (128 google_speech ResNet-34 models: 14 080 pointers), so it
+// travels to the device as one table per call (one H2D copy on the stream).  Workgroup b finds its
+// tensor from the tensors' first workgroups (uniform: scalar loads), then folds 64 vectors of it
+// exactly as wsum_vec_kernel does (8 bytes per lane, G peers' loads in flight, list order); a tensor
+// with a ragged tail has one more workgroup, which runs fold_tail.  A launch covers up to 256 tensors.
+struct MultiSeg {
+  int64_t wg_begin;         // first workgroup of this tensor in the launch
+  int64_t n_vecs;           // whole 8-byte vectors of the tensor
+  int64_t n_elems;
+  void* out;
+  const void* const* ptrs;  // this tensor's row of the device pointer table (n_peers entries)
+};
+
+// The tensors' first workgroups for the two-level search: coarse[q] = fine[16 q]; entries past the
+// last tensor are INT32_MAX.  Workgroup b counts the coarse entries <= b (one s_load_dwordx16), then
+// the fine entries <= b in that block of 16 (one more): two dependent scalar loads instead of the
+// eight of a binary search over 256 tensors.
+struct MultiIndex {
+  int32_t coarse[16];
+  int32_t fine[256];
+};
+constexpr int kMultiTensorsPerLaunch = 256;
+
+// One row of the device pointer table, read through the constant address space: the table is never
+// written while the kernel runs, and uniform reads of it then become scalar loads (s_load_dwordx16
+// batches, as from the kernel-argument table) instead of a vector load per pointer per lane.
+typedef const void* PeerPtr;
+typedef const __attribute__((address_space(4))) PeerPtr* ConstPeerTab;
+typedef const __attribute__((address_space(4))) int32_t* ConstI32;
+
+template <typename W>
+struct PeerRef {  // the PeerTable interface (tab.p[k], tab.w[k]) over one row of the device table
+  ConstPeerTab p;
+  const W* __restrict__ w;
+};
+
+// SEARCH 1: the two-level count over MultiIndex; 0: a binary search over segs[].wg_begin.
+template <int SEARCH>
+__device__ __attribute__((always_inline)) inline int multi_segment(const MultiIndex* idx, const MultiSeg* segs,
+                                                                   int n_seg, int b) {
+  if constexpr (SEARCH == 1) {
+    const ConstI32 cz = (ConstI32)(idx->coarse);
+    int c = 0;
+#pragma unroll
+    for (int q = 1; q < 16; ++q) c += cz[q] <= b ? 1 : 0;
+    const ConstI32 fz = (ConstI32)(idx->fine + 16 * c);
+    int t = 16 * c;
+#pragma unroll
+    for (int q = 1; q < 16; ++q) t += fz[q] <= b ? 1 : 0;
+    return t;
+  } else {
+    int lo = 0, hi = n_seg - 1;  // the last tensor whose first workgroup is <= b
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (segs[mid].wg_begin <= b)
+        lo = mid;
+      else
+        hi = mid - 1;
+    }
+    return lo;
+  }
+}
+
+template <typename W, int KMAX>
+struct WeightTable {
+  W w[KMAX];
+};
+
+template <int DT, int KMAX, int G, bool ACC_IN, bool PLAIN_ST, int SEARCH>
+__global__ __launch_bounds__(64) void wsum_multi_vec_kernel(const MultiIndex* __restrict__ idx,
+                                                            const MultiSeg* __restrict__ segs, int n_seg, int k0,
+                                                            int n_peers,
+                                                            const WeightTable<typename Ops<DT>::w_t, KMAX> wt) {
+  static_assert(DT != DLA_F64, "dword folds: f32 / bf16 / f16");
+  using O = Ops<DT>;
+  using acc_t = typename O::acc_t;
+  constexpr int VW = 2;
+  using V = typename VecOf<VW>::T;
+  constexpr int WE = O::WE;
+  const int64_t b = blockIdx.x;
+  const int lo = multi_segment<SEARCH>(idx, segs, n_seg, static_cast<int>(blockIdx.x));
+  const int64_t n_vecs = segs[lo].n_vecs;
+  const int64_t local = b - segs[lo].wg_begin;
+  const PeerRef<typename O::w_t> tab{(ConstPeerTab)(segs[lo].ptrs + k0), wt.w};
+  void* const out_v = segs[lo].out;
+  if (local >= (n_vecs + 63) / 64) {  // this tensor's ragged-tail workgroup
+    fold_tail<DT, ACC_IN>(segs[lo].ptrs + k0, tab.w, n_peers, n_vecs * VW * WE, segs[lo].n_elems, out_v);
+    return;
+  }
+  const int64_t j = local * 64 + threadIdx.x;
+  const bool live = j < n_vecs;
+  const int64_t i = live ? j : n_vecs - 1;  // clamped: loads stay unpredicated
+  V* out = static_cast<V*>(out_v);
+  __attribute__((address_space(1))) V* gout = (__attribute__((address_space(1))) V*)out_v;  // global_* access
+  acc_t acc[VW][WE];
+  if constexpr (ACC_IN) {
+    const V o = gout[i];
+#pragma unroll
+    for (int d = 0; d < VW; ++d) O::unpack_w(o[d], acc[d]);
+  }
+#pragma unroll
+  for (int r = 0; r < (KMAX + G - 1) / G; ++r) {
+    const int r0 = r * G;
+    if (r0 >= n_peers) break;
+    if (r0 + G <= n_peers) {
+      vec_round<DT, KMAX, G, VW, true, ACC_IN>(tab, r0, G, r == 0, i, acc);
+    } else {
+      vec_tail<DT, KMAX, G, VW, ACC_IN>(tab, r0, n_peers - r0, r == 0, i, acc);
+      break;
+    }
+  }
+  if (live) {
+    V o;
+#pragma unroll
+    for (int d = 0; d < VW; ++d) o[d] = O::pack_w(acc[d]);
+    if constexpr (PLAIN_ST)
+      gout[i] = o;
     else
       store_vec_sc1(out + i, o);
   }
@@ -1435,6 +1570,111 @@ hipError_t run_multi_dt(const std::vector<int>& packed, const void* const* peer_
   return run_multi<DT, 32, 8>(packed, peer_ptrs, outs, numels, weights, n, s);
 }
 
+// dla_wsum_multi_table: the device table is, per launch of up to 256 tensors, [MultiIndex][MultiSeg x mc]
+// (16-byte aligned), then the m x n_peers peer pointers of every tensor.
+int64_t multi_chunk_bytes(int mc) {
+  return static_cast<int64_t>(sizeof(MultiIndex)) + (static_cast<int64_t>(mc) * sizeof(MultiSeg) + 15) / 16 * 16;
+}
+
+int64_t multi_table_bytes(int n_tensors, int n_peers) {
+  int64_t b = 0;
+  for (int c0 = 0; c0 < n_tensors; c0 += kMultiTensorsPerLaunch)
+    b += multi_chunk_bytes(n_tensors - c0 < kMultiTensorsPerLaunch ? n_tensors - c0 : kMultiTensorsPerLaunch);
+  return b + static_cast<int64_t>(n_tensors) * n_peers * 8;
+}
+
+// DLA_MULTI_SEARCH=0: the binary search (A/B only); default 1, the two-level count
+int multi_search() {
+  static const int v = [] {
+    const char* e = std::getenv("DLA_MULTI_SEARCH");
+    return e && std::atoi(e) == 0 ? 0 : 1;
+  }();
+  return v;
+}
+
+template <int DT, int KMAX, int G, bool ACC_IN>
+hipError_t launch_multi_vec(const MultiIndex* idx, const MultiSeg* segs, int n_seg, int64_t grid, int k0, int pm,
+                            const double* weights, bool plain, hipStream_t s) {
+  using W = typename Ops<DT>::w_t;
+  WeightTable<W, KMAX> wt;
+  std::memset(&wt, 0, sizeof(wt));
+  for (int k = 0; k < pm; ++k) wt.w[k] = static_cast<W>(weights[k0 + k]);  // RNE double -> op-math
+  const dim3 g(static_cast<unsigned>(grid)), bl(64);
+#define DLA_MV(PL, SE) \
+  hipLaunchKernelGGL((wsum_multi_vec_kernel<DT, KMAX, G, ACC_IN, PL, SE>), g, bl, 0, s, idx, segs, n_seg, k0, pm, wt)
+  if (multi_search() == 1) {
+    if (plain) DLA_MV(true, 1); else DLA_MV(false, 1);
+  } else {
+    if (plain) DLA_MV(true, 0); else DLA_MV(false, 0);
+  }
+#undef DLA_MV
+  return hipGetLastError();
+}
+
+template <int DT, bool ACC_IN>
+hipError_t launch_multi_vec_pass(const MultiIndex* idx, const MultiSeg* segs, int n_seg, int64_t grid, int k0, int pm,
+                                 const double* weights, bool plain, hipStream_t s) {
+  // peers in flight per lane as the single-tensor vec kernel (vec_variant): 32 for passes of >= 32
+  // peers, 16 above 8, else 8
+  if (pm > 32)
+    return launch_multi_vec<DT, kMaxPeersPerPass, 32, ACC_IN>(idx, segs, n_seg, grid, k0, pm, weights, plain, s);
+  if (pm == 32) return launch_multi_vec<DT, 32, 32, ACC_IN>(idx, segs, n_seg, grid, k0, pm, weights, plain, s);
+  if (pm > 8) return launch_multi_vec<DT, 32, 16, ACC_IN>(idx, segs, n_seg, grid, k0, pm, weights, plain, s);
+  return launch_multi_vec<DT, 8, 8, ACC_IN>(idx, segs, n_seg, grid, k0, pm, weights, plain, s);
+}
+
+template <int DT>
+hipError_t run_multi_table(const std::vector<int>& packed, const void* const* peer_ptrs, void* const* outs,
+                           const int64_t* numels, const double* weights, int n, char* th, char* td, hipStream_t s) {
+  constexpr int per_vec = 2 * Ops<DT>::WE;  // elements per 8-byte vector
+  const int m = static_cast<int>(packed.size());
+  const int64_t ptab_off = multi_table_bytes(m, n) - static_cast<int64_t>(m) * n * 8;
+  const void** ptab = reinterpret_cast<const void**>(th + ptab_off);
+  int64_t out_bytes = 0;
+  for (int i = 0; i < m; ++i) out_bytes += numels[packed[i]] * static_cast<int64_t>(sizeof(typename Ops<DT>::elem_t));
+  // plain output stores for passes of >= 32 peers writing <= 8 MiB in all (vec_store_policy)
+  const bool plain_ok = out_bytes <= (int64_t{8} << 20);
+  struct Launch1 { int64_t off; int mc; int64_t grid; };
+  std::vector<Launch1> launches;
+  int64_t off = 0;
+  for (int c0 = 0; c0 < m; c0 += kMultiTensorsPerLaunch) {
+    const int mc = m - c0 < kMultiTensorsPerLaunch ? m - c0 : kMultiTensorsPerLaunch;
+    MultiIndex* ix = reinterpret_cast<MultiIndex*>(th + off);
+    MultiSeg* segs = reinterpret_cast<MultiSeg*>(th + off + sizeof(MultiIndex));
+    for (int q = 0; q < 256; ++q) ix->fine[q] = 0x7fffffff;
+    int64_t wg = 0;
+    for (int i = 0; i < mc; ++i) {
+      const int t = packed[c0 + i];
+      const int64_t nv = numels[t] / per_vec;
+      segs[i].wg_begin = wg;
+      segs[i].n_vecs = nv;
+      segs[i].n_elems = numels[t];
+      segs[i].out = outs[t];
+      segs[i].ptrs = reinterpret_cast<const void* const*>(td + ptab_off + static_cast<int64_t>(c0 + i) * n * 8);
+      std::memcpy(ptab + static_cast<int64_t>(c0 + i) * n, peer_ptrs + static_cast<int64_t>(t) * n, sizeof(void*) * n);
+      ix->fine[i] = static_cast<int32_t>(wg);
+      wg += (nv + 63) / 64 + (numels[t] > nv * per_vec ? 1 : 0);
+      if (wg > 0x7fffffff) return hipErrorInvalidValue;
+    }
+    for (int q = 0; q < 16; ++q) ix->coarse[q] = ix->fine[16 * q];
+    launches.push_back({off, mc, wg});
+    off += multi_chunk_bytes(mc);
+  }
+  hipError_t e = hipMemcpyAsync(td, th, static_cast<size_t>(multi_table_bytes(m, n)), hipMemcpyHostToDevice, s);
+  if (e != hipSuccess) return e;
+  for (int k0 = 0; k0 < n; k0 += kMaxPeersPerPass) {
+    const int pm = n - k0 < kMaxPeersPerPass ? n - k0 : kMaxPeersPerPass;
+    for (const Launch1& L : launches) {
+      const MultiIndex* ix = reinterpret_cast<const MultiIndex*>(td + L.off);
+      const MultiSeg* segs = reinterpret_cast<const MultiSeg*>(td + L.off + sizeof(MultiIndex));
+      e = k0 > 0 ? launch_multi_vec_pass<DT, true>(ix, segs, L.mc, L.grid, k0, pm, weights, plain_ok && pm >= 32, s)
+                 : launch_multi_vec_pass<DT, false>(ix, segs, L.mc, L.grid, k0, pm, weights, plain_ok && pm >= 32, s);
+      if (e != hipSuccess) return e;
+    }
+  }
+  return hipSuccess;
+}
+
 template <int DT, int KMAX>
 hipError_t mean_pass(const void* const* peers, int n, int n_total, int64_t n_elems, void* out, hipStream_t s,
                      bool acc_in, bool divide) {
@@ -1567,6 +1807,20 @@ int owner_device(const void* p) {
   }
   if (a.type != hipMemoryTypeDevice) return -1;
   return a.device;
+}
+
+bool is_pinned_host_ptr(const void* p) {
+  hipPointerAttribute_t a;
+  const bool ok = hipPointerGetAttributes(&a, p) == hipSuccess && a.type == hipMemoryTypeHost;
+  if (!ok) (void)hipGetLastError();
+  return ok;
+}
+
+bool is_device_ptr(const void* p) {
+  hipPointerAttribute_t a;
+  const bool ok = hipPointerGetAttributes(&a, p) == hipSuccess && a.type == hipMemoryTypeDevice;
+  if (!ok) (void)hipGetLastError();
+  return ok;
 }
 
 // Let `dev` read / write memory owned by `owner` (caller holds g_shard_mu; device set to dev).
@@ -1903,6 +2157,60 @@ int dla_wsum_multi(int dtype, int n_tensors, const void* const* peer_ptrs, void*
   return DLA_OK;
 }
 
+int64_t dla_wsum_multi_table_bytes(int n_tensors, int n_peers) {
+  if (n_tensors < 0 || n_peers < 1) return 0;
+  return multi_table_bytes(n_tensors, n_peers);
+}
+
+int dla_wsum_multi_table(int dtype, int n_tensors, const void* const* peer_ptrs, void* const* outs,
+                         const int64_t* numels, const double* weights, int n_peers, void* table_host,
+                         void* table_dev, void* stream) {
+  g_last_error.clear();
+  if (n_tensors < 0 || (n_tensors > 0 && (!peer_ptrs || !outs || !numels)))
+    return fail(DLA_E_INVALID, "dla_wsum_multi_table: bad tensor table");
+  const int es = elem_size(dtype);
+  if (es == 0) return fail(DLA_E_INVALID, "dla_wsum_multi_table: unknown dtype " + std::to_string(dtype));
+  if (n_peers < 1 || !weights) return fail(DLA_E_INVALID, "dla_wsum_multi_table: n_peers must be >= 1");
+  std::vector<int> packed;
+  for (int t = 0; t < n_tensors; ++t) {
+    if (numels[t] < 0) return fail(DLA_E_INVALID, "dla_wsum_multi_table: negative numel");
+    if (numels[t] == 0) continue;
+    const void* const* row = peer_ptrs + static_cast<int64_t>(t) * n_peers;
+    bool ok = dtype != DLA_F64 && outs[t] && (reinterpret_cast<uintptr_t>(outs[t]) & 15u) == 0;
+    for (int k = 0; ok && k < n_peers; ++k) ok = row[k] && (reinterpret_cast<uintptr_t>(row[k]) & 15u) == 0;
+    if (ok && n_peers > kMaxPeersPerPass)  // multi-pass: out carries the running sum (as dla_wsum)
+      for (int k = 1; ok && k < n_peers; ++k)
+        if (row[k] == outs[t])
+          return fail(DLA_E_ALIAS, "dla_wsum_multi_table: out of tensor " + std::to_string(t) + " aliases peer " +
+                                       std::to_string(k) + "; only peers[0] may alias out when n_peers > " +
+                                       std::to_string(kMaxPeersPerPass));
+    if (ok) {
+      packed.push_back(t);
+      continue;
+    }
+    const int rc = wsum_impl(dtype, row, weights, n_peers, numels[t], outs[t], stream, nullptr);
+    if (rc != DLA_OK) return rc;
+  }
+  if (packed.empty()) return DLA_OK;
+  if (!table_host || !table_dev) return fail(DLA_E_INVALID, "dla_wsum_multi_table: null table buffer");
+  if (!is_pinned_host_ptr(table_host))
+    return fail(DLA_E_INVALID, "dla_wsum_multi_table: table_host must be page-locked host memory (hipHostMalloc)");
+  if (!is_device_ptr(table_dev)) return fail(DLA_E_INVALID, "dla_wsum_multi_table: table_dev must be device memory");
+  if ((reinterpret_cast<uintptr_t>(table_host) & 15u) || (reinterpret_cast<uintptr_t>(table_dev) & 15u))
+    return fail(DLA_E_INVALID, "dla_wsum_multi_table: table buffers must be 16-byte aligned");
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  char* th = static_cast<char*>(table_host);
+  char* td = static_cast<char*>(table_dev);
+  hipError_t e;
+  switch (dtype) {
+    case DLA_F32: e = run_multi_table<DLA_F32>(packed, peer_ptrs, outs, numels, weights, n_peers, th, td, s); break;
+    case DLA_BF16: e = run_multi_table<DLA_BF16>(packed, peer_ptrs, outs, numels, weights, n_peers, th, td, s); break;
+    default: e = run_multi_table<DLA_F16>(packed, peer_ptrs, outs, numels, weights, n_peers, th, td, s); break;
+  }
+  if (e != hipSuccess) return fail(static_cast<int>(e), std::string("dla_wsum_multi_table: ") + hipGetErrorString(e));
+  return DLA_OK;
+}
+
 int dla_plan_create(dla_plan_t** plan, int dtype, const void* const* peers, const double* weights, int n_peers,
                     int64_t n_elems, void* out, const dla_launch_cfg_t* cfg) {
   g_last_error.clear();
@@ -2050,18 +2358,6 @@ int dla_host_round_finish(int dtype, int n_tensors, const int64_t* numels, const
 }
 
 namespace {
-bool is_pinned_host(const void* p) {
-  hipPointerAttribute_t a;
-  const bool ok = hipPointerGetAttributes(&a, p) == hipSuccess && a.type == hipMemoryTypeHost;
-  if (!ok) (void)hipGetLastError();
-  return ok;
-}
-bool is_device_mem(const void* p) {
-  hipPointerAttribute_t a;
-  const bool ok = hipPointerGetAttributes(&a, p) == hipSuccess && a.type == hipMemoryTypeDevice;
-  if (!ok) (void)hipGetLastError();
-  return ok;
-}
 struct Events {
   hipEvent_t e[6] = {};
   hipError_t create() {
@@ -2102,9 +2398,9 @@ int dla_host_reduce(int dtype, int n_peers, int n_tensors, const void* const* te
   if (begin < 0 || end < begin || end > total)
     return fail(DLA_E_INVALID, "dla_host_reduce: need 0 <= begin <= end <= sum(numels)");
   if (end == begin) return DLA_OK;
-  if (!is_pinned_host(h_stage) || !is_pinned_host(h_out))
+  if (!is_pinned_host_ptr(h_stage) || !is_pinned_host_ptr(h_out))
     return fail(DLA_E_INVALID, "dla_host_reduce: h_stage / h_out must be page-locked host memory (hipHostMalloc)");
-  if (!is_device_mem(d_stage) || !is_device_mem(d_out))
+  if (!is_device_ptr(d_stage) || !is_device_ptr(d_out))
     return fail(DLA_E_INVALID, "dla_host_reduce: d_stage / d_out must be device memory");
   const hipStream_t cs_ = static_cast<hipStream_t>(stream);
   const hipStream_t xs = static_cast<hipStream_t>(copy_stream);

@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define DLA_ABI_VERSION 7
+#define DLA_ABI_VERSION 8
 
 /* element dtypes of the peer buffers and of the output */
 #define DLA_F32 0
@@ -138,6 +138,23 @@ int64_t dla_slab_tile_elems(int dtype, int slab_rows, int64_t n_elems);
  * Tensors are packed into as few launches as the kernel-argument block allows. */
 int dla_wsum_multi(int dtype, int n_tensors, const void* const* peer_ptrs, void* const* outs,
                    const int64_t* numels, const double* weights, int n_peers, void* stream);
+
+/* dla_wsum_multi for rounds of many peers (device-resident models: FedAvg.aggregate on modules in
+ * HBM, accdfl/core/gradient_aggregation/fedavg.py:24 walking every parameter of every model; the
+ * simulator's large-N average, simulations/gl/gl_simulation.py:96-105).  The (tensor x peer)
+ * pointer table and one record per tensor travel to the device as ONE table — written into the
+ * caller's page-locked `table_host`, copied by one hipMemcpyAsync on `stream` into `table_dev`
+ * (both at least dla_wsum_multi_table_bytes(n_tensors, n_peers) bytes, 16-byte aligned) — and
+ * every 16-byte aligned F32 / BF16 / F16 tensor is folded by ONE launch per pass of up to
+ * DLA_MAX_PEERS_PER_PASS peers, whatever the peer and tensor counts (128 google_speech ResNet-34
+ * models: 14 080 tensors, 1 launch; dla_wsum_multi: 110).  Other tensors (unaligned, F64) take the
+ * per-tensor path.  Same arguments and arithmetic as dla_wsum_multi; outs[t] may alias tensor t of
+ * peer 0.  The caller leaves table_host and table_dev untouched until the stream has passed this
+ * work (e.g. an event recorded after the call).  ABI v8. */
+int64_t dla_wsum_multi_table_bytes(int n_tensors, int n_peers);
+int dla_wsum_multi_table(int dtype, int n_tensors, const void* const* peer_ptrs, void* const* outs,
+                         const int64_t* numels, const double* weights, int n_peers, void* table_host,
+                         void* table_dev, void* stream);
 
 /* Replaces scripts/distill.py:124-129 (teacher-logit aggregation,
  * torch.mean(torch.stack(preds), dim=0)) for a whole batch of logits at once:

@@ -60,7 +60,7 @@ def test_library_version_and_argument_errors(lib_path):
     from accdfl_amd import _lib
 
     L = _lib.lib()
-    assert L.so.dla_version() == 7
+    assert L.so.dla_version() == 8
     assert L.build_id == _lib.source_build_id() == _lib.file_build_id(lib_path)
     assert L.max_peers_per_pass == 128
     # kernel selection by shape (host-only query): north star, configs[3] share, configs[4] share,
@@ -106,6 +106,14 @@ def test_library_version_and_argument_errors(lib_path):
     ptrs = [4096 * (k + 1) for k in range(130)]
     with pytest.raises(_lib.DlaggError, match="alias"):
         _lib.wsum_ptrs(0, ptrs, [1.0] * 130, 64, ptrs[5], 0)
+    # dla_wsum_multi_table: the table size, and argument errors caught before any GPU work
+    assert _lib.wsum_multi_table_bytes(110, 128) == (1088 + 110 * 40) + 110 * 128 * 8  # index, records, pointers
+    assert _lib.wsum_multi_table_bytes(300, 2) == (1088 + 256 * 40) + (1088 + 44 * 40 + 0) + 300 * 2 * 8
+    assert _lib.wsum_multi_table_bytes(3, 0) == 0
+    rc = L.so.dla_wsum_multi_table(0, 1, None, None, None, None, 1, None, None, None)
+    assert rc == -1 and b"tensor table" in L.so.dla_last_error()
+    with pytest.raises(_lib.DlaggError, match="aliases peer 5"):
+        _lib.wsum_multi_table_ptrs(0, ptrs, [ptrs[5]], [64], [1.0] * 130, 0, 0, 0)
     # launch knobs outside the built set are refused before any launch
     for bad in (_lib.LaunchCfg(3, 0, 0, 0), _lib.LaunchCfg(4, 3, 0, 0), _lib.LaunchCfg(4, 1, 0, 128)):
         with pytest.raises(_lib.DlaggError):

@@ -354,6 +354,79 @@ def test_multi_tensor_batches(n):
         assert same_bits(outs[i].cpu().numpy(), want, "f32"), "tensor %d (numel %d)" % (i, sz)
 
 
+@pytest.mark.parametrize("dtype", ["f32", "bf16", "f16"])
+@pytest.mark.parametrize("n,min_peers", [(33, 33), (128, 33), (130, 33), (200, 33), (8, 1), (20, 1), (32, 1)])
+def test_multi_table_many_peers(dtype, n, min_peers, monkeypatch):
+    """dla_wsum_multi_table (device-side pointer table, one launch per 128-peer pass): ragged and tiny
+    tensors (1, 3, 5 elements: tail workgroups only), an empty one, one aliased in place (out = peer 0's
+    tensor), several passes (130, 200 peers carry the running sum in out), and small peer counts forced
+    onto the table path; every element against the oracle."""
+    from accdfl_amd.core import wsum
+
+    monkeypatch.setattr(wsum, "MULTI_TABLE_MIN_PEERS", min_peers)
+    rng = np.random.default_rng(n + min_peers)
+    sizes = [int(x) for x in rng.integers(1, 3000, size=23)] + [0, 1, 3, 5, 64, 300_007]
+    g = torch.Generator().manual_seed(n)
+    peers_cpu = [[(torch.randn(sz, generator=g) * 0.05).to(TDT[dtype]) for sz in sizes] for _ in range(n)]
+    dev = [[t.cuda() for t in pl] for pl in peers_cpu]
+    w = [float(x) for x in rng.dirichlet(np.ones(n))]
+    outs = [torch.empty(sz, dtype=TDT[dtype], device="cuda") for sz in sizes]
+    outs[7] = dev[0][7]  # in place into peer 0's tensor (allowed: out may alias peer 0)
+    for rnd in range(2):  # twice: the table ring's slots are reused
+        wsum.wsum_multi(dev, w, outs)
+        torch.cuda.synchronize()
+        for i, sz in enumerate(sizes):
+            want = fedavg_bits([gc.as_float(_bits(peers_cpu[k][i], dtype), dtype) for k in range(n)], w, dtype)
+            got = gc.as_float(_bits(outs[i], dtype), dtype)
+            assert same_bits(got, want, dtype), "round %d tensor %d (numel %d)" % (rnd, i, sz)
+        dev[0][7].copy_(peers_cpu[0][7].cuda())  # restore the aliased input for the second round
+
+
+def test_multi_table_refuses_alias_of_a_later_peer():
+    """Several passes carry the running sum in out: out may alias peer 0 only (as dla_wsum)."""
+    from accdfl_amd import _lib
+    from accdfl_amd.core import wsum
+
+    n = 130
+    dev = [[torch.zeros(64, device="cuda")] for _ in range(n)]
+    with pytest.raises(_lib.DlaggError, match="aliases peer 5"):
+        wsum.wsum_multi(dev, [1.0 / n] * n, [dev[5][0]])
+
+
+@pytest.mark.parametrize("name,n,dtype", [("cifar10_resnet8", 64, "f32"), ("cifar10_resnet8", 130, "f32"),
+                                          ("google_speech_resnet34", 40, "bf16")])
+def test_device_modules_of_real_layouts_through_fedavg(name, n, dtype):
+    """FedAvg.aggregate on device-resident modules of the reference layouts (tests/golden/layouts.json)
+    with many peers: one pointer table, one launch per 128-peer pass (_device_round); every parameter
+    element against the oracle, buffers copied from models[0]."""
+    import json
+
+    from accdfl_amd.core.gradient_aggregation.fedavg import FedAvg
+
+    lay = json.load(open(os.path.join(ROOT, "tests", "golden", "layouts.json")))[name]
+    numels = [int(np.prod(s)) if s else 1 for _, s, _ in lay["params"]]
+    g = torch.Generator().manual_seed(n)
+    base = torch.randn(sum(numels), generator=g) * 0.05
+    models = []
+    for k in range(n):
+        flat = (base * (1.0 + 0.01 * k)).to(TDT[dtype])
+        m = torch.nn.Module()
+        m.ps = torch.nn.ParameterList([torch.nn.Parameter(t.view(s).clone().cuda())
+                                       for t, (_, s, _) in zip(flat.split(numels), lay["params"])])
+        m.register_buffer("steps", torch.full((3,), k, dtype=torch.int64, device="cuda"))
+        models.append(m)
+    w = [float(x) for x in np.random.default_rng(n).dirichlet(np.ones(n))]
+    out = FedAvg.aggregate(models, w)
+    torch.cuda.synchronize()
+    flat = [torch.cat([p.detach().reshape(-1) for p in m.parameters()]).cpu() for m in models]
+    want = c_wsum([_bits(f, dtype) if dtype != "f32" else f.numpy() for f in flat], w, dtype)
+    got_t = torch.cat([p.detach().reshape(-1) for p in out.parameters()])
+    got = _bits(got_t, dtype) if dtype != "f32" else got_t.cpu().numpy()
+    assert same_bits(got, want, dtype)
+    assert all(p.is_cuda and p.requires_grad for p in out.parameters())
+    assert torch.equal(out.steps, models[0].steps)
+
+
 def test_multi_tensor_bf16_gnlenet_shapes_one_launch():
     """Device-resident GNLeNet (14 tensors, configs[1]) in bf16 through the fused path."""
     from accdfl_amd.core import wsum
