@@ -83,18 +83,18 @@ def source_build_id() -> str:
 _ID_PREFIX = b"dlagg-build-id:"
 
 
-def file_build_id(path: str) -> Optional[str]:
+def file_build_id(path: str, prefix: bytes = _ID_PREFIX) -> Optional[str]:
     """The build id embedded in a built library file (read from its bytes, not loaded)."""
     try:
         with open(path, "rb") as f:
             data = f.read()
     except OSError:
         return None
-    i = data.find(_ID_PREFIX)
+    i = data.find(prefix)
     if i < 0:
         return None
     j = data.find(b"\0", i)
-    return data[i + len(_ID_PREFIX):j].decode(errors="replace")
+    return data[i + len(prefix):j].decode(errors="replace")
 
 
 def build(force: bool = False, verbose: bool = False) -> str:
@@ -115,15 +115,29 @@ def build(force: bool = False, verbose: bool = False) -> str:
     return out
 
 
+_PROBE_ID_PREFIX = b"dlagg-probe-build-id:"
+
+
+def probe_build_id() -> str:
+    """Hash of csrc/probe.hip and HIPCC_FLAGS (the probe library's build id)."""
+    h = hashlib.sha256()
+    with open(os.path.join(PKG_ROOT, "csrc", "probe.hip"), "rb") as f:
+        h.update(f.read())
+    h.update(" ".join(HIPCC_FLAGS).encode())
+    return h.hexdigest()[:20]
+
+
 def build_probe(force: bool = False) -> str:
-    """Compile the HBM ceiling probes (csrc/probe.hip -> lib/libdlagg_probe.so; diagnostics only)."""
+    """Compile the HBM ceiling probes (csrc/probe.hip -> lib/libdlagg_probe.so; diagnostics only),
+    unless the library there already carries this tree's probe build id (as build() does)."""
     src = os.path.join(PKG_ROOT, "csrc", "probe.hip")
     out = os.path.join(PKG_ROOT, "lib", "libdlagg_probe.so")
-    if not force and os.path.exists(out) and os.path.getmtime(out) >= os.path.getmtime(src):
+    bid = probe_build_id()
+    if not force and file_build_id(out, _PROBE_ID_PREFIX) == bid:
         return out
     os.makedirs(os.path.dirname(out), exist_ok=True)
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-    subprocess.run([hipcc, *HIPCC_FLAGS, "-o", out + ".tmp", src], check=True)
+    subprocess.run([hipcc, *HIPCC_FLAGS, '-DDLP_BUILD_ID="%s"' % bid, "-o", out + ".tmp", src], check=True)
     os.replace(out + ".tmp", out)
     return out
 

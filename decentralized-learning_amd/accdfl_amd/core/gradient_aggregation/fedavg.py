@@ -141,19 +141,36 @@ _MIN_SHARD_BYTES = 8 << 20  # per device; smaller models stay on one GPU
 
 
 def set_host_devices(devices) -> None:
-    """Use these HIP devices for CPU-resident models (default: the current device, or the
-    comma list in ACCDFL_AMD_DEVICES)."""
+    """Use these HIP devices for CPU-resident models (an empty list restores the default: see
+    _devices_for)."""
     global _host_devices
     _host_devices = [torch.device("cuda", d) if isinstance(d, int) else torch.device(d) for d in devices]
 
 
-def _devices_for(device: torch.device) -> List[torch.device]:
+def _devices_for(device: torch.device, round_bytes: int = 0) -> List[torch.device]:
+    """The GPUs a host-staged round of CPU models streams through, in bucket order:
+    * set_host_devices([...]), else ACCDFL_AMD_DEVICES: a comma list of device ids, "current" (only
+      the current device: the opt-out) or "all";
+    * by default, a round that moves at least _MIN_SHARD_BYTES per device over PCIe uses every visible
+      GPU, the current one first — each bucket crosses its own GPU's PCIe link, bit-identically —
+      unless the process is one rank of a multi-rank torch.distributed group (one process per GPU:
+      the other GPUs belong to the other ranks).  The caller trims the list to the round's size."""
     if _host_devices:
         return list(_host_devices)
-    env = os.environ.get("ACCDFL_AMD_DEVICES", "")
-    if env:
+    env = os.environ.get("ACCDFL_AMD_DEVICES", "").strip().lower()
+    if env and env not in ("all", "current"):
         return [torch.device("cuda", int(x)) for x in env.split(",") if x.strip()]
-    return [device]
+    if env == "current" or round_bytes < 2 * _MIN_SHARD_BYTES:
+        return [device]
+    count = torch.cuda.device_count()
+    if count < 2:
+        return [device]
+    if env != "all":
+        import torch.distributed as dist
+
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+            return [device]
+    return [device] + [torch.device("cuda", d) for d in range(count) if d != device.index]
 
 
 def _flat_slices(tensors: List[torch.Tensor], numels: List[int], start: int, end: int) -> List[torch.Tensor]:
@@ -234,13 +251,51 @@ def _reduce_host_small(device, dtype, center: List[torch.Tensor], peers: List[Li
         _lib.host_round_finish(code, hr.numels_arr, hr.h_out.data_ptr(), [c.data_ptr() for c in center], stream)
 
 
+# list(m.parameters()) for module trees whose classes all keep nn.Module's own walk: the same order and
+# the same de-duplication (pre-order over modules, a module or parameter seen before is skipped), without
+# named_modules' prefix strings and generator frames — the walk over every parameter of every model is
+# the host path's largest Python cost (128 google_speech ResNet-34 models: 14 080 parameters).
+_WALK_METHODS = ("parameters", "named_parameters", "named_modules", "_named_members", "modules")
+_plain_walk_cls: Dict[type, bool] = {}
+
+
+def _plain_walk(cls: type) -> bool:
+    ok = _plain_walk_cls.get(cls)
+    if ok is None:
+        ok = all(getattr(cls, name, None) is getattr(nn.Module, name) for name in _WALK_METHODS)
+        _plain_walk_cls[cls] = ok
+    return ok
+
+
+def _parameters(model: nn.Module) -> List[nn.Parameter]:
+    out: List[nn.Parameter] = []
+    seen_p, seen_m = set(), set()
+
+    def walk(mod) -> bool:
+        if id(mod) in seen_m:
+            return True
+        if not _plain_walk(type(mod)):
+            return False
+        seen_m.add(id(mod))
+        for p in mod._parameters.values():
+            if p is not None and id(p) not in seen_p:
+                seen_p.add(id(p))
+                out.append(p)
+        for child in mod._modules.values():
+            if child is not None and not walk(child):
+                return False
+        return True
+
+    return out if walk(model) else list(model.parameters())
+
+
 def _host_layout(models: List[nn.Module]):
     """(dtype, numels, pointers) of a round whose models all have models[0]'s parameter shapes, one
     supported dtype and contiguous CPU storage — the models at every reference call site — with the
     parameters' host pointers peer-major, gathered in one pass without a tensor view per parameter
     (a round of 128 ResNet-34 models has 14 080 parameters: a detach + reshape + slice of each costs
     more than the GPU work); None when the round does not qualify (the general path handles it)."""
-    p0 = list(models[0].parameters())
+    p0 = _parameters(models[0])
     if not p0 or not torch.cuda.is_available():
         return None
     dtype = p0[0].dtype
@@ -251,7 +306,7 @@ def _host_layout(models: List[nn.Module]):
     ptrs = []
     add = ptrs.append
     for m in models:
-        ps = list(m.parameters())
+        ps = p0 if m is models[0] else _parameters(m)
         if len(ps) != n_t:
             return None
         for p, shape in zip(ps, shapes):
@@ -268,7 +323,7 @@ def _device_layout(models: List[nn.Module]):
     general path handles it).  The table is [n_tensors x n_peers] uint64, as dla_wsum_multi takes it."""
     import numpy as np
 
-    p0 = list(models[0].parameters())
+    p0 = _parameters(models[0])
     if not p0 or not p0[0].is_cuda:
         return None
     dtype = p0[0].dtype
@@ -279,7 +334,7 @@ def _device_layout(models: List[nn.Module]):
     n_t = len(shapes)
     rows = []
     for m in models:
-        ps = p0 if m is models[0] else list(m.parameters())
+        ps = p0 if m is models[0] else _parameters(m)
         if len(ps) != n_t:
             return None
         row = []
@@ -354,7 +409,6 @@ def _large_round(models: List[nn.Module], weights, layout) -> "nn.Module | None"
     _host_layout: every GPU of the host path (set_host_devices) streams its parameter bucket in
     packed chunks (one DMA per chunk), one host thread per GPU; the averaged elements land in the
     result's parameters.  None when the result's parameters are not dense CPU tensors."""
-    from concurrent.futures import ThreadPoolExecutor
 
     from accdfl_amd.core.sharding import bucket_bounds
 
@@ -364,11 +418,13 @@ def _large_round(models: List[nn.Module], weights, layout) -> "nn.Module | None"
     total = sum(numels)
     align = _ALIGN_BYTES // esize
     device = _wsum.require_device(None)
-    devices = _devices_for(device)
+    devices = _devices_for(device, total * esize)
     devices = devices[:max(1, min(len(devices), (total * esize) // _MIN_SHARD_BYTES))]
-    center = _center_copy(models[0])
-    params = list(center.parameters())
-    if len(params) != len(numels) or not all(c.is_cpu and c.is_contiguous() for c in params):
+    # the result's parameters first; the module tree (deepcopy of models[0], fedavg.py:20) is cloned
+    # on this thread while the native call streams the round through the GPU on another
+    memo = _fresh_params(models[0])
+    params = [memo.get(id(p)) for p in models[0].parameters()] if len(memo) == len(numels) else []
+    if len(params) != len(numels) or not all(c is not None and c.is_cpu and c.is_contiguous() for c in params):
         return None
     code = _wsum.dtype_code(dtype)
     tensor_arr = (ctypes.c_void_p * len(ptrs))(*ptrs)
@@ -387,16 +443,35 @@ def _large_round(models: List[nn.Module], weights, layout) -> "nn.Module | None"
             compute = torch.cuda.current_stream(dev)
             st.copy_stream.wait_stream(compute)  # earlier users of the device staging are done
             with torch.cuda.device(dev):
-                _lib.host_reduce(code, n, tensor_arr, numel_arr, weights, out_arr, s, e, chunk, st.h_stage.data_ptr(),
-                                 st.d_stage.data_ptr(), st.h_out.data_ptr(), st.d_out.data_ptr(),
-                                 compute.cuda_stream, st.copy_stream.cuda_stream)
+                _lib.host_reduce(code, n, tensor_arr, numel_arr, weights, out_arr, s, e, chunk,
+                                 st.h_stage.data_ptr(), st.d_stage.data_ptr(), st.h_out.data_ptr(),
+                                 st.d_out.data_ptr(), compute.cuda_stream, st.copy_stream.cuda_stream)
 
-        if len(jobs) == 1:
-            bucket(jobs[0])
-        else:
-            with ThreadPoolExecutor(max_workers=len(jobs)) as pool:
-                list(pool.map(bucket, jobs))  # re-raises the first failure
+        futures = [_round_executor().submit(bucket, job) for job in jobs]
+        try:
+            center = _clone_value(models[0], memo)
+        finally:
+            for f in futures:
+                f.exception()  # waits; every bucket has finished with the staging before the lock goes
+        for f in futures:
+            f.result()  # re-raises the first failure
     return center
+
+
+_round_pool = None
+_round_pool_pid = None
+
+
+def _round_executor():
+    """Persistent worker threads for the native host-round calls (one per GPU bucket), so a round
+    pays no thread start-up; rebuilt in a forked child, which has none of the parent's threads."""
+    global _round_pool, _round_pool_pid
+    if _round_pool is None or _round_pool_pid != os.getpid():
+        from concurrent.futures import ThreadPoolExecutor
+
+        _round_pool = ThreadPoolExecutor(max_workers=8, thread_name_prefix="accdfl-host-round")
+        _round_pool_pid = os.getpid()
+    return _round_pool
 
 
 def _stage_rows(st, dev, k: int, flat: List[torch.Tensor], numels: List[int], s: int, e: int):
@@ -729,7 +804,8 @@ def reduce_parameters(center_params: List[torch.Tensor], peer_params: List[List[
         elif all(t.device.type == "cuda" for t in center) and all(t.device.type == "cuda" for pl in peers for t in pl):
             _reduce_multi_device(center, peers, weights)
         else:
-            _reduce_host_staged(_devices_for(device), dtype, center, peers, weights)
+            round_bytes = n * sum(c.numel() for c in center) * center[0].element_size()
+            _reduce_host_staged(_devices_for(device, round_bytes), dtype, center, peers, weights)
     for i in partial:
         ks = [k for k in range(n) if len(peer_params[k]) > i]
         _reduce_param(device, center_params[i], [peer_params[k][i] for k in ks], [weights[k] for k in ks])

@@ -910,31 +910,20 @@ struct PeerRef {  // the PeerTable interface (tab.p[k], tab.w[k]) over one row o
   const W* __restrict__ w;
 };
 
-// SEARCH 1: the two-level count over MultiIndex; 0: a binary search over segs[].wg_begin.
-template <int SEARCH>
-__device__ __attribute__((always_inline)) inline int multi_segment(const MultiIndex* idx, const MultiSeg* segs,
-                                                                   int n_seg, int b) {
-  if constexpr (SEARCH == 1) {
-    const ConstI32 cz = (ConstI32)(idx->coarse);
-    int c = 0;
+// Workgroup b's tensor: count the coarse entries <= b (one s_load_dwordx16 batch), then the fine
+// entries <= b in that block of 16 (a second one).  (A binary search over the records' wg_begin — eight
+// dependent scalar loads for 256 tensors — measured the same, profiles/r03d/: the lookup is not what
+// bounds this kernel.)
+__device__ __attribute__((always_inline)) inline int multi_segment(const MultiIndex* idx, int b) {
+  const ConstI32 cz = (ConstI32)(idx->coarse);
+  int c = 0;
 #pragma unroll
-    for (int q = 1; q < 16; ++q) c += cz[q] <= b ? 1 : 0;
-    const ConstI32 fz = (ConstI32)(idx->fine + 16 * c);
-    int t = 16 * c;
+  for (int q = 1; q < 16; ++q) c += cz[q] <= b ? 1 : 0;
+  const ConstI32 fz = (ConstI32)(idx->fine + 16 * c);
+  int t = 16 * c;
 #pragma unroll
-    for (int q = 1; q < 16; ++q) t += fz[q] <= b ? 1 : 0;
-    return t;
-  } else {
-    int lo = 0, hi = n_seg - 1;  // the last tensor whose first workgroup is <= b
-    while (lo < hi) {
-      const int mid = (lo + hi + 1) >> 1;
-      if (segs[mid].wg_begin <= b)
-        lo = mid;
-      else
-        hi = mid - 1;
-    }
-    return lo;
-  }
+  for (int q = 1; q < 16; ++q) t += fz[q] <= b ? 1 : 0;
+  return t;
 }
 
 template <typename W, int KMAX>
@@ -942,7 +931,7 @@ struct WeightTable {
   W w[KMAX];
 };
 
-template <int DT, int KMAX, int G, bool ACC_IN, bool PLAIN_ST, int SEARCH>
+template <int DT, int KMAX, int G, bool ACC_IN, bool PLAIN_ST>
 __global__ __launch_bounds__(64) void wsum_multi_vec_kernel(const MultiIndex* __restrict__ idx,
                                                             const MultiSeg* __restrict__ segs, int n_seg, int k0,
                                                             int n_peers,
@@ -954,7 +943,7 @@ __global__ __launch_bounds__(64) void wsum_multi_vec_kernel(const MultiIndex* __
   using V = typename VecOf<VW>::T;
   constexpr int WE = O::WE;
   const int64_t b = blockIdx.x;
-  const int lo = multi_segment<SEARCH>(idx, segs, n_seg, static_cast<int>(blockIdx.x));
+  const int lo = multi_segment(idx, static_cast<int>(blockIdx.x));
   const int64_t n_vecs = segs[lo].n_vecs;
   const int64_t local = b - segs[lo].wg_begin;
   const PeerRef<typename O::w_t> tab{(ConstPeerTab)(segs[lo].ptrs + k0), wt.w};
@@ -1323,8 +1312,6 @@ hipError_t launch_vec(const PeerTable<typename Ops<DT>::w_t, KMAX>& tab, int n, 
     switch (variant) {
       case 9: DLA_VEC(32, 2, false); break;
       case 21: DLA_VEC(32, 2, true); break;
-      case 10: DLA_VEC(16, 4, false); break;
-      case 11: DLA_VEC(32, 4, false); break;
       default: DLA_VEC(16, 2, false); break;  // 12
     }
 #undef DLA_VEC
@@ -1333,7 +1320,7 @@ hipError_t launch_vec(const PeerTable<typename Ops<DT>::w_t, KMAX>& tab, int n, 
 }
 
 // The tile-interleaved slab (dla_wsum_slab_tiled) through the vector-per-lane kernel: variant 12 =
-// dwordx2 x 16 peers in flight, 10 = dwordx4 x 16, 21 = dwordx2 x 32 with plain stores, otherwise
+// dwordx2 x 16 peers in flight, 21 = dwordx2 x 32 with plain stores, otherwise
 // (default, 9) dwordx2 x 32.
 template <int DT, int KMAX, bool ACC_IN>
 hipError_t launch_vec_tiled(const PeerTable<typename Ops<DT>::w_t, KMAX>& tab, int n, int64_t n_elems, void* out,
@@ -1359,7 +1346,6 @@ hipError_t launch_vec_tiled(const PeerTable<typename Ops<DT>::w_t, KMAX>& tab, i
   } while (0)
     switch (variant) {
       case 12: DLA_VECT(16, 2, false); break;
-      case 10: DLA_VECT(16, 4, false); break;
       case 21: DLA_VECT(32, 2, true); break;
       default: DLA_VECT(32, 2, false); break;
     }
@@ -1452,7 +1438,7 @@ hipError_t launch_pass(const PeerTable<typename Ops<DT>::w_t, KMAX>& tab, int n,
                        dim3(kBlock), 0, s, tab, n, n_elems, out);
     return hipGetLastError();
   }
-  if ((l.variant >= 9 && l.variant <= 12) || l.variant == 21) {
+  if (l.variant == 9 || l.variant == 12 || l.variant == 21) {
     if constexpr (DT != DLA_F64) return launch_vec<DT, KMAX, ACC_IN>(tab, n, n_elems, out, s, l.variant);
   }
   if constexpr ((DT == DLA_BF16 || DT == DLA_F16) && KMAX == 8) {
@@ -1583,15 +1569,6 @@ int64_t multi_table_bytes(int n_tensors, int n_peers) {
   return b + static_cast<int64_t>(n_tensors) * n_peers * 8;
 }
 
-// DLA_MULTI_SEARCH=0: the binary search (A/B only); default 1, the two-level count
-int multi_search() {
-  static const int v = [] {
-    const char* e = std::getenv("DLA_MULTI_SEARCH");
-    return e && std::atoi(e) == 0 ? 0 : 1;
-  }();
-  return v;
-}
-
 template <int DT, int KMAX, int G, bool ACC_IN>
 hipError_t launch_multi_vec(const MultiIndex* idx, const MultiSeg* segs, int n_seg, int64_t grid, int k0, int pm,
                             const double* weights, bool plain, hipStream_t s) {
@@ -1600,14 +1577,10 @@ hipError_t launch_multi_vec(const MultiIndex* idx, const MultiSeg* segs, int n_s
   std::memset(&wt, 0, sizeof(wt));
   for (int k = 0; k < pm; ++k) wt.w[k] = static_cast<W>(weights[k0 + k]);  // RNE double -> op-math
   const dim3 g(static_cast<unsigned>(grid)), bl(64);
-#define DLA_MV(PL, SE) \
-  hipLaunchKernelGGL((wsum_multi_vec_kernel<DT, KMAX, G, ACC_IN, PL, SE>), g, bl, 0, s, idx, segs, n_seg, k0, pm, wt)
-  if (multi_search() == 1) {
-    if (plain) DLA_MV(true, 1); else DLA_MV(false, 1);
-  } else {
-    if (plain) DLA_MV(true, 0); else DLA_MV(false, 0);
-  }
-#undef DLA_MV
+  if (plain)
+    hipLaunchKernelGGL((wsum_multi_vec_kernel<DT, KMAX, G, ACC_IN, true>), g, bl, 0, s, idx, segs, n_seg, k0, pm, wt);
+  else
+    hipLaunchKernelGGL((wsum_multi_vec_kernel<DT, KMAX, G, ACC_IN, false>), g, bl, 0, s, idx, segs, n_seg, k0, pm, wt);
   return hipGetLastError();
 }
 
@@ -1748,10 +1721,10 @@ int wsum_impl(int dtype, const void* const* peers, const double* weights, int n_
                                      std::to_string(kMaxPeersPerPass));
   }
   const Launch l = resolve(cfg);
-  if (l.variant != 1 && l.variant != 2 && l.variant != 4 && !(l.variant >= 8 && l.variant <= 12) && l.variant != 16 &&
+  if (l.variant != 1 && l.variant != 2 && l.variant != 4 && l.variant != 8 && l.variant != 9 && l.variant != 12 && l.variant != 16 &&
       l.variant != 17 && l.variant != 21)
     return fail(DLA_E_CONFIG,
-                "dla_wsum: unsupported variant " + std::to_string(l.variant) + " (1, 2, 4, 8-12, 16, 17 or 21)");
+                "dla_wsum: unsupported variant " + std::to_string(l.variant) + " (1, 2, 4, 8, 9, 12, 16, 17 or 21)");
   if (l.chunks != 0 && l.chunks != 1 && l.chunks != 2 && l.chunks != 4)
     return fail(DLA_E_CONFIG, "dla_wsum: chunks must be 0 (auto), 1, 2 or 4");
   if (l.block != 0 && l.block != 64 && l.block != 256)
@@ -2022,14 +1995,55 @@ CopyPool& copy_pool() {
   return *pool;
 }
 
-// dsts[i] <- srcs[i], bytes[i] each (validated by the caller); threaded from 4 MiB.
-void copy_batch(void* const* dsts, const void* const* srcs, const int64_t* bytes, int n) {
+// Streaming (non-temporal) host copy for packs into page-locked staging that only the GPU reads next
+// (a DMA or the kernel across PCIe): 32-byte vmovnt stores go straight to DRAM, with no read for
+// ownership of the destination lines and no eviction of the packing thread's cache.
+typedef long long v4i64 __attribute__((vector_size(32)));
+__attribute__((target("avx2"))) void stream_copy_avx2(char* d, const char* s, size_t n) {
+  size_t head = (32 - (reinterpret_cast<uintptr_t>(d) & 31)) & 31;
+  if (head > n) head = n;
+  std::memcpy(d, s, head);
+  d += head, s += head, n -= head;
+  size_t i = 0;
+  for (; i + 128 <= n; i += 128) {
+    v4i64 a, b, c, e;
+    std::memcpy(&a, s + i, 32), std::memcpy(&b, s + i + 32, 32);
+    std::memcpy(&c, s + i + 64, 32), std::memcpy(&e, s + i + 96, 32);
+    __builtin_nontemporal_store(a, reinterpret_cast<v4i64*>(d + i));
+    __builtin_nontemporal_store(b, reinterpret_cast<v4i64*>(d + i + 32));
+    __builtin_nontemporal_store(c, reinterpret_cast<v4i64*>(d + i + 64));
+    __builtin_nontemporal_store(e, reinterpret_cast<v4i64*>(d + i + 96));
+  }
+  std::memcpy(d + i, s + i, n - i);
+}
+
+// DLA_COPY_NT=0 turns the streaming stores off (A/B); they need AVX2 (every MI355X host has it).
+bool stream_copies() {
+  static const bool on = [] {
+    const char* e = std::getenv("DLA_COPY_NT");
+    return !(e && std::atoi(e) == 0) && __builtin_cpu_supports("avx2");
+  }();
+  return on;
+}
+
+inline void copy_bytes(void* d, const void* s, int64_t n, bool nt) {
+  if (nt && n >= 4096)
+    stream_copy_avx2(static_cast<char*>(d), static_cast<const char*>(s), static_cast<size_t>(n));
+  else
+    std::memcpy(d, s, static_cast<size_t>(n));
+}
+
+// dsts[i] <- srcs[i], bytes[i] each (validated by the caller); threaded from 4 MiB.  nt: streaming
+// stores (packs into page-locked staging read by the GPU next), fenced before the call returns.
+void copy_batch(void* const* dsts, const void* const* srcs, const int64_t* bytes, int n, bool nt = false) {
+  nt = nt && stream_copies();
   int64_t total = 0;
   for (int i = 0; i < n; ++i) total += bytes[i];
   const int threads = copy_threads(total);
   if (threads <= 1) {
     for (int i = 0; i < n; ++i)
-      if (bytes[i] > 0) std::memcpy(dsts[i], srcs[i], static_cast<size_t>(bytes[i]));
+      if (bytes[i] > 0) copy_bytes(dsts[i], srcs[i], bytes[i], nt);
+    if (nt) __builtin_ia32_sfence();
     return;
   }
   // Large batches (an EVA block list gathered into a page-locked ingress buffer: ~1 700
@@ -2040,9 +2054,10 @@ void copy_batch(void* const* dsts, const void* const* srcs, const int64_t* bytes
     for (int i = 0; i < n && off < hi; off += bytes[i], ++i) {
       const int64_t s0 = lo > off ? lo : off, e0 = hi < off + bytes[i] ? hi : off + bytes[i];
       if (s0 < e0)
-        std::memcpy(static_cast<char*>(dsts[i]) + (s0 - off), static_cast<const char*>(srcs[i]) + (s0 - off),
-                    static_cast<size_t>(e0 - s0));
+        copy_bytes(static_cast<char*>(dsts[i]) + (s0 - off), static_cast<const char*>(srcs[i]) + (s0 - off), e0 - s0,
+                   nt);
     }
+    if (nt) __builtin_ia32_sfence();  // this thread's streaming stores are visible before it reports done
   };
   const int64_t per = (total + threads - 1) / threads;
   auto part = [&](int t) { copy_range(per * t < total ? per * t : total, per * (t + 1) < total ? per * (t + 1) : total); };
@@ -2327,7 +2342,7 @@ int dla_host_round_start(int dtype, int n_peers, int n_tensors, const void* cons
       off += bytes[i];
     }
   }
-  copy_batch(dsts.data(), srcs.data(), bytes.data(), static_cast<int>(dsts.size()));
+  copy_batch(dsts.data(), srcs.data(), bytes.data(), static_cast<int>(dsts.size()), /*nt=*/true);
   const int rc = wsum_impl(dtype, row_ptrs.data(), weights, n_peers, total, result, stream, nullptr);
   return rc;
 }
@@ -2412,7 +2427,20 @@ int dla_host_reduce(int dtype, int n_peers, int n_tensors, const void* const* te
   hipEvent_t* d2h = ev.e + 4;
   const int64_t row_bytes = chunk_elems * es;
   const int64_t buf_bytes = row_bytes * n_peers;
-  const int64_t n_chunks = (end - begin + chunk_elems - 1) / chunk_elems;
+  // Chunk schedule: nothing crosses PCIe before the first chunk is packed, so the first chunks ramp
+  // up (1/4, then 1/2 of chunk_elems, 256-byte multiples) and the pipeline fills in a quarter of the
+  // time; then full chunks.  cs[c] .. cs[c + 1] are chunk c's flat elements.
+  const int64_t align = 256 / es;
+  std::vector<int64_t> cs{begin};
+  for (int64_t part = 4; cs.back() < end; part = part > 1 ? part / 2 : 1) {
+    int64_t len = chunk_elems / part / align * align;
+    if (len < align) len = align;
+    cs.push_back(cs.back() + len < end ? cs.back() + len : end);
+  }
+  const int64_t n_chunks = static_cast<int64_t>(cs.size()) - 1;
+  // Chunk c's rows are packed dense at pitch(c) (its length in bytes rounded up to 256, so every row
+  // stays 16-byte aligned for the kernel): one contiguous H2D per chunk, the last one included.
+  auto pitch = [&](int64_t c) { return ((cs[c + 1] - cs[c]) * es + 255) / 256 * 256; };
   std::vector<void*> dsts;
   std::vector<const void*> srcs;
   std::vector<int64_t> bytes;
@@ -2436,7 +2464,7 @@ int dla_host_reduce(int dtype, int n_peers, int n_tensors, const void* const* te
   auto unpack = [&](int64_t c) {
     const int buf = static_cast<int>(c & 1);
     if (!check(hipEventSynchronize(d2h[buf]), "D2H")) return;
-    const int64_t c0 = begin + c * chunk_elems, c1 = c0 + chunk_elems < end ? c0 + chunk_elems : end;
+    const int64_t c0 = cs[c], c1 = cs[c + 1];
     dsts.clear(), srcs.clear(), bytes.clear();
     pieces(c0, c1, [&](int t, int64_t a, int64_t b) {
       dsts.push_back(static_cast<char*>(outs[t]) + (a - start[t]) * es);
@@ -2448,13 +2476,14 @@ int dla_host_reduce(int dtype, int n_peers, int n_tensors, const void* const* te
   // DLA_HOST_REDUCE_STATS=1: per-call phase times on stderr (host-path tuning)
   static const bool stats = std::getenv("DLA_HOST_REDUCE_STATS") != nullptr;
   using clk = std::chrono::steady_clock;
-  double t_wait = 0, t_pack = 0, t_issue = 0, t_unpack = 0;
+  double t_wait = 0, t_pack = 0, t_issue = 0, t_unpack = 0, t_first = 0;
   auto secs = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double>(b - a).count(); };
   const auto t_start = clk::now();
   for (int64_t c = 0; c < n_chunks && e == hipSuccess; ++c) {
     const int buf = static_cast<int>(c & 1);
-    const int64_t c0 = begin + c * chunk_elems, c1 = c0 + chunk_elems < end ? c0 + chunk_elems : end;
+    const int64_t c0 = cs[c], c1 = cs[c + 1];
     const int64_t m = c1 - c0;
+    const int64_t rp = pitch(c);
     const auto t0 = clk::now();
     char* hs = static_cast<char*>(h_stage) + buf * buf_bytes;
     char* ds = static_cast<char*>(d_stage) + buf * buf_bytes;
@@ -2465,23 +2494,31 @@ int dla_host_reduce(int dtype, int n_peers, int n_tensors, const void* const* te
     const auto t1 = clk::now();
     dsts.clear(), srcs.clear(), bytes.clear();
     for (int k = 0; k < n_peers; ++k) {
-      rows[k] = ds + k * row_bytes;
+      rows[k] = ds + k * rp;
       pieces(c0, c1, [&](int t, int64_t a, int64_t b) {
-        dsts.push_back(hs + k * row_bytes + (a - c0) * es);
+        dsts.push_back(hs + k * rp + (a - c0) * es);
         srcs.push_back(static_cast<const char*>(tensors[static_cast<size_t>(k) * n_tensors + t]) + (a - start[t]) * es);
         bytes.push_back((b - a) * es);
       });
     }
-    copy_batch(dsts.data(), srcs.data(), bytes.data(), static_cast<int>(dsts.size()));
+    copy_batch(dsts.data(), srcs.data(), bytes.data(), static_cast<int>(dsts.size()), /*nt=*/true);
     const auto t2 = clk::now();
-    // H2D on the copy stream once the reduce of chunk c-2 is done with d_stage[buf]
-    if (c >= 2 && !check(hipStreamWaitEvent(xs, red[buf], 0), "wait")) break;
-    if (m == chunk_elems) {
-      if (!check(hipMemcpyAsync(ds, hs, buf_bytes, hipMemcpyHostToDevice, xs), "H2D")) break;
-    } else if (!check(hipMemcpy2DAsync(ds, row_bytes, hs, row_bytes, m * es, n_peers, hipMemcpyHostToDevice, xs),
-                      "H2D")) {
-      break;
+    if (c == 0) t_first = secs(t_start, t2);
+    // ONE H2D of the chunk's rows on the copy stream, once the reduce of chunk c-2 is done with d_stage[buf].
+    // That reduce has normally finished long before (it is a few microseconds of a chunk's DMA time):
+    // the copy queue is then not made to wait on the compute queue at all — a cross-queue wait in
+    // front of every DMA stalls the copy engine between chunks.  DLA_HOST_WAIT_ALWAYS=1: always wait (A/B).
+    if (c >= 2) {
+      static const bool always = std::getenv("DLA_HOST_WAIT_ALWAYS") != nullptr;
+      const hipError_t q = always ? hipErrorNotReady : hipEventQuery(red[buf]);
+      if (q == hipErrorNotReady) {
+        (void)hipGetLastError();
+        if (!check(hipStreamWaitEvent(xs, red[buf], 0), "wait")) break;
+      } else if (!check(q, "event query")) {
+        break;
+      }
     }
+    if (!check(hipMemcpyAsync(ds, hs, static_cast<size_t>(rp * n_peers), hipMemcpyHostToDevice, xs), "H2D")) break;
     if (!check(hipEventRecord(h2d[buf], xs), "record")) break;
     // reduce (list order, fedavg.py:23-25) and D2H on the compute stream
     if (!check(hipStreamWaitEvent(cs_, h2d[buf], 0), "wait")) break;
@@ -2499,14 +2536,16 @@ int dla_host_reduce(int dtype, int n_peers, int n_tensors, const void* const* te
     const auto t4 = clk::now();
     t_wait += secs(t0, t1), t_pack += secs(t1, t2), t_issue += secs(t2, t3), t_unpack += secs(t3, t4);
   }
+  const auto t_loop = clk::now();
   if (e == hipSuccess) unpack(n_chunks - 1);
   if (stats)
     std::fprintf(stderr,
-                 "dla_host_reduce: %d peers x %lld elems, %lld chunks of %lld: total %.2f ms, wait-h2d %.2f, "
-                 "pack %.2f (%.1f GB/s), issue %.2f, unpack+wait-d2h %.2f\n",
+                 "dla_host_reduce: %d peers x %lld elems, %lld chunks of <= %lld: total %.2f ms, first pack %.2f, "
+                 "wait-h2d %.2f, pack %.2f (%.1f GB/s), issue %.2f, unpack+wait-d2h %.2f, last unpack %.2f\n",
                  n_peers, static_cast<long long>(end - begin), static_cast<long long>(n_chunks),
-                 static_cast<long long>(chunk_elems), secs(t_start, clk::now()) * 1e3, t_wait * 1e3, t_pack * 1e3,
-                 t_pack > 0 ? double(end - begin) * es * n_peers / t_pack / 1e9 : 0.0, t_issue * 1e3, t_unpack * 1e3);
+                 static_cast<long long>(chunk_elems), secs(t_start, clk::now()) * 1e3, t_first * 1e3, t_wait * 1e3,
+                 t_pack * 1e3, t_pack > 0 ? double(end - begin) * es * n_peers / t_pack / 1e9 : 0.0, t_issue * 1e3,
+                 t_unpack * 1e3, secs(t_loop, clk::now()) * 1e3);
   if (e != hipSuccess) {
     (void)hipStreamSynchronize(cs_);
     (void)hipStreamSynchronize(xs);
@@ -2567,8 +2606,8 @@ int dla_wsum_slab_tiled(int dtype, const void* base, int64_t tile_elems, int64_t
       cfg && cfg->variant
           ? cfg->variant
           : vec_store_policy(vec_variant(n_peers < kMaxPeersPerPass ? n_peers : kMaxPeersPerPass), n_elems * es);
-  if (variant != 9 && variant != 10 && variant != 12 && variant != 21)
-    return fail(DLA_E_CONFIG, "dla_wsum_slab_tiled: variant must be 0 (auto), 9, 10, 12 or 21");
+  if (variant != 9 && variant != 12 && variant != 21)
+    return fail(DLA_E_CONFIG, "dla_wsum_slab_tiled: variant must be 0 (auto), 9, 12 or 21");
   const int64_t stride = slab_rows * tile_elems;
   hipStream_t s = static_cast<hipStream_t>(stream);
   hipError_t e;

@@ -11,7 +11,15 @@
 
 #include <cstdint>
 
+// Hash of this file and the compile flags, set by the build (accdfl_amd/_lib.py build_probe()): a
+// probe library is rebuilt when its id differs from the tree's, not by file times.
+#ifndef DLP_BUILD_ID
+#define DLP_BUILD_ID "unversioned"
+#endif
+
 namespace {
+
+__attribute__((used)) const char kProbeIdTag[] = "dlagg-probe-build-id:" DLP_BUILD_ID;
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));

@@ -71,9 +71,9 @@ typedef struct dla_launch_cfg {
                            in flight per lane; chunks/block/grid are ignored)
                        9 = vector-per-lane kernel: 8 bytes per lane per load, 32 peers in
                            flight per lane (passes of more than 8 peers; fp64 and smaller
-                           passes take 4); 10 = 16 bytes x 16 peers; 11 = 16 bytes x 32;
-                           12 = 8 bytes x 16; 21 = 9 with plain (L2 write-back)
-                           output stores instead of sc1
+                           passes take 4); 12 = 8 bytes x 16; 21 = 9 with plain (L2
+                           write-back) output stores instead of sc1.  (16-byte-per-lane forms
+                           were measured slower at every shape and are not built.)
                       16 = peer-major big-tile kernel (fp32 <= 8, 16 or 32 peers, fp64 <= 8:
                            16 KiB of output per wave, one peer's 16 KiB streamed at a
                            time; chunks/block/grid are ignored; other dtypes take 4)
@@ -120,7 +120,7 @@ int dla_wsum_slab(int dtype, const void* base, int64_t pitch_elems, const double
  * of HBM instead of n_peers distant ones.  Peers 0..n_peers-1 (n_peers <= slab_rows) are
  * reduced in row order into the contiguous `out` (n_elems elements).  tile_elems: a power of
  * two of >= 16 bytes; base and out 16-byte aligned; F32, BF16 or F16.  cfg (may be NULL):
- * variant 0 (by shape, as dla_wsum), 9, 10, 12 or 21 picks the vector-per-lane kernel form.
+ * variant 0 (by shape, as dla_wsum), 9, 12 or 21 picks the vector-per-lane kernel form.
  * ABI v5. */
 int dla_wsum_slab_tiled(int dtype, const void* base, int64_t tile_elems, int64_t slab_rows, const double* weights,
                         int n_peers, int64_t n_elems, void* out, void* stream, const dla_launch_cfg_t* cfg);
@@ -247,10 +247,14 @@ int dla_host_round_finish(int dtype, int n_tensors, const int64_t* numels, const
  * the simulators' averages, simulations/learning_simulation.py:335) — streamed through the GPU in
  * element chunks of the flat (parameters()-order) vector.  Only the flat elements [begin, end) are
  * reduced and written (one bucket per GPU when the round is sharded over several GPUs: one call per
- * GPU, each from its own host thread, with that GPU current).  For chunk c (buffer c & 1):
- *   1. pack: elements [begin + c*chunk, begin + (c+1)*chunk) of every peer (HOST pointers tensors[k * n_tensors + t],
- *      numels[t] elements of dtype each) into row k of h_stage[buf] (threaded memcpy);
- *   2. one H2D DMA of the rows into d_stage[buf] on copy_stream;
+ * GPU, each from its own host thread, with that GPU current).  Chunks ramp up — 1/4 and 1/2 of
+ * chunk_elems, then chunk_elems — so the first DMA starts after a quarter-size pack.  For chunk c
+ * (buffer c & 1):
+ *   1. pack: chunk c's elements of every peer (HOST pointers tensors[k * n_tensors + t], numels[t]
+ *      elements of dtype each) into row k of h_stage[buf], rows dense at the chunk's length rounded up
+ *      to 256 bytes (threaded copy with streaming stores);
+ *   2. one contiguous H2D DMA of the rows into d_stage[buf] on copy_stream (made to wait for the
+ *      compute stream only if the reduce that last read d_stage[buf] has not finished yet);
  *   3. the list-order reduce of the rows into d_out[buf] on stream, then a D2H into h_out[buf];
  *   4. while chunk c+1 is packed and copied in: unpack chunk c into outs[t] (HOST pointers).
  * Buffers (caller-owned, untouched by anything else during the call):

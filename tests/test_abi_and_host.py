@@ -115,7 +115,8 @@ def test_library_version_and_argument_errors(lib_path):
     with pytest.raises(_lib.DlaggError, match="aliases peer 5"):
         _lib.wsum_multi_table_ptrs(0, ptrs, [ptrs[5]], [64], [1.0] * 130, 0, 0, 0)
     # launch knobs outside the built set are refused before any launch
-    for bad in (_lib.LaunchCfg(3, 0, 0, 0), _lib.LaunchCfg(4, 3, 0, 0), _lib.LaunchCfg(4, 1, 0, 128)):
+    for bad in (_lib.LaunchCfg(3, 0, 0, 0), _lib.LaunchCfg(4, 3, 0, 0), _lib.LaunchCfg(4, 1, 0, 128),
+                _lib.LaunchCfg(10, 0, 0, 0), _lib.LaunchCfg(11, 0, 0, 0)):  # 16-byte vec forms: not built
         with pytest.raises(_lib.DlaggError):
             _lib.wsum_ptrs(0, [4096], [1.0], 64, 8192, 0, bad)
 
@@ -506,3 +507,35 @@ def test_host_round_routing_and_chunks():
         assert c % align == 0 and c <= -(-bucket // align) * align
         assert n * c * esize <= fa._NATIVE_CHUNK_BYTES
         assert n * c * esize >= min(fa._NATIVE_MIN_CHUNK_BYTES, n * bucket * esize) - n * align * esize
+
+
+def test_fast_parameter_walk_is_parameters():
+    """fedavg._parameters (the layout passes' walk) returns exactly list(m.parameters()): order, tied
+    weights and shared submodules de-duplicated, None parameters skipped; a module class with its own
+    walk falls back to its parameters()."""
+    from torch import nn
+
+    from accdfl_amd.core.gradient_aggregation.fedavg import _parameters
+
+    shared = nn.Linear(3, 3)
+    m = nn.Sequential(nn.Conv2d(2, 4, 3, bias=False), nn.BatchNorm2d(4), shared,
+                      nn.Sequential(shared, nn.Linear(3, 2)), nn.LSTM(3, 5, num_layers=2),
+                      nn.ParameterList([nn.Parameter(torch.ones(2)), nn.Parameter(torch.zeros(3))]),
+                      nn.ParameterDict({"b": nn.Parameter(torch.ones(1)), "a": nn.Parameter(torch.ones(2))}))
+    m[3][1].weight = m[2].weight  # tied across submodules
+    m.extra = nn.Module()
+    m.extra.register_parameter("none", None)
+    assert [id(p) for p in _parameters(m)] == [id(p) for p in m.parameters()]
+
+    class OwnWalk(nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.a, self.b = nn.Linear(2, 2), nn.Linear(2, 2)
+
+        def named_parameters(self, *args, **kw):  # reversed order: a custom walk must be honoured
+            return reversed(list(super().named_parameters(*args, **kw)))
+
+    o = nn.Sequential(nn.Linear(1, 1), OwnWalk())
+    assert [id(p) for p in _parameters(o)] == [id(p) for p in o.parameters()]
+    w = OwnWalk()
+    assert [id(p) for p in _parameters(w)] == [id(p) for p in w.parameters()]
