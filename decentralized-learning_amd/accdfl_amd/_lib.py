@@ -142,6 +142,84 @@ def build_probe(force: bool = False) -> str:
     return out
 
 
+# ------------------------------------------------------------------ host walk extension
+# csrc/walk.cpp: the per-round walk over every parameter of every model (host plumbing, built
+# against torch's headers; not part of the C ABI).  Optional: without it the Python walk runs.
+WALK_SRC = os.path.join(PKG_ROOT, "csrc", "walk.cpp")
+_WALK_ID_PREFIX = b"dlagg-walk-build-id:"
+
+
+def _walk_path() -> str:
+    import sysconfig
+
+    return os.path.join(PKG_ROOT, "lib", "_dla_walk" + sysconfig.get_config_var("EXT_SUFFIX"))
+
+
+def walk_build_id() -> str:
+    """Hash of csrc/walk.cpp, the torch version it is built against and its flags."""
+    import torch
+
+    h = hashlib.sha256()
+    with open(WALK_SRC, "rb") as f:
+        h.update(f.read())
+    h.update(torch.__version__.encode())
+    h.update(" ".join(_walk_flags()).encode())
+    return h.hexdigest()[:20]
+
+
+def _walk_flags():
+    import sysconfig
+
+    import torch
+    from torch.utils import cpp_extension
+
+    abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
+    inc = cpp_extension.include_paths() + [sysconfig.get_paths()["include"]]
+    libdir = cpp_extension.library_paths()[0]
+    return (["-O2", "-shared", "-fPIC", "-std=c++17", "-D_GLIBCXX_USE_CXX11_ABI=%d" % abi,
+             "-DTORCH_EXTENSION_NAME=_dla_walk", "-DTORCH_API_INCLUDE_EXTENSION_H"] + ["-I" + d for d in inc] +
+            ["-L" + libdir, "-ltorch_python", "-ltorch", "-ltorch_cpu", "-lc10", "-Wl,-rpath," + libdir])
+
+
+def build_walk(force: bool = False) -> str:
+    """Compile csrc/walk.cpp (g++) into lib/_dla_walk*.so unless it already carries this tree's id."""
+    out = _walk_path()
+    bid = walk_build_id()
+    if not force and file_build_id(out, _WALK_ID_PREFIX) == bid:
+        return out
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    cxx = os.environ.get("CXX", "g++")
+    subprocess.run([cxx, WALK_SRC, "-o", out + ".tmp", '-DDLA_WALK_BUILD_ID="%s"' % bid] + _walk_flags(), check=True)
+    os.replace(out + ".tmp", out)
+    return out
+
+
+_walk_mod = None
+_walk_tried = False
+
+
+def walk_module():
+    """The loaded host walk extension, or None when it is absent or not built from this tree (the
+    callers then walk in Python: same result, ~10x slower per parameter)."""
+    global _walk_mod, _walk_tried
+    if not _walk_tried:
+        _walk_tried = True
+        path = _walk_path()
+        try:
+            if os.path.exists(path) and file_build_id(path, _WALK_ID_PREFIX) == walk_build_id():
+                import importlib.machinery
+                import importlib.util
+
+                loader = importlib.machinery.ExtensionFileLoader("_dla_walk", path)
+                spec = importlib.util.spec_from_file_location("_dla_walk", path, loader=loader)
+                mod = importlib.util.module_from_spec(spec)
+                loader.exec_module(mod)
+                _walk_mod = mod
+        except (ImportError, OSError):
+            _walk_mod = None
+    return _walk_mod
+
+
 class _Lib:
     def __init__(self, path: str):
         if not os.path.exists(path):
@@ -365,8 +443,10 @@ def host_round_start(dtype_code: int, n_peers: int, tensor_ptrs: Sequence[int], 
     L = lib()
     if not isinstance(numels, ctypes.Array):
         numels = (ctypes.c_int64 * len(numels))(*numels)
-    rc = L.so.dla_host_round_start(dtype_code, n_peers, len(numels), (ctypes.c_void_p * len(tensor_ptrs))(*tensor_ptrs),
-                                   numels, _dbl_array(weights), rows_ptr, pitch_elems, result_ptr, stream_ptr)
+    if not isinstance(tensor_ptrs, ctypes.Array):
+        tensor_ptrs = (ctypes.c_void_p * len(tensor_ptrs))(*tensor_ptrs)
+    rc = L.so.dla_host_round_start(dtype_code, n_peers, len(numels), tensor_ptrs, numels, _dbl_array(weights),
+                                   rows_ptr, pitch_elems, result_ptr, stream_ptr)
     if rc != 0:
         L.check(rc, "dla_host_round_start")
 

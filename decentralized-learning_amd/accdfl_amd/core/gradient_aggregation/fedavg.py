@@ -259,12 +259,36 @@ _WALK_METHODS = ("parameters", "named_parameters", "named_modules", "_named_memb
 _plain_walk_cls: Dict[type, bool] = {}
 
 
+_PLAIN_SET: set = set()  # the plain classes, as the walk extension takes them
+
+
 def _plain_walk(cls: type) -> bool:
     ok = _plain_walk_cls.get(cls)
     if ok is None:
         ok = all(getattr(cls, name, None) is getattr(nn.Module, name) for name in _WALK_METHODS)
         _plain_walk_cls[cls] = ok
+        if ok:
+            _PLAIN_SET.add(cls)
     return ok
+
+
+def _native_layout(models: List[nn.Module], device: int, tensor_major: bool):
+    """The walk extension's one-pass layout (csrc/walk.cpp; ~10x faster per parameter than the Python
+    walk): (dtype, numels, pointer table bytes, device index), or None when the extension is not
+    loaded or the round does not qualify.  Classes it has not seen are classified (models[0]'s tree)
+    and the walk retried once."""
+    mod = _lib.walk_module()
+    if mod is None:
+        return None
+    r = mod.layout(models, device, _PLAIN_SET, tensor_major)
+    if r is None:
+        fresh = [type(sub) for sub in models[0].modules() if type(sub) not in _plain_walk_cls]
+        if any([_plain_walk(cls) for cls in fresh]):
+            r = mod.layout(models, device, _PLAIN_SET, tensor_major)
+    if r is None:
+        return None
+    name, numels, table, dev = r
+    return getattr(torch, name), numels, table, dev
 
 
 def _parameters(model: nn.Module) -> List[nn.Parameter]:
@@ -294,9 +318,16 @@ def _host_layout(models: List[nn.Module]):
     supported dtype and contiguous CPU storage — the models at every reference call site — with the
     parameters' host pointers peer-major, gathered in one pass without a tensor view per parameter
     (a round of 128 ResNet-34 models has 14 080 parameters: a detach + reshape + slice of each costs
-    more than the GPU work); None when the round does not qualify (the general path handles it)."""
+    more than the GPU work); None when the round does not qualify (the general path handles it).
+    The pointers come back as a ctypes array; the walk runs in the walk extension when it is loaded."""
+    if not torch.cuda.is_available():
+        return None
+    nat = _native_layout(models, -1, tensor_major=False)
+    if nat is not None:
+        dtype, numels, table, _ = nat
+        return dtype, numels, (ctypes.c_void_p * (len(table) // 8)).from_buffer_copy(table)
     p0 = _parameters(models[0])
-    if not p0 or not torch.cuda.is_available():
+    if not p0:
         return None
     dtype = p0[0].dtype
     if dtype not in _wsum.SUPPORTED_DTYPES:
@@ -313,7 +344,7 @@ def _host_layout(models: List[nn.Module]):
             if p.shape != shape or p.dtype is not dtype or not p.is_cpu or not p.is_contiguous():
                 return None
             add(p.data_ptr())
-    return dtype, [p.numel() for p in p0], ptrs
+    return dtype, [p.numel() for p in p0], (ctypes.c_void_p * len(ptrs))(*ptrs)
 
 
 def _device_layout(models: List[nn.Module]):
@@ -323,6 +354,11 @@ def _device_layout(models: List[nn.Module]):
     general path handles it).  The table is [n_tensors x n_peers] uint64, as dla_wsum_multi takes it."""
     import numpy as np
 
+    nat = _native_layout(models, -2, tensor_major=True)
+    if nat is not None:
+        dtype, numels, table, dev = nat
+        return (dtype, torch.device("cuda", dev), numels,
+                np.frombuffer(table, dtype=np.uint64).reshape(len(numels), len(models)).copy())
     p0 = _parameters(models[0])
     if not p0 or not p0[0].is_cuda:
         return None
@@ -427,7 +463,7 @@ def _large_round(models: List[nn.Module], weights, layout) -> "nn.Module | None"
     if len(params) != len(numels) or not all(c is not None and c.is_cpu and c.is_contiguous() for c in params):
         return None
     code = _wsum.dtype_code(dtype)
-    tensor_arr = (ctypes.c_void_p * len(ptrs))(*ptrs)
+    tensor_arr = ptrs  # a ctypes array (_host_layout)
     numel_arr = (ctypes.c_int64 * len(numels))(*numels)
     out_arr = (ctypes.c_void_p * len(params))(*[c.data_ptr() for c in params])
     with _staging_lock:

@@ -539,3 +539,48 @@ def test_fast_parameter_walk_is_parameters():
     assert [id(p) for p in _parameters(o)] == [id(p) for p in o.parameters()]
     w = OwnWalk()
     assert [id(p) for p in _parameters(w)] == [id(p) for p in w.parameters()]
+
+
+def test_native_walk_matches_the_python_walk():
+    """csrc/walk.cpp (the host walk extension) returns the pointers of list(m.parameters()) for every
+    model — tied weights and shared submodules de-duplicated, None parameters skipped — peer- or
+    tensor-major, and None when the round does not qualify (shapes, dtypes, devices, density)."""
+    import numpy as np
+    from torch import nn
+
+    from accdfl_amd import _lib
+    from accdfl_amd.core.gradient_aggregation import fedavg as fa
+
+    _lib.build_walk()
+    _lib._walk_tried = False
+    assert _lib.walk_module() is not None
+
+    def model(seed):
+        torch.manual_seed(seed)
+        shared = nn.Linear(3, 3)
+        m = nn.Sequential(nn.Conv2d(2, 4, 3, bias=False), nn.BatchNorm2d(4), shared,
+                          nn.Sequential(shared, nn.Linear(3, 2)), nn.LSTM(3, 5),
+                          nn.ParameterList([nn.Parameter(torch.ones(2))]))
+        m[3][1].weight = m[2].weight
+        m.extra = nn.Module()
+        m.extra.register_parameter("none", None)
+        return m
+
+    models = [model(k) for k in range(5)]
+    want = [[p.data_ptr() for p in m.parameters()] for m in models]
+    dtype, numels, table, dev = fa._native_layout(models, -1, tensor_major=False)
+    assert dtype is torch.float32 and dev == -1
+    assert numels == [p.numel() for p in models[0].parameters()]
+    assert np.frombuffer(table, dtype=np.uint64).tolist() == [x for row in want for x in row]
+    _, _, table_t, _ = fa._native_layout(models, -1, tensor_major=True)
+    assert np.frombuffer(table_t, dtype=np.uint64).reshape(len(numels), 5).T.reshape(-1).tolist() == \
+        [x for row in want for x in row]
+    bad = [model(9) for _ in range(2)]
+    bad[1][0].weight = nn.Parameter(torch.zeros(4, 2, 3, 2))  # shape differs
+    assert fa._native_layout(bad, -1, tensor_major=False) is None
+    half = [model(9).half(), model(9)]  # dtype differs
+    assert fa._native_layout(half, -1, tensor_major=False) is None
+    strided = [model(9)]
+    strided[0][0].weight = nn.Parameter(torch.zeros(4, 2, 3, 6)[..., ::2])  # not dense
+    assert fa._native_layout(strided, -1, tensor_major=False) is None
+    assert fa._native_layout(models, 0, tensor_major=False) is None  # CPU models asked for device 0

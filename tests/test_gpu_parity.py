@@ -26,6 +26,7 @@ def _native():
     # refuses it loudly if its build id is not this tree's (a stale prebuilt .so)
     L = _lib.lib()
     assert L.build_id == _lib.source_build_id()
+    assert _lib.walk_module() is not None, "the host walk extension is not built from this tree"
     yield
 
 
