@@ -23,7 +23,7 @@ LIB_PATH = os.environ.get("DLAGG_LIB", os.path.join(PKG_ROOT, "lib", "libdlagg.s
 
 # dtype codes (include/dlagg.h)
 DLA_F32, DLA_BF16, DLA_F16, DLA_F64 = 0, 1, 2, 3
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 HIPCC_FLAGS = [
     "--offload-arch=gfx950",
@@ -59,6 +59,7 @@ EXPORTED = (
     "dla_host_round_start",
     "dla_host_round_finish",
     "dla_host_reduce",
+    "dla_host_reduce_deferred",
     "dla_wsum_multi_table_bytes",
     "dla_wsum_multi_table",
 )
@@ -287,6 +288,11 @@ class _Lib:
                                        ctypes.POINTER(vp), ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, vp, vp,
                                        vp, vp, vp, vp]
         so.dla_host_reduce.restype = ctypes.c_int
+        so.dla_host_reduce_deferred.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(vp),
+                                                ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_double),
+                                                ctypes.POINTER(vp), ctypes.POINTER(ctypes.c_int), ctypes.c_int64,
+                                                ctypes.c_int64, ctypes.c_int64, vp, vp, vp, vp, vp, vp]
+        so.dla_host_reduce_deferred.restype = ctypes.c_int
         so.dla_wsum_multi_table_bytes.argtypes = [ctypes.c_int, ctypes.c_int]
         so.dla_wsum_multi_table_bytes.restype = ctypes.c_int64
         so.dla_wsum_multi_table.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(vp), ctypes.POINTER(vp),
@@ -453,10 +459,12 @@ def host_round_start(dtype_code: int, n_peers: int, tensor_ptrs: Sequence[int], 
 
 def host_reduce(dtype_code: int, n_peers: int, tensor_ptrs, numels, weights: Sequence[float], out_ptrs,
                 begin: int, end: int, chunk_elems: int, h_stage: int, d_stage: int, h_out: int, d_out: int,
-                stream_ptr: int, copy_stream_ptr: int) -> None:
+                stream_ptr: int, copy_stream_ptr: int, outs_ready: "ctypes.c_int | None" = None) -> None:
     """dla_host_reduce: flat elements [begin, end) of a round of host tensors through the GPU in packed
     chunks (synchronous).  ``tensor_ptrs``: peer-major, n_peers * len(numels) host pointers;
-    ``out_ptrs``: one per tensor.  Sequences or ctypes arrays (reused across the buckets of a round)."""
+    ``out_ptrs``: one per tensor.  Sequences or ctypes arrays (reused across the buckets of a round).
+    ``outs_ready`` (a ctypes.c_int): dla_host_reduce_deferred — ``out_ptrs`` must then be a ctypes
+    array the caller fills in place, then sets ``outs_ready.value`` to 1 (or -1 to give up)."""
     L = lib()
     if not isinstance(numels, ctypes.Array):
         numels = (ctypes.c_int64 * len(numels))(*numels)
@@ -464,8 +472,14 @@ def host_reduce(dtype_code: int, n_peers: int, tensor_ptrs, numels, weights: Seq
         tensor_ptrs = (ctypes.c_void_p * len(tensor_ptrs))(*tensor_ptrs)
     if not isinstance(out_ptrs, ctypes.Array):
         out_ptrs = (ctypes.c_void_p * len(out_ptrs))(*out_ptrs)
-    rc = L.so.dla_host_reduce(dtype_code, n_peers, len(numels), tensor_ptrs, numels, _dbl_array(weights), out_ptrs,
-                              begin, end, chunk_elems, h_stage, d_stage, h_out, d_out, stream_ptr, copy_stream_ptr)
+    if outs_ready is None:
+        rc = L.so.dla_host_reduce(dtype_code, n_peers, len(numels), tensor_ptrs, numels, _dbl_array(weights),
+                                  out_ptrs, begin, end, chunk_elems, h_stage, d_stage, h_out, d_out, stream_ptr,
+                                  copy_stream_ptr)
+    else:
+        rc = L.so.dla_host_reduce_deferred(dtype_code, n_peers, len(numels), tensor_ptrs, numels,
+                                           _dbl_array(weights), out_ptrs, ctypes.byref(outs_ready), begin, end,
+                                           chunk_elems, h_stage, d_stage, h_out, d_out, stream_ptr, copy_stream_ptr)
     if rc != 0:
         L.check(rc, "dla_host_reduce")
 

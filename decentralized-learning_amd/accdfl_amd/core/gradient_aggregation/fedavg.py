@@ -456,16 +456,15 @@ def _large_round(models: List[nn.Module], weights, layout) -> "nn.Module | None"
     device = _wsum.require_device(None)
     devices = _devices_for(device, total * esize)
     devices = devices[:max(1, min(len(devices), (total * esize) // _MIN_SHARD_BYTES))]
-    # the result's parameters first; the module tree (deepcopy of models[0], fedavg.py:20) is cloned
-    # on this thread while the native call streams the round through the GPU on another
-    memo = _fresh_params(models[0])
-    params = [memo.get(id(p)) for p in models[0].parameters()] if len(memo) == len(numels) else []
-    if len(params) != len(numels) or not all(c is not None and c.is_cpu and c.is_contiguous() for c in params):
-        return None
+    # The native call starts streaming the round through the GPU at once, on another thread; this one
+    # allocates the result's parameters meanwhile, publishes them (out_arr, then ready = 1: only the
+    # native call's first unpack waits for them, dla_host_reduce_deferred), then clones the module
+    # tree around them (deepcopy of models[0], fedavg.py:20) while the call runs on.
     code = _wsum.dtype_code(dtype)
     tensor_arr = ptrs  # a ctypes array (_host_layout)
     numel_arr = (ctypes.c_int64 * len(numels))(*numels)
-    out_arr = (ctypes.c_void_p * len(params))(*[c.data_ptr() for c in params])
+    out_arr = (ctypes.c_void_p * len(numels))()
+    ready = ctypes.c_int(0)
     with _staging_lock:
         jobs = []
         for i, (dev, (s, e)) in enumerate(zip(devices, bucket_bounds(total, len(devices), align))):
@@ -481,14 +480,26 @@ def _large_round(models: List[nn.Module], weights, layout) -> "nn.Module | None"
             with torch.cuda.device(dev):
                 _lib.host_reduce(code, n, tensor_arr, numel_arr, weights, out_arr, s, e, chunk,
                                  st.h_stage.data_ptr(), st.d_stage.data_ptr(), st.h_out.data_ptr(),
-                                 st.d_out.data_ptr(), compute.cuda_stream, st.copy_stream.cuda_stream)
+                                 st.d_out.data_ptr(), compute.cuda_stream, st.copy_stream.cuda_stream,
+                                 outs_ready=ready)
 
         futures = [_round_executor().submit(bucket, job) for job in jobs]
+        center = None
         try:
-            center = _clone_value(models[0], memo)
+            memo = _fresh_params(models[0])
+            params = [memo.get(id(p)) for p in models[0].parameters()] if len(memo) == len(numels) else []
+            if len(params) == len(numels) and all(c is not None and c.is_cpu and c.is_contiguous() for c in params):
+                for i, c in enumerate(params):
+                    out_arr[i] = c.data_ptr()
+                ready.value = 1
+                center = _clone_value(models[0], memo)
         finally:
+            if ready.value == 0:
+                ready.value = -1  # no result tensors: the native calls drain and give up
             for f in futures:
                 f.exception()  # waits; every bucket has finished with the staging before the lock goes
+        if ready.value < 0:
+            return None  # the general path handles this round (the abandoned calls' errors are expected)
         for f in futures:
             f.result()  # re-raises the first failure
     return center

@@ -20,6 +20,7 @@ by ``ACCDFL_AMD_RESULT_MEMORY`` or ``set_result_memory``:
 """
 from __future__ import annotations
 
+import math
 import mmap
 import os
 import threading
@@ -67,6 +68,15 @@ class _Pool:
         self._free: Dict[int, List[mmap.mmap]] = {}
         self._free_bytes = 0
         self._lock = threading.Lock()
+        # id(weakref) -> (weakref, size, block) of every block handed out: the weakref's callback returns
+        # the block (a plain weakref callback, ~1 us, where weakref.finalize costs ~10 us per tensor)
+        self._live: Dict[int, tuple] = {}
+
+    def _dead(self, ref: weakref.ref):
+        with self._lock:
+            item = self._live.pop(id(ref), None)
+        if item is not None:
+            self._release(item[1], item[2])
 
     def _release(self, size: int, block: mmap.mmap):
         with self._lock:
@@ -75,10 +85,10 @@ class _Pool:
                 self._free_bytes += size
         # otherwise the block is dropped: unmapped once the dying array lets go of it
 
-    def take(self, shape, dtype: torch.dtype) -> torch.Tensor:
-        numel = int(np.prod(shape)) if len(shape) else 1
-        esize = torch.empty((), dtype=dtype).element_size()
-        size = -(-numel * esize // mmap.PAGESIZE) * mmap.PAGESIZE
+    def take(self, shape, dtype: torch.dtype, numel: "int | None" = None) -> torch.Tensor:
+        if numel is None:
+            numel = math.prod(shape)
+        size = -(-numel * dtype.itemsize // mmap.PAGESIZE) * mmap.PAGESIZE
         with self._lock:
             blocks = self._free.get(size)
             block = blocks.pop() if blocks else None
@@ -92,11 +102,11 @@ class _Pool:
                 except OSError:
                     pass
         arr = np.frombuffer(block, dtype=_NP[dtype], count=numel)
-        weakref.finalize(arr, self._release, size, block)
-        t = torch.from_numpy(arr)
-        if dtype == torch.bfloat16:
-            t = t.view(torch.bfloat16)
-        return t.view(tuple(shape))
+        ref = weakref.ref(arr, self._dead)
+        with self._lock:
+            self._live[id(ref)] = (ref, size, block)
+        t = torch.from_numpy(arr.reshape(shape))  # the tensor keeps arr (and so the block) alive
+        return t.view(torch.bfloat16) if dtype == torch.bfloat16 else t
 
     def free_bytes(self) -> int:
         return self._free_bytes
@@ -107,11 +117,11 @@ _pool = _Pool()
 
 def result_tensor(shape, dtype: torch.dtype) -> torch.Tensor:
     """An uninitialised contiguous CPU tensor for a result parameter, per the mode."""
-    numel = int(np.prod(shape)) if len(shape) else 1
-    nbytes = numel * torch.empty((), dtype=dtype).element_size()
+    numel = math.prod(shape)
+    nbytes = numel * dtype.itemsize
     if nbytes >= POOL_MIN_BYTES:  # smaller tensors: plain torch.empty in every mode
         if _mode == "pooled" and dtype in _NP:
-            return _pool.take(tuple(shape), dtype)
+            return _pool.take(tuple(shape), dtype, numel)
         if _mode == "pinned" and torch.cuda.is_available():
             return torch.empty(tuple(shape), dtype=dtype, pin_memory=True)
     return torch.empty(tuple(shape), dtype=dtype)

@@ -139,10 +139,16 @@ template <> struct Ops<DLA_F64> {
 // bf16: op-math float, every product and every sum rounded RNE to bf16
 // (torch-CPU reduced-float kernels: float(a) * float(w) -> bf16; float(c) + float(t) -> bf16).
 __device__ inline float bf16_bits_to_f(uint32_t h) { return __uint_as_float(h << 16); }
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 __device__ inline float round_bf16(float f) {
-  // Plain cast: v_cvt_pk_bf16_f32 on gfx950, round-to-nearest-even, NaN stays NaN.
-  __bf16 b = static_cast<__bf16>(f);
-  return static_cast<float>(b);
+  // v_cvt_pk_bf16_f32 (round-to-nearest-even, NaN stays NaN) with a zero LOW operand: the rounded
+  // bf16 lands in the high half over a zero low half, which IS the rounded value's f32 bit pattern
+  // — one instruction, where a cast back to f32 costs a cvt plus a shift or mask per element.
+  const bf16x2 h = __builtin_convertvector(f32x2{0.0f, f}, bf16x2);
+  uint32_t bits;
+  __builtin_memcpy(&bits, &h, 4);
+  return __uint_as_float(bits);
 }
 
 template <> struct Ops<DLA_BF16> {
@@ -185,15 +191,9 @@ template <> struct Ops<DLA_BF16> {
 
 // Two bf16 FedAvg steps on one 32-bit word of two bf16 values (element 0 in the low half):
 // acc[e] = R(acc[e] + R(w * x[e])), R = RNE to bf16, op-math fp32 — Ops<DLA_BF16>::step on
-// both elements, with packed fp32 ops and one packed conversion per rounding.
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
-__device__ inline f32x2 round_bf16x2(f32x2 v) {
-  const bf16x2 h = __builtin_convertvector(v, bf16x2);  // v_cvt_pk_bf16_f32 (RNE, NaN kept)
-  uint32_t bits;
-  __builtin_memcpy(&bits, &h, 4);
-  return f32x2{__uint_as_float(bits << 16), __uint_as_float(bits & 0xffff0000u)};
-}
+// both elements, with packed fp32 ops and one conversion per element per rounding
+// (round_bf16: 8 VALU per word and step against 10 for one packed conversion + shift + mask).
+__device__ inline f32x2 round_bf16x2(f32x2 v) { return f32x2{round_bf16(v.x), round_bf16(v.y)}; }
 __device__ inline void bf16_step2(float& a0, float& a1, float w, uint32_t word) {
   const f32x2 x = {__uint_as_float(word << 16), __uint_as_float(word & 0xffff0000u)};
   const f32x2 prod = round_bf16x2(x * w);               // fedavg.py:25 w * p1
@@ -2389,9 +2389,13 @@ struct Events {
 };
 }  // namespace
 
-int dla_host_reduce(int dtype, int n_peers, int n_tensors, const void* const* tensors, const int64_t* numels,
-                    const double* weights, void* const* outs, int64_t begin, int64_t end, int64_t chunk_elems,
-                    void* h_stage, void* d_stage, void* h_out, void* d_out, void* stream, void* copy_stream) {
+namespace {
+// dla_host_reduce and dla_host_reduce_deferred: outs_ready == nullptr means outs[] is valid on entry;
+// otherwise outs[] is read only once *outs_ready turns non-zero (> 0: filled; < 0: the caller gave up).
+int host_reduce_impl(int dtype, int n_peers, int n_tensors, const void* const* tensors, const int64_t* numels,
+                     const double* weights, void* const* outs, const int* outs_ready, int64_t begin, int64_t end,
+                     int64_t chunk_elems, void* h_stage, void* d_stage, void* h_out, void* d_out, void* stream,
+                     void* copy_stream) {
   g_last_error.clear();
   const int es = elem_size(dtype);
   if (es == 0) return fail(DLA_E_INVALID, "dla_host_reduce: unknown dtype");
@@ -2403,7 +2407,8 @@ int dla_host_reduce(int dtype, int n_peers, int n_tensors, const void* const* te
   std::vector<int64_t> start(n_tensors + 1, 0);
   for (int t = 0; t < n_tensors; ++t) {
     if (numels[t] < 0) return fail(DLA_E_INVALID, "dla_host_reduce: negative numel at " + std::to_string(t));
-    if (numels[t] > 0 && !outs[t]) return fail(DLA_E_INVALID, "dla_host_reduce: null output " + std::to_string(t));
+    if (!outs_ready && numels[t] > 0 && !outs[t])
+      return fail(DLA_E_INVALID, "dla_host_reduce: null output " + std::to_string(t));
     start[t + 1] = start[t] + numels[t];
   }
   for (int i = 0; i < n_peers * n_tensors; ++i)
@@ -2460,9 +2465,32 @@ int dla_host_reduce(int dtype, int n_peers, int n_tensors, const void* const* te
     }
     return r == hipSuccess;
   };
+  // Deferred outputs: the first unpack waits for the caller to publish outs[] (it allocates the
+  // result's tensors while the first chunks are packed and copied in).  Acquire load: the caller's
+  // stores into outs[] before its flag store are visible once the flag is.
+  bool outs_known = outs_ready == nullptr;
+  auto await_outs = [&]() {
+    if (outs_known) return true;
+    int v;
+    while ((v = __atomic_load_n(outs_ready, __ATOMIC_ACQUIRE)) == 0) std::this_thread::yield();
+    if (v < 0) {
+      e = hipErrorInvalidValue;
+      g_last_error = "dla_host_reduce: the caller abandoned the outputs";
+      return false;
+    }
+    for (int t = 0; t < n_tensors; ++t)
+      if (numels[t] > 0 && !outs[t]) {
+        e = hipErrorInvalidValue;
+        g_last_error = "dla_host_reduce: null output " + std::to_string(t);
+        return false;
+      }
+    outs_known = true;
+    return true;
+  };
   // chunk c's averaged elements (h_out buffer c & 1) -> the result tensors (fedavg.py:25)
   auto unpack = [&](int64_t c) {
     const int buf = static_cast<int>(c & 1);
+    if (!await_outs()) return;
     if (!check(hipEventSynchronize(d2h[buf]), "D2H")) return;
     const int64_t c0 = cs[c], c1 = cs[c + 1];
     dsts.clear(), srcs.clear(), bytes.clear();
@@ -2549,9 +2577,27 @@ int dla_host_reduce(int dtype, int n_peers, int n_tensors, const void* const* te
   if (e != hipSuccess) {
     (void)hipStreamSynchronize(cs_);
     (void)hipStreamSynchronize(xs);
+    if (!outs_known && !g_last_error.empty()) return DLA_E_INVALID;  // abandoned / null outputs
     return static_cast<int>(e);
   }
   return DLA_OK;
+}
+}  // namespace
+
+int dla_host_reduce(int dtype, int n_peers, int n_tensors, const void* const* tensors, const int64_t* numels,
+                    const double* weights, void* const* outs, int64_t begin, int64_t end, int64_t chunk_elems,
+                    void* h_stage, void* d_stage, void* h_out, void* d_out, void* stream, void* copy_stream) {
+  return host_reduce_impl(dtype, n_peers, n_tensors, tensors, numels, weights, outs, nullptr, begin, end, chunk_elems,
+                          h_stage, d_stage, h_out, d_out, stream, copy_stream);
+}
+
+int dla_host_reduce_deferred(int dtype, int n_peers, int n_tensors, const void* const* tensors, const int64_t* numels,
+                             const double* weights, void* const* outs, const int* outs_ready, int64_t begin,
+                             int64_t end, int64_t chunk_elems, void* h_stage, void* d_stage, void* h_out, void* d_out,
+                             void* stream, void* copy_stream) {
+  if (!outs_ready) return fail(DLA_E_INVALID, "dla_host_reduce_deferred: outs_ready is required");
+  return host_reduce_impl(dtype, n_peers, n_tensors, tensors, numels, weights, outs, outs_ready, begin, end,
+                          chunk_elems, h_stage, d_stage, h_out, d_out, stream, copy_stream);
 }
 
 int dla_shard_range(int dtype, int64_t n_elems, int n_shards, int shard, int64_t* start, int64_t* end) {

@@ -329,6 +329,70 @@ __global__ __launch_bounds__(64) void mread_unrolled_kernel(const SrcTable tab, 
   }
 }
 
+// LDS-DMA staging of the north star: the FedAvg fp32 fold of 8 peers held in
+// the tile-interleaved slab ([tiles][8][4096 f32], 16 KiB tiles — the headline's layout), with
+// every peer load a global_load_lds_dwordx4 into LDS instead of a VGPR load.  Persistent: a
+// one-wave workgroup walks units u = wave, wave + n_waves, ... of 1 KiB of output (64 lanes x
+// 16 B) through S LDS stages of 8 x 1 KiB, so S x 8 KiB per wave are in flight with no VGPR
+// held for them.  A stage is consumed after `s_waitcnt vmcnt(8 (S - 1))` — the loads of the S - 1
+// younger stages may stay in flight; the output stores, if the counter tallies them, only make
+// that wait stricter.  Each lane reads back only the 16 B it loaded (an LDS-DMA piece lands at
+// base + lane x 16), so the issuing wave's own counter is the only ordering needed.  The fold is
+// the product's fp32 fold (p0 * 0, then acc + w * p in list order, no FMA), so the probe's output
+// is compared bit for bit with dla_wsum_slab_tiled's.  Units past n_units (the < 256-element
+// tail) are not computed.
+template <int S>
+__global__ __launch_bounds__(64) void ldsdma_tiled8_kernel(const float* __restrict__ slab, const float w0,
+                                                           const float w1, const float w2, const float w3,
+                                                           const float w4, const float w5, const float w6,
+                                                           const float w7, int64_t n_units, float* __restrict__ out) {
+  __shared__ u32x4 stage[S][8][64];
+  const float w[8] = {w0, w1, w2, w3, w4, w5, w6, w7};
+  const int lane = threadIdx.x;
+  const int64_t n_waves = gridDim.x;
+  const int64_t first = blockIdx.x;
+  // unit u: tile u >> 4, 1 KiB piece u & 15 of it; peer k's piece at ((u >> 4) * 8 + k) * 4096 + (u & 15) * 256
+  auto issue = [&](int b, int64_t u) {
+    const float* src = slab + ((u >> 4) * 8) * 4096 + (u & 15) * 256 + lane * 4;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const uint32_t lds = __builtin_amdgcn_readfirstlane(
+          static_cast<uint32_t>(reinterpret_cast<uintptr_t>(&stage[b][k][0])));
+      uint32_t keep;
+      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                   : "=&s"(keep) : "v"(src + k * 4096), "s"(lds) : "memory");
+    }
+  };
+  int64_t u = first;
+#pragma unroll
+  for (int b = 0; b < S; ++b)
+    if (u + b * n_waves < n_units) issue(b, u + b * n_waves);
+  if (u + (S - 1) * n_waves >= n_units) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // < S stages issued
+  for (int it = 0; u < n_units; ++it, u += n_waves) {
+    const int b = it % S;
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(8 * (S - 1)) : "memory");
+    u32x4 v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = stage[b][k][lane];
+    float acc[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) acc[e] = __uint_as_float(v[0][e]) * 0.0f;  // fedavg.py:22
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc[e] = acc[e] + w[k] * __uint_as_float(v[k][e]);  // fedavg.py:25
+    u32x4 o = {__float_as_uint(acc[0]), __float_as_uint(acc[1]), __float_as_uint(acc[2]), __float_as_uint(acc[3])};
+    u32x4* dst = reinterpret_cast<u32x4*>(out + u * 256) + lane;
+    asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(dst), "v"(o) : "memory");
+    const int64_t nu = u + S * n_waves;
+    if (nu < n_units) {
+      issue(b, nu);
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain: the count above assumes S stages in flight
+    }
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -538,6 +602,33 @@ int dlp_mread_unrolled(const void* const* srcs, int64_t bytes_each, void* dst, v
   else if (width == 4 && group == 64) DLP_MU(uint32_t, 64);
   else return -1;
 #undef DLP_MU
+  return static_cast<int>(hipGetLastError());
+}
+
+// The LDS-DMA north-star probe (ldsdma_tiled8_kernel): slab = [tiles][8][4096] f32, w8 = 8
+// fp32 weights, n_elems per peer (units of 256 computed; the tail is not), stages in {2, 3, 4, 6},
+// grid = persistent one-wave workgroups (<= 0: 256 CUs x the stage's LDS-limited occupancy).
+int dlp_ldsdma_tiled8(const void* slab, const float* w8, int64_t n_elems, void* out, int stages, int grid,
+                      void* stream) {
+  if (!slab || !w8 || !out || n_elems < 256) return -1;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const int64_t n_units = n_elems / 256;
+  const float* sl = static_cast<const float*>(slab);
+  float* o = static_cast<float*>(out);
+#define DLP_LD(SV)                                                                                               \
+  do {                                                                                                           \
+    const int g = grid > 0 ? grid : 256 * (160 / (8 * (SV)));                                                    \
+    hipLaunchKernelGGL((ldsdma_tiled8_kernel<SV>), dim3(g), dim3(64), 0, s, sl, w8[0], w8[1], w8[2], w8[3], w8[4], \
+                       w8[5], w8[6], w8[7], n_units, o);                                                         \
+  } while (0)
+  switch (stages) {
+    case 2: DLP_LD(2); break;
+    case 3: DLP_LD(3); break;
+    case 4: DLP_LD(4); break;
+    case 6: DLP_LD(6); break;
+    default: return -1;
+  }
+#undef DLP_LD
   return static_cast<int>(hipGetLastError());
 }
 

@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define DLA_ABI_VERSION 8
+#define DLA_ABI_VERSION 9
 
 /* element dtypes of the peer buffers and of the output */
 #define DLA_F32 0
@@ -267,6 +267,17 @@ int dla_host_round_finish(int dtype, int n_tensors, const int64_t* numels, const
 int dla_host_reduce(int dtype, int n_peers, int n_tensors, const void* const* tensors, const int64_t* numels,
                     const double* weights, void* const* outs, int64_t begin, int64_t end, int64_t chunk_elems,
                     void* h_stage, void* d_stage, void* h_out, void* d_out, void* stream, void* copy_stream);
+
+/* dla_host_reduce with the outputs published late: outs[] is read only once *outs_ready (written by
+ * the caller, read with acquire semantics) turns non-zero — > 0: outs[] is filled; < 0: the caller
+ * gives up, and the call drains its copies and returns DLA_E_INVALID.  The caller starts the call on
+ * one thread, allocates the result tensors on another while the first chunks are packed, copied in
+ * and reduced (fedavg.py:20's deepcopy and the reduce overlap), fills outs[], then sets the flag;
+ * only the first unpack waits for it.  outs_ready must not be NULL.  ABI v9. */
+int dla_host_reduce_deferred(int dtype, int n_peers, int n_tensors, const void* const* tensors, const int64_t* numels,
+                             const double* weights, void* const* outs, const int* outs_ready, int64_t begin,
+                             int64_t end, int64_t chunk_elems, void* h_stage, void* d_stage, void* h_out, void* d_out,
+                             void* stream, void* copy_stream);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,136 @@
+"""r03 interleaved A/B on the tile-interleaved slab (dla_wsum_slab_tiled), one process:
+  * the tree's libdlagg.so against a saved build (--base, default lib/ab/libdlagg_r03base.so), bit
+    for bit on every shape;
+  * the LDS-DMA probe of the north star (probe dlp_ldsdma_tiled8, S stages of 8 x 1 KiB
+    global_load_lds_dwordx4 per wave, persistent one-wave workgroups) against the product kernel,
+    bit for bit on the units it computes.
+Shapes: the north star (8 x 25 M f32, 16 KiB tiles), configs[4]'s per-GPU share (128 x 2 662 045
+bf16, 4 KiB), configs[4] whole (128 x 21 296 355 bf16, 4 KiB), 16 x 21.3 M bf16 (16 KiB).
+Median over interleaved rounds of HIP-event time per launch (events on the launch stream)."""
+import argparse
+import ctypes
+import json
+import os
+import statistics
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "decentralized-learning_amd"))
+from accdfl_amd import _lib  # noqa: E402
+
+vp, i64 = ctypes.c_void_p, ctypes.c_int64
+
+
+def bind_tiled(so):
+    so.dla_wsum_slab_tiled.argtypes = [ctypes.c_int, vp, i64, i64, ctypes.POINTER(ctypes.c_double), ctypes.c_int,
+                                       i64, vp, vp, vp]
+    so.dla_wsum_slab_tiled.restype = ctypes.c_int
+    return so
+
+
+def ev_time(fn, reps, stream):
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    fn()
+    e0.record(stream)
+    for _ in range(reps):
+        fn()
+    e1.record(stream)
+    e1.synchronize()
+    return e0.elapsed_time(e1) / reps * 1e3  # us per launch
+
+
+def settle(fn, seconds=0.2):
+    t = time.time()
+    while time.time() - t < seconds:
+        for _ in range(20):
+            fn()
+        torch.cuda.synchronize()
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--base", default=os.path.join(ROOT, "decentralized-learning_amd", "lib", "ab", "libdlagg_r03base.so"))
+    ap.add_argument("--rounds", type=int, default=7)
+    ap.add_argument("--reps", type=int, default=30)
+    ap.add_argument("--shapes", default="ns,c4share,c4whole,b16")
+    ap.add_argument("--stages", default="2,3,4,6")
+    ap.add_argument("--grids", default="0")
+    args = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    stream = torch.cuda.current_stream(dev)
+    sp = stream.cuda_stream
+    libs = {"tree": bind_tiled(_lib.lib().so)}
+    if args.base and os.path.exists(args.base):
+        libs["base"] = bind_tiled(ctypes.CDLL(os.path.abspath(args.base)))
+    probe = ctypes.CDLL(_lib.build_probe())
+    probe.dlp_ldsdma_tiled8.argtypes = [vp, ctypes.POINTER(ctypes.c_float), i64, vp, ctypes.c_int, ctypes.c_int, vp]
+    probe.dlp_ldsdma_tiled8.restype = ctypes.c_int
+    shapes = {
+        "ns": ("north star 8 x 25 M f32", 8, 25_000_000, torch.float32, 16384),
+        "c4share": ("configs[4] share 128 x 2 662 045 bf16", 128, 2_662_045, torch.bfloat16, 4096),
+        "c4whole": ("configs[4] whole 128 x 21 296 355 bf16", 128, 21_296_355, torch.bfloat16, 4096),
+        "b16": ("16 x 21 296 355 bf16", 16, 21_296_355, torch.bfloat16, 16384),
+    }
+    g = torch.Generator(device="cpu").manual_seed(3)
+    for key in args.shapes.split(","):
+        name, n, p, dt, tile_b = shapes[key]
+        es = torch.tensor([], dtype=dt).element_size()
+        te = tile_b // es
+        n_t = -(-p // te)
+        slab = torch.empty(n_t * n * te, dtype=dt, device=dev)
+        slab.normal_(0, 0.05)
+        w = torch.distributions.Dirichlet(torch.ones(n)).sample().tolist()
+        wa = (ctypes.c_double * n)(*w)
+        code = {torch.float32: 0, torch.bfloat16: 1}[dt]
+        outs = {}
+        legs = {}
+        for lname, so in libs.items():
+            o = torch.empty(p, dtype=dt, device=dev)
+            outs[lname] = o
+
+            def fn(so=so, o=o):
+                rc = so.dla_wsum_slab_tiled(code, slab.data_ptr(), te, n, wa, n, p, o.data_ptr(), sp, None)
+                if rc != 0:
+                    raise RuntimeError("dla_wsum_slab_tiled rc=%d" % rc)
+            legs[lname] = fn
+        if key == "ns":
+            w8 = (ctypes.c_float * 8)(*[float(torch.tensor(x, dtype=torch.float32)) for x in w])
+            for s in [int(x) for x in args.stages.split(",")]:
+                for gr in [int(x) for x in args.grids.split(",")]:
+                    o = torch.zeros(p, dtype=dt, device=dev)
+                    lname = "ldsdma S=%d grid=%s" % (s, gr or "auto")
+                    outs[lname] = o
+
+                    def fn(s=s, gr=gr, o=o):
+                        rc = probe.dlp_ldsdma_tiled8(slab.data_ptr(), w8, p, o.data_ptr(), s, gr, sp)
+                        if rc != 0:
+                            raise RuntimeError("dlp_ldsdma_tiled8 rc=%d" % rc)
+                    legs[lname] = fn
+        for fn in legs.values():
+            settle(fn)
+        res = {k: [] for k in legs}
+        for _ in range(args.rounds):
+            for k, fn in legs.items():
+                res[k].append(ev_time(fn, args.reps, stream))
+        torch.cuda.synchronize()
+        ref = outs["tree"]
+        byts = (n + 1) * p * es
+        for k in legs:
+            o = outs[k]
+            cover = p if not k.startswith("ldsdma") else p // 256 * 256
+            same = bool(torch.equal(o[:cover].view(torch.int16 if es == 2 else torch.int32),
+                                    ref[:cover].view(torch.int16 if es == 2 else torch.int32)))
+            t = statistics.median(res[k])
+            print(json.dumps({"shape": name, "leg": k, "us": round(t, 2), "min_us": round(min(res[k]), 2),
+                              "GB/s": round(byts / t / 1e3, 1), "frac_8TBs": round(byts / t / 1e3 / 8000, 4),
+                              "bit_exact_vs_tree": same}), flush=True)
+        del slab, outs, legs
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()

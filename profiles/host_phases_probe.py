@@ -25,7 +25,9 @@ for c in cfgs:
     dt = torch.float32 if dts == "f32" else torch.bfloat16
     models, p = bench._layout_models(lay, n, dt, False)
     w = [1.0 / n] * n
-    phases = {k: [] for k in ("layout", "fresh_params", "clone", "host_reduce_call", "aggregate_total")}
+    phases = {k: [] for k in ("layout", "fresh_params", "clone", "host_reduce_call", "aggregate_total",
+                              "pre_native", "post_native")}
+    stamps = {}
     orig = (fa._host_layout, fa._fresh_params, fa._clone_value, fa._lib.host_reduce)
 
     depth = {}
@@ -34,12 +36,15 @@ for c in cfgs:
         def wrap(*a, **kw):  # the outermost call only (_clone_value recurses through the module name)
             depth[key] = depth.get(key, 0) + 1
             t0 = time.perf_counter()
+            stamps.setdefault(key + "_enter", t0)
             try:
                 return fn(*a, **kw)
             finally:
                 depth[key] -= 1
                 if depth[key] == 0:
-                    phases[key].append((time.perf_counter() - t0) * 1e3)
+                    t1 = time.perf_counter()
+                    stamps[key + "_exit"] = t1
+                    phases[key].append((t1 - t0) * 1e3)
         return wrap
 
     fa._host_layout = timed("layout", orig[0])
@@ -48,9 +53,14 @@ for c in cfgs:
     fa._lib.host_reduce = timed("host_reduce_call", orig[3])
     try:
         for i in range(6):
+            stamps.clear()
             t0 = time.perf_counter()
             fa.FedAvg.aggregate(models, w)
-            phases["aggregate_total"].append((time.perf_counter() - t0) * 1e3)
+            t1 = time.perf_counter()
+            phases["aggregate_total"].append((t1 - t0) * 1e3)
+            if "host_reduce_call_enter" in stamps:  # first native call in, last native call out
+                phases["pre_native"].append((stamps["host_reduce_call_enter"] - t0) * 1e3)
+                phases["post_native"].append((t1 - stamps["host_reduce_call_exit"]) * 1e3)
     finally:
         fa._host_layout, fa._fresh_params, fa._clone_value, fa._lib.host_reduce = orig
     row = {k: round(statistics.median(v[1:]), 3) for k, v in phases.items() if v}

@@ -60,7 +60,7 @@ def test_library_version_and_argument_errors(lib_path):
     from accdfl_amd import _lib
 
     L = _lib.lib()
-    assert L.so.dla_version() == 8
+    assert L.so.dla_version() == 9
     assert L.build_id == _lib.source_build_id() == _lib.file_build_id(lib_path)
     assert L.max_peers_per_pass == 128
     # kernel selection by shape (host-only query): north star, configs[3] share, configs[4] share,
@@ -198,6 +198,15 @@ def test_host_reduce_argument_errors(lib_path):
         call(begin=5, end=4)
     with pytest.raises(_lib.DlaggError, match="page-locked"):
         call()
+    # the deferred form: outputs are checked only once published, and a flag is required
+    L = _lib.lib()
+    rc = L.so.dla_host_reduce_deferred(0, 2, 1, (ctypes.c_void_p * 2)(*ptrs), (ctypes.c_int64 * 1)(10),
+                                       (ctypes.c_double * 2)(0.5, 0.5), (ctypes.c_void_p * 1)(0), None, 0, 10, 64,
+                                       buf, buf, buf, buf, 0, 0)
+    assert rc != 0 and b"outs_ready" in L.so.dla_last_error()
+    with pytest.raises(_lib.DlaggError, match="page-locked"):  # not "null output": outs unpublished yet
+        _lib.host_reduce(0, 2, ptrs, [10], [0.5, 0.5], (ctypes.c_void_p * 1)(0), 0, 10, 64, buf, buf, buf, buf, 0,
+                         0, outs_ready=ctypes.c_int(0))
 
 
 class _OddModule(nn.Module):

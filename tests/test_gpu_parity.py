@@ -1,6 +1,7 @@
 """GPU parity: the HIP reduce (through the C ABI) against the reference's golden vectors
 and the CPU oracle, bit for bit (NaN compared as NaN).  Run on the MI355X: -m gpu."""
 import os
+import time
 
 import numpy as np
 import pytest
@@ -598,6 +599,101 @@ def test_native_host_reduce_chunks(dtype, pinned, chunk_bytes):
         want = fedavg_bits([gc.as_float(_bits(m[i].detach().reshape(-1), dtype), dtype) for m in models], w, dtype)
         assert same_bits(gc.as_float(_bits(p.detach().reshape(-1), dtype), dtype), want, dtype), i
     assert torch.equal(out.running_mean, models[0].running_mean)
+
+
+@pytest.mark.parametrize("delay_s", [0.0, 0.02])
+def test_host_reduce_deferred_outputs(delay_s):
+    """dla_host_reduce_deferred (ABI v9): the call starts with no outputs; they are published from
+    another thread (at once, or 20 ms into the call, after several chunks were packed, copied in and
+    reduced) and the round is bit-exact; a call whose outputs are abandoned (-1) drains and fails,
+    and the staging serves the next round."""
+    import ctypes
+    import threading
+
+    from accdfl_amd import _lib
+    from accdfl_amd.core.gradient_aggregation import fedavg as fa
+
+    dev = torch.device("cuda", 0)
+    n, numels = 6, [1_000_003, 17, 2_500_000]
+    g = torch.Generator().manual_seed(5)
+    peers = [[(torch.randn(m, generator=g) * 0.05) for m in numels] for _ in range(n)]
+    w = [float(x) for x in np.random.default_rng(5).dirichlet(np.ones(n))]
+    tensors = (ctypes.c_void_p * (n * len(numels)))(*[t.data_ptr() for pl in peers for t in pl])
+    total = sum(numels)
+    chunk = 1 << 16  # 256 KiB rows: dozens of chunks
+    fa.release_staging()
+    try:
+        st = fa._get_native_staging(dev, torch.float32, -1, n, chunk)
+        comp = torch.cuda.current_stream(dev)
+
+        def run(outs, ready, errs):
+            try:
+                _lib.host_reduce(0, n, tensors, numels, w, outs, 0, total, chunk, st.h_stage.data_ptr(),
+                                 st.d_stage.data_ptr(), st.h_out.data_ptr(), st.d_out.data_ptr(), comp.cuda_stream,
+                                 st.copy_stream.cuda_stream, outs_ready=ready)
+            except Exception as e:  # noqa: BLE001
+                errs.append(e)
+
+        # abandoned: the call drains and reports it
+        outs = (ctypes.c_void_p * len(numels))()
+        ready, errs = ctypes.c_int(0), []
+        th = threading.Thread(target=run, args=(outs, ready, errs))
+        th.start()
+        time.sleep(delay_s)
+        ready.value = -1
+        th.join(60)
+        assert not th.is_alive() and len(errs) == 1 and "abandoned" in str(errs[0])
+        # published late: bit-exact
+        outs = (ctypes.c_void_p * len(numels))()
+        ready, errs = ctypes.c_int(0), []
+        th = threading.Thread(target=run, args=(outs, ready, errs))
+        th.start()
+        time.sleep(delay_s)
+        res = [torch.empty(m) for m in numels]
+        for i, r in enumerate(res):
+            outs[i] = r.data_ptr()
+        ready.value = 1
+        th.join(60)
+        assert not th.is_alive() and not errs, errs
+        for i, r in enumerate(res):
+            want = fedavg_bits([pl[i].numpy() for pl in peers], w, "f32")
+            assert same_bits(r.numpy(), want, "f32"), i
+    finally:
+        fa.release_staging()
+
+
+def test_large_round_abandons_to_the_general_path():
+    """_large_round starts the native call before it has the result's tensors; when models[0] turns
+    out to have a parameter it cannot allocate (an nn.Parameter subclass keeps the stock deepcopy),
+    it abandons the call and the general path averages the round — still bit-exact."""
+    from torch import nn
+
+    from accdfl_amd.core.gradient_aggregation import fedavg as fa
+
+    class MyParam(nn.Parameter):
+        pass
+
+    g = torch.Generator().manual_seed(9)
+    models = []
+    for k in range(3):
+        m = nn.Module()
+        m.a = nn.Parameter(torch.randn(2_000_000, generator=g) * 0.05)
+        m.b = MyParam(torch.randn(1000, generator=g) * 0.05)
+        models.append(m)
+    w = [0.2, 0.3, 0.5]
+    old = fa._SMALL_ROUND_BYTES
+    fa._SMALL_ROUND_BYTES = 0
+    try:
+        out = fa.FedAvg.aggregate(models, w)
+        out2 = fa.FedAvg.aggregate(models, w)  # the staging is usable after an abandoned call
+    finally:
+        fa._SMALL_ROUND_BYTES = old
+        fa.release_staging()
+    for o in (out, out2):
+        for name in ("a", "b"):
+            want = fedavg_bits([getattr(m, name).detach().numpy() for m in models], w, "f32")
+            assert same_bits(getattr(o, name).detach().numpy(), want, "f32"), name
+        assert type(o.b) is MyParam
 
 
 def test_native_staging_grows_with_the_footprint():
