@@ -60,6 +60,8 @@ EXPORTED = (
     "dla_host_round_finish",
     "dla_host_reduce",
     "dla_host_reduce_deferred",
+    "dla_host_reduce_launch",
+    "dla_host_reduce_join",
     "dla_wsum_multi_table_bytes",
     "dla_wsum_multi_table",
 )
@@ -293,6 +295,14 @@ class _Lib:
                                                 ctypes.POINTER(vp), ctypes.POINTER(ctypes.c_int), ctypes.c_int64,
                                                 ctypes.c_int64, ctypes.c_int64, vp, vp, vp, vp, vp, vp]
         so.dla_host_reduce_deferred.restype = ctypes.c_int
+        so.dla_host_reduce_launch.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                              ctypes.POINTER(vp), ctypes.POINTER(ctypes.c_int64),
+                                              ctypes.POINTER(ctypes.c_double), ctypes.POINTER(vp),
+                                              ctypes.POINTER(ctypes.c_int), ctypes.c_int64, ctypes.c_int64,
+                                              ctypes.c_int64, vp, vp, vp, vp, vp, vp, ctypes.POINTER(vp)]
+        so.dla_host_reduce_launch.restype = ctypes.c_int
+        so.dla_host_reduce_join.argtypes = [vp]
+        so.dla_host_reduce_join.restype = ctypes.c_int
         so.dla_wsum_multi_table_bytes.argtypes = [ctypes.c_int, ctypes.c_int]
         so.dla_wsum_multi_table_bytes.restype = ctypes.c_int64
         so.dla_wsum_multi_table.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(vp), ctypes.POINTER(vp),
@@ -482,6 +492,50 @@ def host_reduce(dtype_code: int, n_peers: int, tensor_ptrs, numels, weights: Seq
                                            chunk_elems, h_stage, d_stage, h_out, d_out, stream_ptr, copy_stream_ptr)
     if rc != 0:
         L.check(rc, "dla_host_reduce")
+
+
+class HostReduceJob:
+    """A dla_host_reduce_launch job: holds every array the library reads until join()."""
+
+    def __init__(self, handle: int, keep: tuple):
+        self._handle = handle
+        self._keep = keep
+
+    def join(self) -> None:
+        """dla_host_reduce_join (the wait releases the interpreter lock); raises DlaggError on failure.
+        A job is joined once; later calls do nothing."""
+        h, self._handle = self._handle, None
+        if h is None:
+            return
+        L = lib()
+        rc = L.so.dla_host_reduce_join(h)
+        self._keep = None
+        L.check(rc, "dla_host_reduce")
+
+    def __del__(self):  # a job never joined would leak its thread: join it (errors dropped)
+        if getattr(self, "_handle", None) is not None:
+            try:
+                lib().so.dla_host_reduce_join(self._handle)
+            except Exception:  # noqa: BLE001  (interpreter shutdown)
+                pass
+
+
+def host_reduce_launch(device: int, dtype_code: int, n_peers: int, tensor_ptrs, numels, weights: Sequence[float],
+                       out_ptrs, outs_ready, begin: int, end: int, chunk_elems: int, h_stage: int, d_stage: int,
+                       h_out: int, d_out: int, stream_ptr: int, copy_stream_ptr: int) -> HostReduceJob:
+    """dla_host_reduce_launch: dla_host_reduce_deferred on a library thread; returns at once.
+    ``out_ptrs`` (a ctypes array) is filled by the caller, then ``outs_ready.value`` set to 1 (or -1)."""
+    L = lib()
+    if not isinstance(numels, ctypes.Array):
+        numels = (ctypes.c_int64 * len(numels))(*numels)
+    if not isinstance(tensor_ptrs, ctypes.Array):
+        tensor_ptrs = (ctypes.c_void_p * len(tensor_ptrs))(*tensor_ptrs)
+    h = ctypes.c_void_p()
+    rc = L.so.dla_host_reduce_launch(device, dtype_code, n_peers, len(numels), tensor_ptrs, numels,
+                                     _dbl_array(weights), out_ptrs, ctypes.byref(outs_ready), begin, end, chunk_elems,
+                                     h_stage, d_stage, h_out, d_out, stream_ptr, copy_stream_ptr, ctypes.byref(h))
+    L.check(rc, "dla_host_reduce_launch")
+    return HostReduceJob(h.value, (tensor_ptrs, numels, out_ptrs, outs_ready))
 
 
 def host_round_finish(dtype_code: int, numels, result_ptr: int, out_ptrs: Sequence[int], stream_ptr: int) -> None:

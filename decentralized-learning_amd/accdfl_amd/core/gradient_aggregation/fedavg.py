@@ -441,9 +441,9 @@ def _small_round(models: List[nn.Module], weights, layout) -> "nn.Module | None"
 
 
 def _large_round(models: List[nn.Module], weights, layout) -> "nn.Module | None":
-    """A large round of same-layout CPU models through dla_host_reduce from the pointer table of
-    _host_layout: every GPU of the host path (set_host_devices) streams its parameter bucket in
-    packed chunks (one DMA per chunk), one host thread per GPU; the averaged elements land in the
+    """A large round of same-layout CPU models through dla_host_reduce_launch from the pointer table
+    of _host_layout: every GPU of the host path (_devices_for) streams its parameter bucket in packed
+    chunks (one DMA per chunk) on a library thread of its own; the averaged elements land in the
     result's parameters.  None when the result's parameters are not dense CPU tensors."""
 
     from accdfl_amd.core.sharding import bucket_bounds
@@ -456,36 +456,31 @@ def _large_round(models: List[nn.Module], weights, layout) -> "nn.Module | None"
     device = _wsum.require_device(None)
     devices = _devices_for(device, total * esize)
     devices = devices[:max(1, min(len(devices), (total * esize) // _MIN_SHARD_BYTES))]
-    # The native call starts streaming the round through the GPU at once, on another thread; this one
-    # allocates the result's parameters meanwhile, publishes them (out_arr, then ready = 1: only the
-    # native call's first unpack waits for them, dla_host_reduce_deferred), then clones the module
-    # tree around them (deepcopy of models[0], fedavg.py:20) while the call runs on.
+    # Every GPU bucket starts streaming through its GPU at once, on a thread of the library's own
+    # (dla_host_reduce_launch: no interpreter lock needed while it runs); this thread allocates the
+    # result's parameters meanwhile, publishes them (out_arr, then ready = 1: only the native first
+    # unpack waits for them), then clones the module tree around them (deepcopy of models[0],
+    # fedavg.py:20) while the round streams on, and joins.
     code = _wsum.dtype_code(dtype)
     tensor_arr = ptrs  # a ctypes array (_host_layout)
     numel_arr = (ctypes.c_int64 * len(numels))(*numels)
     out_arr = (ctypes.c_void_p * len(numels))()
     ready = ctypes.c_int(0)
     with _staging_lock:
-        jobs = []
-        for i, (dev, (s, e)) in enumerate(zip(devices, bucket_bounds(total, len(devices), align))):
-            if s < e:
-                chunk = _native_chunk(n, esize, e - s, align)
-                jobs.append((_get_native_staging(dev, dtype, i if len(devices) > 1 else -1, n, chunk), dev, s, e,
-                             chunk))
-
-        def bucket(job):
-            st, dev, s, e, chunk = job
-            compute = torch.cuda.current_stream(dev)
-            st.copy_stream.wait_stream(compute)  # earlier users of the device staging are done
-            with torch.cuda.device(dev):
-                _lib.host_reduce(code, n, tensor_arr, numel_arr, weights, out_arr, s, e, chunk,
-                                 st.h_stage.data_ptr(), st.d_stage.data_ptr(), st.h_out.data_ptr(),
-                                 st.d_out.data_ptr(), compute.cuda_stream, st.copy_stream.cuda_stream,
-                                 outs_ready=ready)
-
-        futures = [_round_executor().submit(bucket, job) for job in jobs]
+        launched = []
         center = None
         try:
+            for i, (dev, (s, e)) in enumerate(zip(devices, bucket_bounds(total, len(devices), align))):
+                if s >= e:
+                    continue
+                chunk = _native_chunk(n, esize, e - s, align)
+                st = _get_native_staging(dev, dtype, i if len(devices) > 1 else -1, n, chunk)
+                compute = torch.cuda.current_stream(dev)
+                st.copy_stream.wait_stream(compute)  # earlier users of the device staging are done
+                launched.append(_lib.host_reduce_launch(
+                    dev.index, code, n, tensor_arr, numel_arr, weights, out_arr, ready, s, e, chunk,
+                    st.h_stage.data_ptr(), st.d_stage.data_ptr(), st.h_out.data_ptr(), st.d_out.data_ptr(),
+                    compute.cuda_stream, st.copy_stream.cuda_stream))
             memo = _fresh_params(models[0])
             params = [memo.get(id(p)) for p in models[0].parameters()] if len(memo) == len(numels) else []
             if len(params) == len(numels) and all(c is not None and c.is_cpu and c.is_contiguous() for c in params):
@@ -496,29 +491,17 @@ def _large_round(models: List[nn.Module], weights, layout) -> "nn.Module | None"
         finally:
             if ready.value == 0:
                 ready.value = -1  # no result tensors: the native calls drain and give up
-            for f in futures:
-                f.exception()  # waits; every bucket has finished with the staging before the lock goes
+            errors = []
+            for job in launched:  # every bucket has finished with the staging before the lock goes
+                try:
+                    job.join()
+                except _lib.DlaggError as err:
+                    errors.append(err)
         if ready.value < 0:
             return None  # the general path handles this round (the abandoned calls' errors are expected)
-        for f in futures:
-            f.result()  # re-raises the first failure
+        if errors:
+            raise errors[0]
     return center
-
-
-_round_pool = None
-_round_pool_pid = None
-
-
-def _round_executor():
-    """Persistent worker threads for the native host-round calls (one per GPU bucket), so a round
-    pays no thread start-up; rebuilt in a forked child, which has none of the parent's threads."""
-    global _round_pool, _round_pool_pid
-    if _round_pool is None or _round_pool_pid != os.getpid():
-        from concurrent.futures import ThreadPoolExecutor
-
-        _round_pool = ThreadPoolExecutor(max_workers=8, thread_name_prefix="accdfl-host-round")
-        _round_pool_pid = os.getpid()
-    return _round_pool
 
 
 def _stage_rows(st, dev, k: int, flat: List[torch.Tensor], numels: List[int], s: int, e: int):

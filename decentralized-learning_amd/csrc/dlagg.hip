@@ -2035,11 +2035,19 @@ inline void copy_bytes(void* d, const void* s, int64_t n, bool nt) {
 
 // dsts[i] <- srcs[i], bytes[i] each (validated by the caller); threaded from 4 MiB.  nt: streaming
 // stores (packs into page-locked staging read by the GPU next), fenced before the call returns.
-void copy_batch(void* const* dsts, const void* const* srcs, const int64_t* bytes, int n, bool nt = false) {
+// min_threads: at least this many threads from 256 KiB per thread on (a copy on the critical path:
+// the last chunk's unpack, which nothing else overlaps).
+void copy_batch(void* const* dsts, const void* const* srcs, const int64_t* bytes, int n, bool nt = false,
+                int min_threads = 1) {
   nt = nt && stream_copies();
   int64_t total = 0;
   for (int i = 0; i < n; ++i) total += bytes[i];
-  const int threads = copy_threads(total);
+  int threads = copy_threads(total);
+  if (min_threads > threads) {
+    const int64_t by_quarter_mib = total >> 18;
+    threads = static_cast<int>(by_quarter_mib < min_threads ? (by_quarter_mib < threads ? threads : by_quarter_mib)
+                                                            : min_threads);
+  }
   if (threads <= 1) {
     for (int i = 0; i < n; ++i)
       if (bytes[i] > 0) copy_bytes(dsts[i], srcs[i], bytes[i], nt);
@@ -2488,7 +2496,7 @@ int host_reduce_impl(int dtype, int n_peers, int n_tensors, const void* const* t
     return true;
   };
   // chunk c's averaged elements (h_out buffer c & 1) -> the result tensors (fedavg.py:25)
-  auto unpack = [&](int64_t c) {
+  auto unpack = [&](int64_t c, int min_threads) {
     const int buf = static_cast<int>(c & 1);
     if (!await_outs()) return;
     if (!check(hipEventSynchronize(d2h[buf]), "D2H")) return;
@@ -2499,7 +2507,7 @@ int host_reduce_impl(int dtype, int n_peers, int n_tensors, const void* const* t
       srcs.push_back(static_cast<const char*>(h_out) + buf * row_bytes + (a - c0) * es);
       bytes.push_back((b - a) * es);
     });
-    copy_batch(dsts.data(), srcs.data(), bytes.data(), static_cast<int>(dsts.size()));
+    copy_batch(dsts.data(), srcs.data(), bytes.data(), static_cast<int>(dsts.size()), false, min_threads);
   };
   // DLA_HOST_REDUCE_STATS=1: per-call phase times on stderr (host-path tuning)
   static const bool stats = std::getenv("DLA_HOST_REDUCE_STATS") != nullptr;
@@ -2560,12 +2568,12 @@ int host_reduce_impl(int dtype, int n_peers, int n_tensors, const void* const* t
     if (!check(hipMemcpyAsync(hout, dout, m * es, hipMemcpyDeviceToHost, cs_), "D2H")) break;
     if (!check(hipEventRecord(d2h[buf], cs_), "record")) break;
     const auto t3 = clk::now();
-    if (c >= 1) unpack(c - 1);  // overlaps chunk c's H2D
+    if (c >= 1) unpack(c - 1, 1);  // overlaps chunk c's H2D
     const auto t4 = clk::now();
     t_wait += secs(t0, t1), t_pack += secs(t1, t2), t_issue += secs(t2, t3), t_unpack += secs(t3, t4);
   }
   const auto t_loop = clk::now();
-  if (e == hipSuccess) unpack(n_chunks - 1);
+  if (e == hipSuccess) unpack(n_chunks - 1, 4);  // nothing left to overlap: spread it
   if (stats)
     std::fprintf(stderr,
                  "dla_host_reduce: %d peers x %lld elems, %lld chunks of <= %lld: total %.2f ms, first pack %.2f, "
@@ -2598,6 +2606,58 @@ int dla_host_reduce_deferred(int dtype, int n_peers, int n_tensors, const void* 
   if (!outs_ready) return fail(DLA_E_INVALID, "dla_host_reduce_deferred: outs_ready is required");
   return host_reduce_impl(dtype, n_peers, n_tensors, tensors, numels, weights, outs, outs_ready, begin, end,
                           chunk_elems, h_stage, d_stage, h_out, d_out, stream, copy_stream);
+}
+
+struct dla_host_job {
+  std::thread th;
+  int rc = DLA_OK;
+  std::string err;
+  std::vector<double> weights;  // the caller's array may be a temporary
+};
+
+int dla_host_reduce_launch(int device, int dtype, int n_peers, int n_tensors, const void* const* tensors,
+                           const int64_t* numels, const double* weights, void* const* outs, const int* outs_ready,
+                           int64_t begin, int64_t end, int64_t chunk_elems, void* h_stage, void* d_stage, void* h_out,
+                           void* d_out, void* stream, void* copy_stream, dla_host_job_t** job) {
+  g_last_error.clear();
+  if (!job) return fail(DLA_E_INVALID, "dla_host_reduce_launch: job is required");
+  *job = nullptr;
+  if (n_peers < 1 || !weights) return fail(DLA_E_INVALID, "dla_host_reduce_launch: need n_peers >= 1 and weights");
+  int n_dev = 0;
+  const hipError_t de = hipGetDeviceCount(&n_dev);
+  if (de != hipSuccess || device < 0 || device >= n_dev)
+    return fail(DLA_E_INVALID, "dla_host_reduce_launch: no HIP device " + std::to_string(device));
+  dla_host_job* j = new (std::nothrow) dla_host_job;
+  if (!j) return fail(DLA_E_INVALID, "dla_host_reduce_launch: out of memory");
+  j->weights.assign(weights, weights + n_peers);
+  try {
+    j->th = std::thread([=] {
+      const hipError_t se = hipSetDevice(device);
+      if (se != hipSuccess) {
+        j->rc = static_cast<int>(se);
+        j->err = std::string("dla_host_reduce_launch: hipSetDevice: ") + hipGetErrorString(se);
+        return;
+      }
+      j->rc = host_reduce_impl(dtype, n_peers, n_tensors, tensors, numels, j->weights.data(), outs, outs_ready, begin,
+                               end, chunk_elems, h_stage, d_stage, h_out, d_out, stream, copy_stream);
+      if (j->rc != DLA_OK) j->err = g_last_error;  // this worker thread's message
+    });
+  } catch (const std::exception& ex) {
+    delete j;
+    return fail(DLA_E_INVALID, std::string("dla_host_reduce_launch: ") + ex.what());
+  }
+  *job = j;
+  return DLA_OK;
+}
+
+int dla_host_reduce_join(dla_host_job_t* job) {
+  g_last_error.clear();
+  if (!job) return fail(DLA_E_INVALID, "dla_host_reduce_join: null job");
+  if (job->th.joinable()) job->th.join();
+  const int rc = job->rc;
+  if (rc != DLA_OK) g_last_error = job->err;
+  delete job;
+  return rc;
 }
 
 int dla_shard_range(int dtype, int64_t n_elems, int n_shards, int shard, int64_t* start, int64_t* end) {

@@ -279,6 +279,21 @@ int dla_host_reduce_deferred(int dtype, int n_peers, int n_tensors, const void* 
                              int64_t end, int64_t chunk_elems, void* h_stage, void* d_stage, void* h_out, void* d_out,
                              void* stream, void* copy_stream);
 
+/* dla_host_reduce_deferred on a thread of the library's own, with `device` current there: returns at
+ * once with *job set (NULL on a validation failure).  The calling thread keeps no lock while the round
+ * streams — a Python caller allocates and publishes the outputs and clones the result module under
+ * its interpreter lock meanwhile, which a worker thread of its own would need for every step.
+ * tensors, numels, outs, outs_ready, the staging buffers and the streams must stay valid until
+ * dla_host_reduce_join; weights are copied.  Every launched job must be joined exactly once.  ABI v9. */
+typedef struct dla_host_job dla_host_job_t;
+int dla_host_reduce_launch(int device, int dtype, int n_peers, int n_tensors, const void* const* tensors,
+                           const int64_t* numels, const double* weights, void* const* outs, const int* outs_ready,
+                           int64_t begin, int64_t end, int64_t chunk_elems, void* h_stage, void* d_stage, void* h_out,
+                           void* d_out, void* stream, void* copy_stream, dla_host_job_t** job);
+/* Waits for a launched job and frees it; returns its status (its message: dla_last_error on this
+ * thread). */
+int dla_host_reduce_join(dla_host_job_t* job);
+
 #ifdef __cplusplus
 }
 #endif

@@ -58,6 +58,7 @@ def main():
     ap.add_argument("--shapes", default="ns,c4share,c4whole,b16")
     ap.add_argument("--stages", default="2,3,4,6")
     ap.add_argument("--grids", default="0")
+    ap.add_argument("--ns-tiles", default="", help="extra tile sizes (bytes) for the north star, tree build")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
@@ -97,9 +98,30 @@ def main():
                 if rc != 0:
                     raise RuntimeError("dla_wsum_slab_tiled rc=%d" % rc)
             legs[lname] = fn
+        if key == "ns" and args.ns_tiles:
+            for tb in [int(x) for x in args.ns_tiles.split(",")]:
+                t2 = tb // es
+                sl2 = torch.empty(-(-p // t2) * n * t2, dtype=dt, device=dev)
+                # the same peers, re-tiled: peer k's element i at ((i // t2) * n + k) * t2 + i % t2
+                src = slab[: n_t * n * te].view(n_t, n, te).permute(1, 0, 2).reshape(n, -1)[:, :p]
+                full = -(-p // t2) * t2
+                pad = torch.zeros(n, full, dtype=dt, device=dev)
+                pad[:, :p] = src
+                sl2.copy_(pad.view(n, -1, t2).permute(1, 0, 2).reshape(-1))
+                del pad, src
+                o = torch.empty(p, dtype=dt, device=dev)
+                lname = "tree tile %d B" % tb
+                outs[lname] = o
+
+                def fn(sl2=sl2, t2=t2, o=o):
+                    rc = libs["tree"].dla_wsum_slab_tiled(code, sl2.data_ptr(), t2, n, wa, n, p, o.data_ptr(), sp,
+                                                          None)
+                    if rc != 0:
+                        raise RuntimeError("dla_wsum_slab_tiled rc=%d" % rc)
+                legs[lname] = fn
         if key == "ns":
             w8 = (ctypes.c_float * 8)(*[float(torch.tensor(x, dtype=torch.float32)) for x in w])
-            for s in [int(x) for x in args.stages.split(",")]:
+            for s in [int(x) for x in args.stages.split(",") if x]:
                 for gr in [int(x) for x in args.grids.split(",")]:
                     o = torch.zeros(p, dtype=dt, device=dev)
                     lname = "ldsdma S=%d grid=%s" % (s, gr or "auto")

@@ -28,7 +28,7 @@ for c in cfgs:
     phases = {k: [] for k in ("layout", "fresh_params", "clone", "host_reduce_call", "aggregate_total",
                               "pre_native", "post_native")}
     stamps = {}
-    orig = (fa._host_layout, fa._fresh_params, fa._clone_value, fa._lib.host_reduce)
+    orig = (fa._host_layout, fa._fresh_params, fa._clone_value, fa._lib.host_reduce_launch, fa._lib.HostReduceJob.join)
 
     depth = {}
 
@@ -44,13 +44,16 @@ for c in cfgs:
                 if depth[key] == 0:
                     t1 = time.perf_counter()
                     stamps[key + "_exit"] = t1
-                    phases[key].append((t1 - t0) * 1e3)
+                    if key in phases:
+                        phases[key].append((t1 - t0) * 1e3)
         return wrap
 
     fa._host_layout = timed("layout", orig[0])
     fa._fresh_params = timed("fresh_params", orig[1])
     fa._clone_value = timed("clone", orig[2])
-    fa._lib.host_reduce = timed("host_reduce_call", orig[3])
+    # the native round: from the (first) launch to the return of the (last) join
+    fa._lib.host_reduce_launch = timed("launch", orig[3])
+    fa._lib.HostReduceJob.join = timed("join", orig[4])
     try:
         for i in range(6):
             stamps.clear()
@@ -58,11 +61,13 @@ for c in cfgs:
             fa.FedAvg.aggregate(models, w)
             t1 = time.perf_counter()
             phases["aggregate_total"].append((t1 - t0) * 1e3)
-            if "host_reduce_call_enter" in stamps:  # first native call in, last native call out
-                phases["pre_native"].append((stamps["host_reduce_call_enter"] - t0) * 1e3)
-                phases["post_native"].append((t1 - stamps["host_reduce_call_exit"]) * 1e3)
+            if "launch_enter" in stamps:  # first launch in, last join out
+                phases["pre_native"].append((stamps["launch_enter"] - t0) * 1e3)
+                phases["post_native"].append((t1 - stamps["join_exit"]) * 1e3)
+                phases["host_reduce_call"].append((stamps["join_exit"] - stamps["launch_enter"]) * 1e3)
     finally:
-        fa._host_layout, fa._fresh_params, fa._clone_value, fa._lib.host_reduce = orig
+        (fa._host_layout, fa._fresh_params, fa._clone_value, fa._lib.host_reduce_launch,
+         fa._lib.HostReduceJob.join) = orig
     row = {k: round(statistics.median(v[1:]), 3) for k, v in phases.items() if v}
     print(json.dumps(dict(config=c, peers=n, params=p, **row)), flush=True)
     del models

@@ -237,6 +237,39 @@ int main(void) {
         return 1;
       }
     }
+    /* the same round launched on a library thread, its outputs published after the launch (ABI v9) */
+    {
+      void* late_outs[2] = {NULL, NULL};
+      int ready = 0;
+      dla_host_job_t* job = NULL;
+      memset(out_host, 0xff, sizeof(float) * P);
+      CHECK_DLA(dla_host_reduce_launch(0, DLA_F32, N, 2, tensors, numels, w, late_outs, &ready, 0, P, chunk, h_stage,
+                                       d_stage, h_out, d_out2, st, cst, &job));
+      late_outs[0] = out_host;
+      late_outs[1] = out_host + split;
+      __atomic_store_n(&ready, 1, __ATOMIC_RELEASE);
+      CHECK_DLA(dla_host_reduce_join(job));
+      for (int64_t j = 0; j < P; ++j) {
+        volatile float acc = host[0][j] * 0.0f;
+        for (int k = 0; k < N; ++k) {
+          volatile float prod = (float)w[k] * host[k][j];
+          acc = acc + prod;
+        }
+        if (!same_f32(acc, out_host[j])) {
+          fprintf(stderr, "dla_host_reduce_launch mismatch at %lld\n", (long long)j);
+          return 1;
+        }
+      }
+      /* abandoned: the job drains and reports it */
+      ready = 0;
+      CHECK_DLA(dla_host_reduce_launch(0, DLA_F32, N, 2, tensors, numels, w, late_outs, &ready, 0, P, chunk, h_stage,
+                                       d_stage, h_out, d_out2, st, cst, &job));
+      __atomic_store_n(&ready, -1, __ATOMIC_RELEASE);
+      if (dla_host_reduce_join(job) != DLA_E_INVALID || !strstr(dla_last_error(), "abandoned")) {
+        fprintf(stderr, "expected an abandoned job to fail with DLA_E_INVALID\n");
+        return 1;
+      }
+    }
     /* a pageable staging buffer is refused before any copy */
     if (dla_host_reduce(DLA_F32, N, 2, tensors, numels, w, outs_host, 0, P, chunk, out_host, d_stage, h_out, d_out2,
                         st, cst) != DLA_E_INVALID) {
@@ -265,7 +298,7 @@ int main(void) {
   CHECK_HIP(hipFree(dev_out));
   free(out_host);
   printf("c_abi_demo ok: dla_wsum, dla_plan, dla_mean, dla_wsum_sharded, dla_wsum_slab_tiled, dla_host_round, "
-         "dla_host_reduce "
+         "dla_host_reduce (+ launch / join) "
          "bit-exact on %d peers "
          "x %lld fp32\n", N, (long long)P);
   return 0;

@@ -204,6 +204,13 @@ def test_host_reduce_argument_errors(lib_path):
                                        (ctypes.c_double * 2)(0.5, 0.5), (ctypes.c_void_p * 1)(0), None, 0, 10, 64,
                                        buf, buf, buf, buf, 0, 0)
     assert rc != 0 and b"outs_ready" in L.so.dla_last_error()
+    job = ctypes.c_void_p()
+    args = (0, 2, 1, (ctypes.c_void_p * 2)(*ptrs), (ctypes.c_int64 * 1)(10), (ctypes.c_double * 2)(0.5, 0.5),
+            (ctypes.c_void_p * 1)(0), ctypes.byref(ctypes.c_int(0)), 0, 10, 64, buf, buf, buf, buf, 0, 0)
+    assert L.so.dla_host_reduce_launch(0, *args, None) != 0 and b"job is required" in L.so.dla_last_error()
+    assert L.so.dla_host_reduce_launch(4096, *args, ctypes.byref(job)) != 0 and job.value is None
+    assert b"no HIP device 4096" in L.so.dla_last_error()
+    assert L.so.dla_host_reduce_join(None) != 0 and b"null job" in L.so.dla_last_error()
     with pytest.raises(_lib.DlaggError, match="page-locked"):  # not "null output": outs unpublished yet
         _lib.host_reduce(0, 2, ptrs, [10], [0.5, 0.5], (ctypes.c_void_p * 1)(0), 0, 10, 64, buf, buf, buf, buf, 0,
                          0, outs_ready=ctypes.c_int(0))
