@@ -42,6 +42,7 @@
 #include <condition_variable>
 #include <cstring>
 #include <functional>
+#include <map>
 #include <mutex>
 #include <new>
 #include <set>
@@ -2609,11 +2610,78 @@ int dla_host_reduce_deferred(int dtype, int n_peers, int n_tensors, const void* 
 }
 
 struct dla_host_job {
-  std::thread th;
+  std::thread th;  // only when no persistent worker was free (a concurrent launch on the same device)
+  std::mutex mu;
+  std::condition_variable cv;
+  bool done = false;
   int rc = DLA_OK;
   std::string err;
   std::vector<double> weights;  // the caller's array may be a temporary
+  std::function<void()> body;
+  std::chrono::steady_clock::time_point t_launch, t_start, t_end;
 };
+
+namespace {
+// One persistent worker thread per HIP device runs launched host rounds: a new thread per round
+// pays its creation and the HIP runtime's first-call set-up on that thread (hipSetDevice, event
+// creation) on the round's critical path.  A worker holds at most one job; a launch that finds it
+// busy (two rounds at once on one device) gets a thread of its own.  Rebuilt in a forked child,
+// which has none of the parent's threads; never destroyed (the workers sleep until exit).
+class HostWorkers {
+ public:
+  static HostWorkers& get() {
+    static HostWorkers* w = new HostWorkers;  // leaked on purpose
+    return *w;
+  }
+  bool try_post(int device, dla_host_job* j) {
+    std::lock_guard<std::mutex> g(mu_);
+    if (pid_ != getpid()) {  // forked: the parent's workers do not exist here
+      slots_.clear();
+      pid_ = getpid();
+    }
+    Slot*& sl = slots_[device];
+    if (!sl) {
+      sl = new Slot;  // leaked on purpose: no join at exit
+      sl->th = std::thread([sl, device] { loop(sl, device); });
+      sl->th.detach();
+    }
+    std::lock_guard<std::mutex> sg(sl->mu);
+    if (sl->job) return false;
+    sl->job = j;
+    sl->cv.notify_one();
+    return true;
+  }
+
+ private:
+  struct Slot {
+    std::thread th;
+    std::mutex mu;
+    std::condition_variable cv;
+    dla_host_job* job = nullptr;
+  };
+  static void loop(Slot* sl, int device) {
+    (void)hipSetDevice(device);
+    for (;;) {
+      dla_host_job* j;
+      {
+        std::unique_lock<std::mutex> g(sl->mu);
+        sl->cv.wait(g, [sl] { return sl->job != nullptr; });
+        j = sl->job;
+      }
+      // run a copy: the joiner may free the job as soon as the body has signalled completion
+      std::function<void()> body = std::move(j->body);
+      body();
+      {
+        std::lock_guard<std::mutex> g(sl->mu);
+        sl->job = nullptr;
+      }
+    }
+  }
+  std::mutex mu_;
+  pid_t pid_ = getpid();
+  std::map<int, Slot*> slots_;
+};
+}  // namespace
 
 int dla_host_reduce_launch(int device, int dtype, int n_peers, int n_tensors, const void* const* tensors,
                            const int64_t* numels, const double* weights, void* const* outs, const int* outs_ready,
@@ -2630,18 +2698,29 @@ int dla_host_reduce_launch(int device, int dtype, int n_peers, int n_tensors, co
   dla_host_job* j = new (std::nothrow) dla_host_job;
   if (!j) return fail(DLA_E_INVALID, "dla_host_reduce_launch: out of memory");
   j->weights.assign(weights, weights + n_peers);
+  j->t_launch = std::chrono::steady_clock::now();
+  j->body = [=] {
+    j->t_start = std::chrono::steady_clock::now();
+    int rc;
+    std::string err;
+    const hipError_t se = hipSetDevice(device);
+    if (se != hipSuccess) {
+      rc = static_cast<int>(se);
+      err = std::string("dla_host_reduce_launch: hipSetDevice: ") + hipGetErrorString(se);
+    } else {
+      rc = host_reduce_impl(dtype, n_peers, n_tensors, tensors, numels, j->weights.data(), outs, outs_ready, begin,
+                            end, chunk_elems, h_stage, d_stage, h_out, d_out, stream, copy_stream);
+      if (rc != DLA_OK) err = g_last_error;  // this worker thread's message
+    }
+    std::lock_guard<std::mutex> g(j->mu);
+    j->rc = rc;
+    j->err = err;
+    j->t_end = std::chrono::steady_clock::now();
+    j->done = true;
+    j->cv.notify_all();
+  };
   try {
-    j->th = std::thread([=] {
-      const hipError_t se = hipSetDevice(device);
-      if (se != hipSuccess) {
-        j->rc = static_cast<int>(se);
-        j->err = std::string("dla_host_reduce_launch: hipSetDevice: ") + hipGetErrorString(se);
-        return;
-      }
-      j->rc = host_reduce_impl(dtype, n_peers, n_tensors, tensors, numels, j->weights.data(), outs, outs_ready, begin,
-                               end, chunk_elems, h_stage, d_stage, h_out, d_out, stream, copy_stream);
-      if (j->rc != DLA_OK) j->err = g_last_error;  // this worker thread's message
-    });
+    if (!HostWorkers::get().try_post(device, j)) j->th = std::thread(j->body);
   } catch (const std::exception& ex) {
     delete j;
     return fail(DLA_E_INVALID, std::string("dla_host_reduce_launch: ") + ex.what());
@@ -2653,7 +2732,20 @@ int dla_host_reduce_launch(int device, int dtype, int n_peers, int n_tensors, co
 int dla_host_reduce_join(dla_host_job_t* job) {
   g_last_error.clear();
   if (!job) return fail(DLA_E_INVALID, "dla_host_reduce_join: null job");
+  {
+    std::unique_lock<std::mutex> g(job->mu);
+    job->cv.wait(g, [job] { return job->done; });
+  }
   if (job->th.joinable()) job->th.join();
+  static const bool stats = std::getenv("DLA_HOST_REDUCE_STATS") != nullptr;
+  if (stats) {
+    const auto now = std::chrono::steady_clock::now();
+    auto ms = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
+      return std::chrono::duration<double, std::milli>(b - a).count();
+    };
+    std::fprintf(stderr, "dla_host_reduce_join: launch->start %.3f ms, run %.3f ms, end->join %.3f ms\n",
+                 ms(job->t_launch, job->t_start), ms(job->t_start, job->t_end), ms(job->t_end, now));
+  }
   const int rc = job->rc;
   if (rc != DLA_OK) g_last_error = job->err;
   delete job;
