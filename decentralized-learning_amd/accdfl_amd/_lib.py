@@ -51,6 +51,7 @@ EXPORTED = (
     "dla_plan_destroy",
     "dla_mean",
     "dla_host_copy_batch",
+    "dla_host_copy_batch_ex",
     "dla_wsum_sharded",
     "dla_shard_range",
     "dla_shutdown",
@@ -264,6 +265,9 @@ class _Lib:
         so.dla_host_copy_batch.argtypes = [ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(ctypes.c_int64),
                                            ctypes.c_int]
         so.dla_host_copy_batch.restype = ctypes.c_int
+        so.dla_host_copy_batch_ex.argtypes = [ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(ctypes.c_int64),
+                                              ctypes.c_int, ctypes.c_int]
+        so.dla_host_copy_batch_ex.restype = ctypes.c_int
         so.dla_wsum_sharded.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(vp),
                                          ctypes.POINTER(ctypes.c_double), ctypes.c_int, ctypes.c_int64,
                                          ctypes.POINTER(vp), ctypes.c_int, ctypes.POINTER(vp)]
@@ -441,12 +445,17 @@ def wsum_multi_table_ptrs(dtype_code: int, peer_ptrs, out_ptrs, numels, weights:
         L.check(rc, "dla_wsum_multi_table")
 
 
-def host_copy_batch(dst_ptrs: Sequence[int], src_ptrs: Sequence[int], nbytes: Sequence[int]) -> None:
-    """dla_host_copy_batch: dst_ptrs[i] <- src_ptrs[i] (host memory), nbytes[i] bytes each."""
+DLA_COPY_STREAMING = 1
+
+
+def host_copy_batch(dst_ptrs: Sequence[int], src_ptrs: Sequence[int], nbytes: Sequence[int],
+                    streaming: bool = False) -> None:
+    """dla_host_copy_batch(_ex): dst_ptrs[i] <- src_ptrs[i] (host memory), nbytes[i] bytes each;
+    ``streaming``: non-temporal stores (destinations only the GPU reads next)."""
     L = lib()
     m = len(nbytes)
-    rc = L.so.dla_host_copy_batch((ctypes.c_void_p * m)(*dst_ptrs), (ctypes.c_void_p * m)(*src_ptrs),
-                                  (ctypes.c_int64 * m)(*nbytes), m)
+    rc = L.so.dla_host_copy_batch_ex((ctypes.c_void_p * m)(*dst_ptrs), (ctypes.c_void_p * m)(*src_ptrs),
+                                     (ctypes.c_int64 * m)(*nbytes), m, DLA_COPY_STREAMING if streaming else 0)
     if rc != 0:
         L.check(rc, "dla_host_copy_batch")
 

@@ -123,6 +123,11 @@ def _block_address(block) -> int:
     return np.frombuffer(block, dtype=np.uint8).__array_interface__["data"][0]
 
 
+# Gathers into a page-locked ingress buffer (read next by the H2D DMA, not by the CPU) use streaming
+# stores (dla_host_copy_batch_ex, DLA_COPY_STREAMING); ACCDFL_AMD_INGRESS_NT=0 turns them off (A/B).
+_INGRESS_NT = os.environ.get("ACCDFL_AMD_INGRESS_NT", "1") != "0"
+
+
 def _gather(addrs, lens, dst: torch.Tensor) -> None:
     """Copy the pieces back to back into the host uint8 tensor ``dst`` (one native batched
     memcpy, threaded from 4 MiB: libdlagg's dla_host_copy_batch)."""
@@ -131,7 +136,7 @@ def _gather(addrs, lens, dst: torch.Tensor) -> None:
     if not lens:
         return
     dsts = list(itertools.accumulate(lens[:-1], initial=dst.data_ptr()))
-    _lib.host_copy_batch(dsts, addrs, lens)
+    _lib.host_copy_batch(dsts, addrs, lens, streaming=_INGRESS_NT and sum(lens) >= (4 << 20) and dst.is_pinned())
 
 
 def _parse_storage_blob(blob, alloc=None) -> torch.TypedStorage:

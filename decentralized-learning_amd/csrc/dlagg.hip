@@ -2293,14 +2293,19 @@ int dla_mean(int dtype, const void* const* peers, int n_peers, int64_t n_elems, 
 }
 
 int dla_host_copy_batch(void* const* dsts, const void* const* srcs, const int64_t* bytes, int n) {
+  return dla_host_copy_batch_ex(dsts, srcs, bytes, n, 0);
+}
+
+int dla_host_copy_batch_ex(void* const* dsts, const void* const* srcs, const int64_t* bytes, int n, int flags) {
   g_last_error.clear();
+  if (flags & ~DLA_COPY_STREAMING) return fail(DLA_E_INVALID, "dla_host_copy_batch: unknown flags");
   if (n < 0 || (n > 0 && (!dsts || !srcs || !bytes))) return fail(DLA_E_INVALID, "dla_host_copy_batch: bad table");
   for (int i = 0; i < n; ++i) {
     if (bytes[i] < 0) return fail(DLA_E_INVALID, "dla_host_copy_batch: negative size at " + std::to_string(i));
     if (bytes[i] > 0 && (!dsts[i] || !srcs[i]))
       return fail(DLA_E_INVALID, "dla_host_copy_batch: null pointer at " + std::to_string(i));
   }
-  copy_batch(dsts, srcs, bytes, n);
+  copy_batch(dsts, srcs, bytes, n, (flags & DLA_COPY_STREAMING) != 0);
   return DLA_OK;
 }
 

@@ -222,6 +222,12 @@ void dla_plan_destroy(dla_plan_t* plan);
  * tensors).  One native call instead of a torch op per tensor: the GL merge of two
  * GNLeNet models (configs[1]) packs 28 tensors per round.  Regions must not overlap. */
 int dla_host_copy_batch(void* const* dsts, const void* const* srcs, const int64_t* bytes, int n);
+/* dla_host_copy_batch with flags.  DLA_COPY_STREAMING: streaming (non-temporal) stores, for
+ * destinations only the GPU reads next — an EVA block list gathered into a page-locked ingress
+ * buffer before its H2D (accdfl/util/eva/transfer/incoming.py:35's join): no read-for-ownership of
+ * the destination lines and no dirty lines the DMA's reads must snoop.  ABI v9. */
+#define DLA_COPY_STREAMING 1
+int dla_host_copy_batch_ex(void* const* dsts, const void* const* srcs, const int64_t* bytes, int n, int flags);
 
 /* A round of CPU-resident models in two calls — fedavg.py:20-25 for the reference's own call
  * sites, whose models live in host memory (the GL merge of N=2 models every round,
