@@ -2644,11 +2644,18 @@ class HostWorkers {
       slots_.clear();
       pid_ = getpid();
     }
-    Slot*& sl = slots_[device];
+    Slot* sl = slots_[device];
     if (!sl) {
-      sl = new Slot;  // leaked on purpose: no join at exit
-      sl->th = std::thread([sl, device] { loop(sl, device); });
-      sl->th.detach();
+      Slot* fresh = new Slot;  // leaked on purpose: no join at exit
+      try {
+        fresh->th = std::thread([fresh, device] { loop(fresh, device); });
+      } catch (...) {
+        delete fresh;  // no worker: this launch gets a thread of its own (or fails there)
+        slots_.erase(device);
+        return false;
+      }
+      fresh->th.detach();
+      sl = slots_[device] = fresh;
     }
     std::lock_guard<std::mutex> sg(sl->mu);
     if (sl->job) return false;
