@@ -12,6 +12,7 @@ summation order = arrival order.
 """
 from __future__ import annotations
 
+import collections
 import copy
 from typing import Dict, List, Optional
 
@@ -231,5 +232,44 @@ class DeviceModelManager(ModelManager):
 
     def aggregate_serialized(self, weights: List[float] = None) -> bytes:
         """``serialize_model(aggregate_trained_models(weights))`` — the bytes a DFL
-        aggregator sends back to the participants (accdfl/dfl/community.py:556-567)."""
-        return wire.serialize_model(self.aggregate_trained_models(weights))
+        aggregator sends back to the participants (accdfl/dfl/community.py:556-567).
+
+        When the round's rows are staged (the slab is the registry), the averaged row is not
+        copied into a result module first: the payload's parameter bytes come from HBM straight
+        into the returned ``bytes`` (wire.DeviceSource), beside the buffers of the module
+        ``aggregate_trained_models`` would have returned (models[0]'s, fedavg.py:20).  The
+        encoded objects are the same."""
+        if self.get_aggregation_method() is not FedAvg or not self._uniform():
+            return wire.serialize_model(self.aggregate_trained_models(weights))
+        entries = list(self.incoming_trained_models.values())
+        n = len(entries)
+        if not weights:
+            weights = [float(1. / n) for _ in range(n)]
+        else:
+            assert len(weights) == n
+        first = entries[0]
+        # the module aggregate_trained_models returns: the template's structure with the first
+        # arrival's buffers (wire peers), or deepcopy(models[0]) (module peers)
+        structure = self.template if isinstance(first, WirePeer) else first
+        names = [name for name, _ in structure.named_parameters()]
+        state = structure.state_dict()
+        bufs = first.state_dict if isinstance(first, WirePeer) else state
+        if len(names) != len(self.slab.numels) or any(
+                k not in state or state[k].shape != s for k, s in zip(names, self.slab.shapes)):
+            return wire.serialize_model(self.aggregate_trained_models(weights))
+        with torch.no_grad():
+            flat = self.slab._reduce_planned(weights)
+            offsets = dict(zip(names, self.slab._offsets()))
+            sd = collections.OrderedDict()
+            for k, v in state.items():
+                if k in offsets:
+                    sd[k] = wire.DeviceSource(flat, offsets[k], v.shape)
+                elif k in bufs and bufs[k].shape == v.shape:
+                    # the round's models[0] buffers (deepcopy, fedavg.py:20), in the structure's dtype
+                    sd[k] = bufs[k].detach().to(v.dtype)
+                else:
+                    sd[k] = v.detach()
+            meta = getattr(state, "_metadata", None)
+            if meta is not None:
+                sd._metadata = meta
+            return wire.dumps_state_dict(sd)

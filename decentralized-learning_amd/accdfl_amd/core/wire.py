@@ -542,6 +542,31 @@ def _owns_storage(t: torch.Tensor) -> bool:
             and not t.requires_grad)
 
 
+class DeviceSource:
+    """A state-dict entry whose values live in HBM: ``numel`` elements of ``flat`` (a contiguous device
+    tensor of the entry's dtype) from element ``offset`` on, with the entry's ``shape``.  dumps_state_dict
+    encodes it like the CPU tensor it stands for and copies its bytes from the device straight into
+    the returned payload (egress without the result module: accdfl/dfl/community.py:556-567)."""
+
+    def __init__(self, flat: torch.Tensor, offset: int, shape):
+        self.flat, self.offset, self.shape = flat, offset, tuple(shape)
+        self.numel = 1
+        for d in self.shape:
+            self.numel *= d
+        self.dtype = flat.dtype
+        # what _TensorRef / _legacy_blob_header read: sizes, contiguous strides, dtype, numel
+        self.meta = torch.empty(self.shape, dtype=flat.dtype, device="meta")
+
+    def data_ptr(self) -> int:
+        return self.flat.data_ptr() + self.offset * self.flat.element_size()
+
+    def nbytes(self) -> int:
+        return self.numel * self.flat.element_size()
+
+    def to_cpu(self) -> torch.Tensor:
+        return self.flat[self.offset:self.offset + self.numel].view(self.shape).cpu()
+
+
 def dumps_state_dict(state_dict: Dict[str, torch.Tensor]) -> bytes:
     """The reference's wire format for a state dict (accdfl/core/models/__init__.py:9-10: a
     pickle of the OrderedDict whose tensors reduce to ``_rebuild_tensor_v2`` over
@@ -558,7 +583,14 @@ def dumps_state_dict(state_dict: Dict[str, torch.Tensor]) -> bytes:
     big = []
     skeleton = collections.OrderedDict()
     for k, v in state_dict.items():
-        if torch.is_tensor(v) and v.numel() * v.element_size() >= _SENTINEL_BYTES and _owns_storage(v):
+        if isinstance(v, DeviceSource):
+            if v.nbytes() >= _SENTINEL_BYTES and _BYTES_ADDR_OK:
+                token = os.urandom(_SENTINEL_BYTES)
+                skeleton[k] = _TensorRef(v.meta, token)
+                big.append((token, v))
+            else:
+                skeleton[k] = v.to_cpu()  # small: through the CPU like any tensor
+        elif torch.is_tensor(v) and v.numel() * v.element_size() >= _SENTINEL_BYTES and _owns_storage(v):
             token = os.urandom(_SENTINEL_BYTES)
             skeleton[k] = _TensorRef(v, token)
             big.append((token, v))
@@ -570,40 +602,103 @@ def dumps_state_dict(state_dict: Dict[str, torch.Tensor]) -> bytes:
     skel = pickle.dumps(skeleton)
     if not big:
         return skel
-    # (host address, length, keep-alive) of every piece of the output, in order
+    # (address, length, keep-alive) of every piece of the output, in order; a DeviceSource's piece
+    # is a device address, copied by _join_pieces from HBM
     pieces, pos = [], 0
     skel_addr = id(skel) + _BYTES_DATA
     for i, (token, t) in enumerate(big):
         at = skel.find(token, pos)
         if at < 5 or skel[at - 5] != 0x42 or int.from_bytes(skel[at - 4:at], "little") != _SENTINEL_BYTES:
-            return pickle.dumps(state_dict)  # unexpected pickler output: the stock path
+            return pickle.dumps(_cpu_state_dict(state_dict))  # unexpected pickler output: the stock path
         pieces.append((skel_addr + pos, at - 5 - pos, skel))
-        head = _legacy_blob_header(t, str(i))
-        n = len(head) + t.numel() * t.element_size()
+        dev = isinstance(t, DeviceSource)
+        head = _legacy_blob_header(t.meta if dev else t, str(i))
+        nbytes = t.nbytes() if dev else t.numel() * t.element_size()
+        n = len(head) + nbytes
         head = (b"B" + n.to_bytes(4, "little") if n < 1 << 32 else b"\x8e" + n.to_bytes(8, "little")) + head
         pieces.append((id(head) + _BYTES_DATA, len(head), head))
-        pieces.append((t.data_ptr(), t.numel() * t.element_size(), t))
+        pieces.append((t.data_ptr(), nbytes, t))
         pos = at + _SENTINEL_BYTES
     pieces.append((skel_addr + pos, len(skel) - pos, skel))
     return _join_pieces(pieces)
+
+
+def _cpu_state_dict(state_dict):
+    out = collections.OrderedDict((k, v.to_cpu() if isinstance(v, DeviceSource) else v) for k, v in state_dict.items())
+    meta = getattr(state_dict, "_metadata", None)
+    if meta is not None:
+        out._metadata = meta
+    return out
 
 
 def _join_pieces(pieces) -> bytes:
     """One ``bytes`` holding the pieces back to back.  The object is created uninitialised
     (PyBytes_FromStringAndSize(NULL, n), as CPython's own builders do) and filled by libdlagg's
     threaded batched memcpy before any other code can see it, so a 100 MB model's page faults
-    and copy are spread over threads instead of b''.join's one."""
+    and copy are spread over threads instead of b''.join's one.  Pieces that are DeviceSources
+    come from HBM through _copy_from_device."""
     import ctypes
 
     total = sum(ln for _, ln, _ in pieces)
-    if not _BYTES_ADDR_OK or total < (8 << 20):
+    has_dev = any(isinstance(k, DeviceSource) for _, _, k in pieces)
+    if not has_dev and (not _BYTES_ADDR_OK or total < (8 << 20)):
         return b"".join(ctypes.string_at(a, ln) if ln else b"" for a, ln, _ in pieces)
     from accdfl_amd import _lib
 
     out = _new_bytes(None, total)
     dsts = list(itertools.accumulate([ln for _, ln, _ in pieces[:-1]], initial=id(out) + _BYTES_DATA))
-    _lib.host_copy_batch(dsts, [a for a, _, _ in pieces], [ln for _, ln, _ in pieces])
+    host = [(d, a, ln) for d, (a, ln, k) in zip(dsts, pieces) if ln and not isinstance(k, DeviceSource)]
+    if host:
+        _lib.host_copy_batch([d for d, _, _ in host], [a for _, a, _ in host], [ln for _, _, ln in host])
+    for d, (a, ln, k) in zip(dsts, pieces):
+        if ln and isinstance(k, DeviceSource):
+            _copy_from_device(d, k, ln)
     return out
+
+
+# Bounce chunk of _copy_from_device (its copy-out runs on up to 8 threads from 16 MiB: a chunk of
+# 8 MiB gets only 4) and the store kind of the copy-out (A/B knobs).
+_EGRESS_CHUNK = int(float(os.environ.get("ACCDFL_AMD_EGRESS_CHUNK_MB", "32")) * (1 << 20))
+_EGRESS_NT = os.environ.get("ACCDFL_AMD_EGRESS_NT", "0") == "1"
+_egress_bounce = {}
+
+
+def _copy_from_device(dst: int, src: "DeviceSource", nbytes: int) -> None:
+    """``nbytes`` from HBM at ``src`` into host memory at ``dst`` (a fresh payload: pageable, not
+    yet faulted in): chunked D2H into two page-locked bounce buffers on a side stream, each chunk
+    copied out by the threaded batched memcpy (which spreads the destination's page faults over
+    threads) while the next chunk's D2H runs.  A D2H straight into the fresh pageable payload would
+    fault it in on one thread (11-13 ms per 100 MB on the MI355X hosts, core/host_memory.py)."""
+    from accdfl_amd import _lib
+
+    dev = src.flat.device
+    st = _egress_bounce.get(dev)
+    if st is None:
+        st = _egress_bounce[dev] = ([torch.empty(_EGRESS_CHUNK, dtype=torch.uint8, pin_memory=True) for _ in range(2)],
+                                    torch.cuda.Stream(dev), [None, None])
+    bufs, stream, evs = st
+    stream.wait_stream(torch.cuda.current_stream(dev))  # the reduce that produced src is done
+    flat_u8 = src.flat.view(torch.uint8)
+    base = src.offset * src.flat.element_size()
+    n_chunks = -(-nbytes // _EGRESS_CHUNK)
+
+    def issue(c):
+        a = c * _EGRESS_CHUNK
+        ln = min(_EGRESS_CHUNK, nbytes - a)
+        with torch.cuda.stream(stream):
+            bufs[c & 1][:ln].copy_(flat_u8[base + a:base + a + ln], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(stream)
+        evs[c & 1] = ev
+
+    issue(0)
+    for c in range(n_chunks):
+        if c + 1 < n_chunks:
+            issue(c + 1)
+        evs[c & 1].synchronize()
+        a = c * _EGRESS_CHUNK
+        ln = min(_EGRESS_CHUNK, nbytes - a)
+        _lib.host_copy_batch([dst + a], [bufs[c & 1].data_ptr()], [ln], streaming=_EGRESS_NT)
 
 
 def _bytes_builder():

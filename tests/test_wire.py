@@ -101,6 +101,52 @@ def test_device_model_manager_wire_round():
         assert same_bits(back[name].numpy(), want[name].numpy(), "f32"), name
 
 
+class _ConvBN(nn.Module):
+    def __init__(self, seed, dtype):
+        super().__init__()
+        torch.manual_seed(seed)
+        self.conv = nn.Conv2d(64, 128, 3).to(dtype)             # 73 728 weights: a device-sourced entry
+        self.bn = nn.BatchNorm2d(128).to(dtype)                  # small params + buffers
+        self.fc = nn.Linear(512, 300).to(dtype)                 # 153 600 weights
+        with torch.no_grad():
+            self.bn.running_mean.fill_(float(seed))
+            self.bn.num_batches_tracked.fill_(seed)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("peers_as", ["wire", "modules"])
+def test_aggregate_serialized_straight_from_hbm(dtype, peers_as):
+    """VERDICT r02 missing 4: aggregate_serialized copies the averaged parameters from HBM straight
+    into the payload (wire.DeviceSource), without the result module; the payload decodes — with the
+    reference's own pickle.loads too — to exactly serialize_model(aggregate_trained_models()): the
+    same keys in order, every parameter bit for bit, the first arrival's buffers."""
+    from types import SimpleNamespace
+
+    from accdfl_amd.core import wire
+    from accdfl_amd.core.gradient_aggregation import GradientAggregationMethod
+    from accdfl_amd.core.model_manager import DeviceModelManager
+
+    models = [_ConvBN(k + 1, dtype) for k in range(5)]
+    w = [float(x) for x in np.random.default_rng(7).dirichlet(np.ones(5))]
+    mm = DeviceModelManager(None, SimpleNamespace(gradient_aggregation=GradientAggregationMethod.FEDAVG),
+                            template=_ConvBN(0, dtype), capacity=5)
+    for k, m in enumerate(models):
+        if peers_as == "wire":
+            mm.process_incoming_serialized(b"p%d" % k, wire.payload_blocks(wire.serialize_model(m), 60_000))
+        else:
+            mm.process_incoming_trained_model(b"p%d" % k, m)
+    assert mm._uniform()
+    direct = mm.aggregate_serialized(w)
+    want = wire.loads_state_dict(wire.serialize_model(mm.aggregate_trained_models(w)))
+    for got in (wire.loads_state_dict(direct), pickle.loads(direct)):
+        assert list(got.keys()) == list(want.keys())
+        for k in want:
+            assert got[k].dtype == want[k].dtype and got[k].shape == want[k].shape, k
+            assert torch.equal(got[k].view(-1).view(torch.uint8), want[k].view(-1).view(torch.uint8)), k
+    assert torch.equal(wire.loads_state_dict(direct)["bn.running_mean"], models[0].bn.running_mean)
+
+
 @pytest.mark.gpu
 def test_ingress_slot_is_never_reused_within_a_round():
     """a registry entry removed mid-round must not hand its page-locked ingress buffer
