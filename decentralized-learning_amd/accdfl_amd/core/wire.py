@@ -24,6 +24,7 @@ import itertools
 import io
 import os
 import pickle
+import threading
 from typing import Callable, Dict, List, Optional, Sequence
 
 import numpy as np
@@ -661,6 +662,7 @@ def _join_pieces(pieces) -> bytes:
 _EGRESS_CHUNK = int(float(os.environ.get("ACCDFL_AMD_EGRESS_CHUNK_MB", "32")) * (1 << 20))
 _EGRESS_NT = os.environ.get("ACCDFL_AMD_EGRESS_NT", "0") == "1"
 _egress_bounce = {}
+_egress_lock = threading.Lock()
 
 
 def _copy_from_device(dst: int, src: "DeviceSource", nbytes: int) -> None:
@@ -669,14 +671,22 @@ def _copy_from_device(dst: int, src: "DeviceSource", nbytes: int) -> None:
     copied out by the threaded batched memcpy (which spreads the destination's page faults over
     threads) while the next chunk's D2H runs.  A D2H straight into the fresh pageable payload would
     fault it in on one thread (11-13 ms per 100 MB on the MI355X hosts, core/host_memory.py)."""
+    dev = src.flat.device
+    with _egress_lock:
+        st = _egress_bounce.get(dev)
+        if st is None:
+            st = _egress_bounce[dev] = (
+                [torch.empty(_EGRESS_CHUNK, dtype=torch.uint8, pin_memory=True) for _ in range(2)],
+                torch.cuda.Stream(dev), [None, None], threading.Lock())
+    bufs, stream, evs, lock = st
+    with lock:  # one copy-out at a time per device: the bounce buffers are shared
+        _copy_chunks(dst, src, nbytes, bufs, stream, evs)
+
+
+def _copy_chunks(dst, src, nbytes, bufs, stream, evs):
     from accdfl_amd import _lib
 
     dev = src.flat.device
-    st = _egress_bounce.get(dev)
-    if st is None:
-        st = _egress_bounce[dev] = ([torch.empty(_EGRESS_CHUNK, dtype=torch.uint8, pin_memory=True) for _ in range(2)],
-                                    torch.cuda.Stream(dev), [None, None])
-    bufs, stream, evs = st
     stream.wait_stream(torch.cuda.current_stream(dev))  # the reduce that produced src is done
     flat_u8 = src.flat.view(torch.uint8)
     base = src.offset * src.flat.element_size()
