@@ -2451,7 +2451,16 @@ int host_reduce_impl(int dtype, int n_peers, int n_tensors, const void* const* t
   // time; then full chunks.  cs[c] .. cs[c + 1] are chunk c's flat elements.
   const int64_t align = 256 / es;
   std::vector<int64_t> cs{begin};
-  for (int64_t part = 4; cs.back() < end; part = part > 1 ? part / 2 : 1) {
+  // DLA_HOST_RAMP=k: the first chunk is 1/k of chunk_elems (a power of two; default 4; A/B knob)
+  static const int64_t ramp = [] {
+    const char* v = std::getenv("DLA_HOST_RAMP");
+    int64_t r = v ? std::atoll(v) : 4;
+    if (r < 1) r = 1;
+    int64_t p = 1;
+    while (p < r && p < 64) p *= 2;
+    return p;
+  }();
+  for (int64_t part = ramp; cs.back() < end; part = part > 1 ? part / 2 : 1) {
     int64_t len = chunk_elems / part / align * align;
     if (len < align) len = align;
     cs.push_back(cs.back() + len < end ? cs.back() + len : end);
