@@ -558,7 +558,7 @@ def cpu_baseline(n, p, budget_s):
         "by_threads": {str(th): {"GB/s": round(byts / v[0] / 1e9, 3), "median_ms": round(v[0] * 1e3, 1),
                                  "reduces": v[1]} for th, v in per.items()},
         "value_1thread": round(byts / per[1][0] / 1e9, 3),
-        "regime": ("LLC-assisted: the held product temporary and the running sum (2 x %d MB) stay in the "
+        "regime": ("LLC-assisted: the held product temporary and the running sum (2 x %d MiB) stay in the "
                    "CPU's last-level cache across peers, so only the peer reads come from DRAM; not a DRAM "
                    "rate. cold_fresh_process is the literal sequence, page faults included" % (p * 4 >> 20)),
         "cold_fresh_process": cold,
