@@ -1320,6 +1320,61 @@ hipError_t launch_vec(const PeerTable<typename Ops<DT>::w_t, KMAX>& tab, int n, 
   }
 }
 
+// DLA_VEC_LDS_PAD=bytes (A/B knob, default 0): dynamic LDS reserved per workgroup of the tiled vector
+// kernel, which caps its workgroups per CU at 160 KiB / (bytes + its static LDS) — an occupancy
+// experiment (fewer waves, fewer DRAM pages open at once), nothing reads it.
+unsigned vec_lds_pad() {
+  static const unsigned pad = [] {
+    const char* v = std::getenv("DLA_VEC_LDS_PAD");
+    const long b = v ? std::atol(v) : 0;
+    return static_cast<unsigned>(b < 0 ? 0 : b > 65536 ? 65536 : b);
+  }();
+  return pad;
+}
+
+// Workgroups per CU the tiled vector kernel is capped at (0: uncapped), through dynamic LDS that only
+// W workgroups fit.  Uncapped, the one-wave workgroups fill a CU to the register limit (32 for the
+// 8-peer f32 instance); every wave holds n x 512 B of loads in flight, and past ~56-90 KiB per CU
+// more waves only keep more DRAM rows open at once.  Measured interleaved against the uncapped
+// kernel on HBM-sized launches (profiles/r03x, profiles/r03y, us): 8 x 25 M f32 (the north star)
+// 129.7 -> 125.8-126.3 at W = 14-15 (W 13: 131.0, W 12: 134.9, W 16: 127.6); 8 x 50 M bf16 130.0 ->
+// 125.1; 12 x 25 M f32 188.1 -> 183.7 at W 15; 16 x 25 M f32 245.4 -> 238.6 at W 9-10; 16 x 21.3 M
+// bf16 105.3 -> 101.8 at W 10; 4 x 25 M f32 73.6 -> 70.0 at W 26-28.  2 and 6 peers, 32 and more
+// peers (register-limited already) and launches that fit the Infinity Cache lose with any cap, so
+// they run uncapped.  DLA_VEC_WGS_PER_CU=W overrides the policy (A/B sweeps).
+int vec_wgs_cap(int dt, int n_peers, int64_t n_vecs) {
+  static const int env = [] {
+    const char* v = std::getenv("DLA_VEC_WGS_PER_CU");
+    return v ? std::atoi(v) : -1;
+  }();
+  if (env >= 0) return env;
+  (void)dt;  // f32 and bf16 measured alike
+  const int64_t in_bytes = static_cast<int64_t>(n_peers) * n_vecs * 8;
+  if (in_bytes < (int64_t{256} << 20)) return 0;
+  switch (n_peers) {
+    case 4: return 26;
+    case 8: return 14;
+    case 12: return 15;
+    case 16: return 10;
+    default: return 0;
+  }
+}
+
+// Dynamic LDS per workgroup that caps a kernel whose own LDS is static_lds bytes at `wgs`
+// workgroups per CU (allocations in 512-byte blocks); DLA_VEC_LDS_PAD's raw bytes when uncapped.
+unsigned lds_pad_for(size_t static_lds, int wgs) {
+  if (wgs <= 0) return vec_lds_pad();
+  static const int64_t lds_cu = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&v, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, dev) != hipSuccess || v <= 0)
+      v = 160 << 10;
+    return static_cast<int64_t>(v);
+  }();
+  const int64_t per = lds_cu / wgs / 512 * 512;
+  return per > static_cast<int64_t>(static_lds) ? static_cast<unsigned>(per - static_lds) : 0;
+}
+
 // The tile-interleaved slab (dla_wsum_slab_tiled) through the vector-per-lane kernel: variant 12 =
 // dwordx2 x 16 peers in flight, 21 = dwordx2 x 32 with plain stores, otherwise
 // (default, 9) dwordx2 x 32.
@@ -1341,9 +1396,17 @@ hipError_t launch_vec_tiled(const PeerTable<typename Ops<DT>::w_t, KMAX>& tab, i
     int64_t grid = (n_vecs + 63) / 64;                                                                        \
     if (n_elems > n_vecs * per_vec) ++grid;                                                                   \
     if (grid < 1 || grid > 0x7fffffff) return hipErrorInvalidValue;                                           \
+    static const size_t st_lds = [] {                                                                          \
+      hipFuncAttributes a{};                                                                                   \
+      return hipFuncGetAttributes(&a, reinterpret_cast<const void*>(                                          \
+                                          &wsum_vec_kernel<DT, KMAX, G, VW_, ACC_IN, true, PST_>)) == hipSuccess \
+                 ? a.sharedSizeBytes                                                                           \
+                 : size_t{1024};                                                                               \
+    }();                                                                                                       \
+    const unsigned lds_pad = lds_pad_for(st_lds, vec_wgs_cap(DT, n, n_vecs));                                  \
     hipLaunchKernelGGL((wsum_vec_kernel<DT, KMAX, G, VW_, ACC_IN, true, PST_>), dim3(static_cast<unsigned>(grid)),   \
-                       dim3(64), 0, s, tab, n, n_vecs, n_elems, out, tshift_e - vs, tstride_e / per_vec, tshift_e, \
-                       tstride_e);                                                                            \
+                       dim3(64), lds_pad, s, tab, n, n_vecs, n_elems, out, tshift_e - vs, tstride_e / per_vec,    \
+                       tshift_e, tstride_e);                                                                  \
   } while (0)
     switch (variant) {
       case 12: DLA_VECT(16, 2, false); break;

@@ -75,6 +75,14 @@ def main():
         "c4share": ("configs[4] share 128 x 2 662 045 bf16", 128, 2_662_045, torch.bfloat16, 4096),
         "c4whole": ("configs[4] whole 128 x 21 296 355 bf16", 128, 21_296_355, torch.bfloat16, 4096),
         "b16": ("16 x 21 296 355 bf16", 16, 21_296_355, torch.bfloat16, 16384),
+        "c2": ("configs[2] 32 x 1 690 046 f32", 32, 1_690_046, torch.float32, 4096),
+        "c3p": ("configs[3'] whole 64 x 4 932 344 f32", 64, 4_932_344, torch.float32, 4096),
+        "ns4": ("4 x 25 M f32", 4, 25_000_000, torch.float32, 16384),
+        "ns16": ("16 x 25 M f32", 16, 25_000_000, torch.float32, 16384),
+        "b8": ("8 x 50 M bf16", 8, 50_000_000, torch.bfloat16, 16384),
+        "ns2": ("2 x 25 M f32", 2, 25_000_000, torch.float32, 16384),
+        "ns12": ("12 x 25 M f32", 12, 25_000_000, torch.float32, 16384),
+        "ns6": ("6 x 25 M f32", 6, 25_000_000, torch.float32, 16384),
     }
     g = torch.Generator(device="cpu").manual_seed(3)
     for key in args.shapes.split(","):
