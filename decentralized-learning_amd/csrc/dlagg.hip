@@ -1375,9 +1375,9 @@ unsigned lds_pad_for(size_t static_lds, int wgs) {
   return per > static_cast<int64_t>(static_lds) ? static_cast<unsigned>(per - static_lds) : 0;
 }
 
-// The tile-interleaved slab (dla_wsum_slab_tiled) through the vector-per-lane kernel: variant 12 =
-// dwordx2 x 16 peers in flight, 21 = dwordx2 x 32 with plain stores, otherwise
-// (default, 9) dwordx2 x 32.
+// The tile-interleaved slab (dla_wsum_slab_tiled) through the vector-per-lane kernel: variant 8 =
+// dwordx2 x 8 peers in flight (28: with plain stores), 12 = dwordx2 x 16, 21 = dwordx2 x 32 with plain
+// stores, otherwise (default, 9) dwordx2 x 32.
 template <int DT, int KMAX, bool ACC_IN>
 hipError_t launch_vec_tiled(const PeerTable<typename Ops<DT>::w_t, KMAX>& tab, int n, int64_t n_elems, void* out,
                             hipStream_t s, int variant, int tshift_e, int64_t tstride_e) {
@@ -1409,8 +1409,10 @@ hipError_t launch_vec_tiled(const PeerTable<typename Ops<DT>::w_t, KMAX>& tab, i
                        tshift_e, tstride_e);                                                                  \
   } while (0)
     switch (variant) {
+      case 8: DLA_VECT(8, 2, false); break;
       case 12: DLA_VECT(16, 2, false); break;
       case 21: DLA_VECT(32, 2, true); break;
+      case 28: DLA_VECT(8, 2, true); break;
       default: DLA_VECT(32, 2, false); break;
     }
 #undef DLA_VECT
@@ -2888,8 +2890,8 @@ int dla_wsum_slab_tiled(int dtype, const void* base, int64_t tile_elems, int64_t
       cfg && cfg->variant
           ? cfg->variant
           : vec_store_policy(vec_variant(n_peers < kMaxPeersPerPass ? n_peers : kMaxPeersPerPass), n_elems * es);
-  if (variant != 9 && variant != 12 && variant != 21)
-    return fail(DLA_E_CONFIG, "dla_wsum_slab_tiled: variant must be 0 (auto), 9, 12 or 21");
+  if (variant != 8 && variant != 9 && variant != 12 && variant != 21 && variant != 28)
+    return fail(DLA_E_CONFIG, "dla_wsum_slab_tiled: variant must be 0 (auto), 8, 9, 12, 21 or 28");
   const int64_t stride = slab_rows * tile_elems;
   hipStream_t s = static_cast<hipStream_t>(stream);
   hipError_t e;

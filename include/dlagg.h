@@ -120,7 +120,8 @@ int dla_wsum_slab(int dtype, const void* base, int64_t pitch_elems, const double
  * of HBM instead of n_peers distant ones.  Peers 0..n_peers-1 (n_peers <= slab_rows) are
  * reduced in row order into the contiguous `out` (n_elems elements).  tile_elems: a power of
  * two of >= 16 bytes; base and out 16-byte aligned; F32, BF16 or F16.  cfg (may be NULL):
- * variant 0 (by shape, as dla_wsum), 9, 12 or 21 picks the vector-per-lane kernel form.
+ * variant 0 (by shape, as dla_wsum), 8, 9, 12, 21 or 28 picks the vector-per-lane kernel form
+ * (8 / 28: 8 peers in flight per lane, sc1 / plain stores; 12: 16; 9 / 21: 32, sc1 / plain).
  * ABI v5. */
 int dla_wsum_slab_tiled(int dtype, const void* base, int64_t tile_elems, int64_t slab_rows, const double* weights,
                         int n_peers, int64_t n_elems, void* out, void* stream, const dla_launch_cfg_t* cfg);

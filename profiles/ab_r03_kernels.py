@@ -59,6 +59,7 @@ def main():
     ap.add_argument("--stages", default="2,3,4,6")
     ap.add_argument("--grids", default="0")
     ap.add_argument("--ns-tiles", default="", help="extra tile sizes (bytes) for the north star, tree build")
+    ap.add_argument("--variants", default="", help="extra tree legs with these launch variants (e.g. 8,12,28)")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
@@ -83,6 +84,10 @@ def main():
         "ns2": ("2 x 25 M f32", 2, 25_000_000, torch.float32, 16384),
         "ns12": ("12 x 25 M f32", 12, 25_000_000, torch.float32, 16384),
         "ns6": ("6 x 25 M f32", 6, 25_000_000, torch.float32, 16384),
+        "c3b": ("configs[3'] bucket 64 x 1 233 086 f32", 64, 1_233_086, torch.float32, 4096),
+        "ns_2": ("north star share at N=2: 8 x 12.5 M f32", 8, 12_500_000, torch.float32, 16384),
+        "ns_4": ("north star share at N=4: 8 x 6.25 M f32", 8, 6_250_000, torch.float32, 16384),
+        "ns_8": ("north star share at N=8: 8 x 3.125 M f32", 8, 3_125_000, torch.float32, 16384),
     }
     g = torch.Generator(device="cpu").manual_seed(3)
     for key in args.shapes.split(","):
@@ -103,6 +108,18 @@ def main():
 
             def fn(so=so, o=o):
                 rc = so.dla_wsum_slab_tiled(code, slab.data_ptr(), te, n, wa, n, p, o.data_ptr(), sp, None)
+                if rc != 0:
+                    raise RuntimeError("dla_wsum_slab_tiled rc=%d" % rc)
+            legs[lname] = fn
+        for v in [int(x) for x in args.variants.split(",") if x]:
+            cfg = _lib.LaunchCfg(v, 0, 0, 0)
+            o = torch.empty(p, dtype=dt, device=dev)
+            lname = "tree v%d" % v
+            outs[lname] = o
+
+            def fn(cfg=cfg, o=o):
+                rc = libs["tree"].dla_wsum_slab_tiled(code, slab.data_ptr(), te, n, wa, n, p, o.data_ptr(), sp,
+                                                      ctypes.byref(cfg))
                 if rc != 0:
                     raise RuntimeError("dla_wsum_slab_tiled rc=%d" % rc)
             legs[lname] = fn
