@@ -1292,34 +1292,6 @@ hipError_t launch_wide(const PeerTable<typename Ops<DT>::w_t, KMAX>& tab, int n,
   return hipGetLastError();
 }
 
-// Variants 9-12: the vector-per-lane kernel (VW dwords per lane, G peers in flight per lane).
-template <int DT, int KMAX, bool ACC_IN>
-hipError_t launch_vec(const PeerTable<typename Ops<DT>::w_t, KMAX>& tab, int n, int64_t n_elems, void* out,
-                      hipStream_t s, int variant) {
-  if constexpr (DT == DLA_F64) {
-    return hipErrorInvalidValue;
-  } else {
-    constexpr int WE = Ops<DT>::WE;
-#define DLA_VEC(G_, VW_, PST_)                                                                                   \
-  do {                                                                                                     \
-    constexpr int G = KMAX < (G_) ? KMAX : (G_);                                                           \
-    const int64_t n_vecs = n_elems / ((VW_) * WE);                                                         \
-    int64_t grid = (n_vecs + 63) / 64;                                                                     \
-    if (n_elems > n_vecs * (VW_) * WE) ++grid;                                                             \
-    if (grid < 1 || grid > 0x7fffffff) return hipErrorInvalidValue;                                        \
-    hipLaunchKernelGGL((wsum_vec_kernel<DT, KMAX, G, VW_, ACC_IN, false, PST_>), dim3(static_cast<unsigned>(grid)), dim3(64), \
-                       0, s, tab, n, n_vecs, n_elems, out);                                                \
-  } while (0)
-    switch (variant) {
-      case 9: DLA_VEC(32, 2, false); break;
-      case 21: DLA_VEC(32, 2, true); break;
-      default: DLA_VEC(16, 2, false); break;  // 12
-    }
-#undef DLA_VEC
-    return hipGetLastError();
-  }
-}
-
 // DLA_VEC_LDS_PAD=bytes (A/B knob, default 0): dynamic LDS reserved per workgroup of the tiled vector
 // kernel, which caps its workgroups per CU at 160 KiB / (bytes + its static LDS) — an occupancy
 // experiment (fewer waves, fewer DRAM pages open at once), nothing reads it.
@@ -1339,9 +1311,10 @@ unsigned vec_lds_pad() {
 // kernel on HBM-sized launches (profiles/r03x, profiles/r03y, us): 8 x 25 M f32 (the north star)
 // 129.7 -> 125.8-126.3 at W = 14-15 (W 13: 131.0, W 12: 134.9, W 16: 127.6); 8 x 50 M bf16 130.0 ->
 // 125.1; 12 x 25 M f32 188.1 -> 183.7 at W 15; 16 x 25 M f32 245.4 -> 238.6 at W 9-10; 16 x 21.3 M
-// bf16 105.3 -> 101.8 at W 10; 4 x 25 M f32 73.6 -> 70.0 at W 26-28.  2 and 6 peers, 32 and more
-// peers (register-limited already) and launches that fit the Infinity Cache lose with any cap, so
-// they run uncapped.  DLA_VEC_WGS_PER_CU=W overrides the policy (A/B sweeps).
+// bf16 105.3 -> 101.8 at W 10; 4 x 25 M f32 73.6 -> 70.0 at W 26-28; 9-15 peers x 25 M f32 3.1-4.5 %
+// faster at W 18-24 (profiles/r03ac).  2, 3, 5, 6 and 7 peers, 32 and more peers (register-limited
+// already) and launches that fit the Infinity Cache lose with any cap, so they run uncapped.
+// DLA_VEC_WGS_PER_CU=W overrides the policy (A/B sweeps).
 int vec_wgs_cap(int dt, int n_peers, int64_t n_vecs) {
   static const int env = [] {
     const char* v = std::getenv("DLA_VEC_WGS_PER_CU");
@@ -1354,7 +1327,13 @@ int vec_wgs_cap(int dt, int n_peers, int64_t n_vecs) {
   switch (n_peers) {
     case 4: return 26;
     case 8: return 14;
+    case 9: return 24;
+    case 10: return 20;
+    case 11: return 24;
     case 12: return 15;
+    case 13: return 24;
+    case 14: return 20;
+    case 15: return 24;
     case 16: return 10;
     default: return 0;
   }
@@ -1373,6 +1352,53 @@ unsigned lds_pad_for(size_t static_lds, int wgs) {
   }();
   const int64_t per = lds_cu / wgs / 512 * 512;
   return per > static_cast<int64_t>(static_lds) ? static_cast<unsigned>(per - static_lds) : 0;
+}
+
+// The same cap for the kernels over separate peer buffers (row-major wsum_vec_kernel, the many-tensor
+// wsum_multi_vec_kernel); DLA_VEC_CAP_ROWS=0 runs them uncapped (A/B).
+int vec_wgs_cap_rows(int dt, int n_peers, int64_t n_vecs) {
+  static const bool off = [] {
+    const char* v = std::getenv("DLA_VEC_CAP_ROWS");
+    return v && std::atoi(v) == 0;
+  }();
+  return off ? 0 : vec_wgs_cap(dt, n_peers, n_vecs);
+}
+
+template <class K>
+size_t static_lds_of(K kernel) {
+  hipFuncAttributes a{};
+  return hipFuncGetAttributes(&a, reinterpret_cast<const void*>(kernel)) == hipSuccess ? a.sharedSizeBytes
+                                                                                       : size_t{1024};
+}
+
+// Variants 9-12: the vector-per-lane kernel (VW dwords per lane, G peers in flight per lane).
+template <int DT, int KMAX, bool ACC_IN>
+hipError_t launch_vec(const PeerTable<typename Ops<DT>::w_t, KMAX>& tab, int n, int64_t n_elems, void* out,
+                      hipStream_t s, int variant) {
+  if constexpr (DT == DLA_F64) {
+    return hipErrorInvalidValue;
+  } else {
+    constexpr int WE = Ops<DT>::WE;
+#define DLA_VEC(G_, VW_, PST_)                                                                                   \
+  do {                                                                                                     \
+    constexpr int G = KMAX < (G_) ? KMAX : (G_);                                                           \
+    const int64_t n_vecs = n_elems / ((VW_) * WE);                                                         \
+    int64_t grid = (n_vecs + 63) / 64;                                                                     \
+    if (n_elems > n_vecs * (VW_) * WE) ++grid;                                                             \
+    if (grid < 1 || grid > 0x7fffffff) return hipErrorInvalidValue;                                        \
+    static const size_t st_lds = static_lds_of(&wsum_vec_kernel<DT, KMAX, G, VW_, ACC_IN, false, PST_>);    \
+    const unsigned lds_pad = lds_pad_for(st_lds, vec_wgs_cap_rows(DT, n, n_vecs));                         \
+    hipLaunchKernelGGL((wsum_vec_kernel<DT, KMAX, G, VW_, ACC_IN, false, PST_>), dim3(static_cast<unsigned>(grid)), dim3(64), \
+                       lds_pad, s, tab, n, n_vecs, n_elems, out);                                          \
+  } while (0)
+    switch (variant) {
+      case 9: DLA_VEC(32, 2, false); break;
+      case 21: DLA_VEC(32, 2, true); break;
+      default: DLA_VEC(16, 2, false); break;  // 12
+    }
+#undef DLA_VEC
+    return hipGetLastError();
+  }
 }
 
 // The tile-interleaved slab (dla_wsum_slab_tiled) through the vector-per-lane kernel: variant 8 =
@@ -1396,13 +1422,7 @@ hipError_t launch_vec_tiled(const PeerTable<typename Ops<DT>::w_t, KMAX>& tab, i
     int64_t grid = (n_vecs + 63) / 64;                                                                        \
     if (n_elems > n_vecs * per_vec) ++grid;                                                                   \
     if (grid < 1 || grid > 0x7fffffff) return hipErrorInvalidValue;                                           \
-    static const size_t st_lds = [] {                                                                          \
-      hipFuncAttributes a{};                                                                                   \
-      return hipFuncGetAttributes(&a, reinterpret_cast<const void*>(                                          \
-                                          &wsum_vec_kernel<DT, KMAX, G, VW_, ACC_IN, true, PST_>)) == hipSuccess \
-                 ? a.sharedSizeBytes                                                                           \
-                 : size_t{1024};                                                                               \
-    }();                                                                                                       \
+    static const size_t st_lds = static_lds_of(&wsum_vec_kernel<DT, KMAX, G, VW_, ACC_IN, true, PST_>);     \
     const unsigned lds_pad = lds_pad_for(st_lds, vec_wgs_cap(DT, n, n_vecs));                                  \
     hipLaunchKernelGGL((wsum_vec_kernel<DT, KMAX, G, VW_, ACC_IN, true, PST_>), dim3(static_cast<unsigned>(grid)),   \
                        dim3(64), lds_pad, s, tab, n, n_vecs, n_elems, out, tshift_e - vs, tstride_e / per_vec,    \
@@ -1643,10 +1663,16 @@ hipError_t launch_multi_vec(const MultiIndex* idx, const MultiSeg* segs, int n_s
   std::memset(&wt, 0, sizeof(wt));
   for (int k = 0; k < pm; ++k) wt.w[k] = static_cast<W>(weights[k0 + k]);  // RNE double -> op-math
   const dim3 g(static_cast<unsigned>(grid)), bl(64);
-  if (plain)
-    hipLaunchKernelGGL((wsum_multi_vec_kernel<DT, KMAX, G, ACC_IN, true>), g, bl, 0, s, idx, segs, n_seg, k0, pm, wt);
-  else
-    hipLaunchKernelGGL((wsum_multi_vec_kernel<DT, KMAX, G, ACC_IN, false>), g, bl, 0, s, idx, segs, n_seg, k0, pm, wt);
+  const int wgs = vec_wgs_cap_rows(DT, pm, grid * 64);  // every workgroup folds 64 vectors
+  if (plain) {
+    static const size_t st_lds = static_lds_of(&wsum_multi_vec_kernel<DT, KMAX, G, ACC_IN, true>);
+    hipLaunchKernelGGL((wsum_multi_vec_kernel<DT, KMAX, G, ACC_IN, true>), g, bl, lds_pad_for(st_lds, wgs), s, idx,
+                       segs, n_seg, k0, pm, wt);
+  } else {
+    static const size_t st_lds = static_lds_of(&wsum_multi_vec_kernel<DT, KMAX, G, ACC_IN, false>);
+    hipLaunchKernelGGL((wsum_multi_vec_kernel<DT, KMAX, G, ACC_IN, false>), g, bl, lds_pad_for(st_lds, wgs), s, idx,
+                       segs, n_seg, k0, pm, wt);
+  }
   return hipGetLastError();
 }
 

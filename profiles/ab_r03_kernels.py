@@ -91,6 +91,8 @@ def main():
     }
     g = torch.Generator(device="cpu").manual_seed(3)
     for key in args.shapes.split(","):
+        if key.startswith("n") and key[1:].isdigit():  # nK: K peers x 25 M f32, 16 KiB tiles
+            shapes[key] = ("%s x 25 M f32" % key[1:], int(key[1:]), 25_000_000, torch.float32, 16384)
         name, n, p, dt, tile_b = shapes[key]
         es = torch.tensor([], dtype=dt).element_size()
         te = tile_b // es
