@@ -1354,14 +1354,16 @@ unsigned lds_pad_for(size_t static_lds, int wgs) {
   return per > static_cast<int64_t>(static_lds) ? static_cast<unsigned>(per - static_lds) : 0;
 }
 
-// The same cap for the kernels over separate peer buffers (row-major wsum_vec_kernel, the many-tensor
-// wsum_multi_vec_kernel); DLA_VEC_CAP_ROWS=0 runs them uncapped (A/B).
+// The kernels over separate peer buffers (row-major wsum_vec_kernel, the many-tensor
+// wsum_multi_vec_kernel) run uncapped: with the tiled kernel's table they lose (google_speech
+// ResNet-34 x 16 bf16 device modules 135.3-135.8 -> 150.3-150.8 us; the other device rounds within
+// noise, profiles/r03ad).  DLA_VEC_CAP_ROWS=1 applies the table to them (A/B).
 int vec_wgs_cap_rows(int dt, int n_peers, int64_t n_vecs) {
-  static const bool off = [] {
+  static const bool on = [] {
     const char* v = std::getenv("DLA_VEC_CAP_ROWS");
-    return v && std::atoi(v) == 0;
+    return v && std::atoi(v) == 1;
   }();
-  return off ? 0 : vec_wgs_cap(dt, n_peers, n_vecs);
+  return on ? vec_wgs_cap(dt, n_peers, n_vecs) : 0;
 }
 
 template <class K>
