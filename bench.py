@@ -1244,7 +1244,7 @@ def dfl_round(msgs, p, device, reps=3):
             "round_GBps": round((n + 1) * p * 4 / med[3] / 1e9, 2),
             "aggregate_serialized_ms": round(med[4] * 1e3, 2),
             "aggregate_serialized_path": "DeviceModelManager.aggregate_serialized: the reduce, then the averaged row "
-                                         "D2H in 8 MiB chunks through page-locked bounce buffers straight into "
+                                         "D2H in 32 MiB chunks through page-locked bounce buffers straight into "
                                          "the payload bytes (no result module; replaces aggregate + serialize)",
             "path": "EVA blocks -> split at model_data_len -> restricted decode into page-locked ingress buffers "
                     "-> async H2D into the tile-interleaved PeerSlab -> reduce -> D2H into the pooled result -> "

@@ -1,6 +1,7 @@
 #!/bin/bash
-# r03ae: the final round-3 build (occupancy-cap table for 4 and 8-16 peers, separate-buffer kernels uncapped) end to end:
-# command), the rocprofv3 kernel trace + FETCH / WRITE passes of the headline (profiles/collect.sh),
+# r03ae: the final round-3 build (occupancy-cap table for 4 and 8-16 peers, separate-buffer kernels
+# uncapped) end to end: the whole GPU suite + smoke, the default N=1 bench (the driver's command), the
+# rocprofv3 kernel trace + FETCH / WRITE passes of the headline (profiles/collect.sh),
 # and the 4-rank gloo rehearsal of the N>1 legs.
 set -o pipefail
 export TMPDIR=/tmp
