@@ -141,6 +141,32 @@ def test_north_star_tiled_slab_dirichlet_every_element():
     assert same_bits(out.cpu().numpy(), want, "f32")
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,dtype", [(4, "f32"), (9, "f32"), (12, "f32"), (16, "f32"), (16, "bf16"), (10, "bf16")])
+def test_occupancy_capped_tiled_passes_every_element(n, dtype):
+    """The occupancy-capped launches (vec_wgs_cap: passes of 4 and 8-16 peers over >= 256 MiB of
+    input get dynamic LDS so only W workgroups fit a CU) compute exactly what the uncapped kernel
+    does: n peers of just over 256 MiB / n of input each, 16 KiB tiles, Dirichlet weights, ragged
+    tail — every element against the C oracle."""
+    from accdfl_amd import _lib
+
+    es = 4 if dtype == "f32" else 2
+    numel = (256 << 20) // (n * es) + 12_345  # past the cap's 256 MiB threshold, odd tail
+    code = _lib.DLA_F32 if dtype == "f32" else _lib.DLA_BF16
+    tile = 16384 // es
+    slab = _slab(n, numel, dtype, 9100 + n)
+    buf = _tiled(slab, n, numel, tile)
+    host = slab[:, :numel].cpu()
+    del slab
+    w = [float(x) for x in np.random.default_rng(n).dirichlet(np.ones(n))]
+    out = torch.empty(numel, dtype=torch.float32 if dtype == "f32" else torch.bfloat16, device="cuda")
+    _lib.wsum_slab_tiled_ptr(code, buf.data_ptr(), tile, n, w, numel, out.data_ptr(),
+                             torch.cuda.current_stream().cuda_stream)
+    want = c_wsum([_bits(host[k], dtype) if dtype == "bf16" else host[k].numpy() for k in range(n)], w, dtype)
+    got = _bits(out, dtype) if dtype == "bf16" else out.cpu().numpy()
+    assert same_bits(got, want, dtype)
+
+
 def test_configs4_whole_model_tiled_4k_bf16_every_lane_position():
     """configs[4]'s whole model (128 x 21,296,355 bf16) in the tile-interleaved slab with 4 KiB
     tiles (dla_slab_tile_elems for it), on the chunk-covering sample: every bf16 position of a
