@@ -1355,15 +1355,22 @@ unsigned lds_pad_for(size_t static_lds, int wgs) {
 }
 
 // The kernels over separate peer buffers (row-major wsum_vec_kernel, the many-tensor
-// wsum_multi_vec_kernel) run uncapped: with the tiled kernel's table they lose (google_speech
-// ResNet-34 x 16 bf16 device modules 135.3-135.8 -> 150.3-150.8 us; the other device rounds within
-// noise, profiles/r03ad).  DLA_VEC_CAP_ROWS=1 applies the table to them (A/B).
-int vec_wgs_cap_rows(int dt, int n_peers, int64_t n_vecs) {
-  static const bool on = [] {
+// wsum_multi_vec_kernel) with the tiled kernel's table lose (google_speech ResNet-34 x 16 bf16
+// device modules 135.3-135.8 -> 150.3-150.8 us, profiles/r03ad; 16 x 25 M f32 rows 253.6 at best
+// against 250.7 for the big tile, profiles/r03ag), except 8-peer passes of the row-major kernel
+// over >= 256 MiB at W = 16: 8 x 25 M f32 134.1 -> 129.4 us (and 134.7 for the big tile it now
+// replaces), 8 x 50 M bf16 134.8 -> 129.0 (profiles/r03ag).  `multi`: the many-tensor kernel, kept
+// uncapped (unmeasured at 8 peers).  DLA_VEC_CAP_ROWS=1 applies the whole tiled table, =0 none (A/B).
+int vec_wgs_cap_rows(int dt, int n_peers, int64_t n_vecs, bool multi = false) {
+  static const int env = [] {
     const char* v = std::getenv("DLA_VEC_CAP_ROWS");
-    return v && std::atoi(v) == 1;
+    return v ? std::atoi(v) : -1;
   }();
-  return on ? vec_wgs_cap(dt, n_peers, n_vecs) : 0;
+  if (env == 1) return vec_wgs_cap(dt, n_peers, n_vecs);
+  if (env == 0 || multi) return 0;
+  const char* forced = std::getenv("DLA_VEC_WGS_PER_CU");
+  if (forced) return std::atoi(forced);
+  return n_peers == 8 && static_cast<int64_t>(n_peers) * n_vecs * 8 >= (int64_t{256} << 20) ? 16 : 0;
 }
 
 template <class K>
@@ -1546,6 +1553,12 @@ hipError_t launch_pass(const PeerTable<typename Ops<DT>::w_t, KMAX>& tab, int n,
   }
   if (l.variant == 8 || (l.auto_kernel && use_wide(n_elems / Ops<DT>::E, n, Ops<DT>::E)))
     return launch_wide<DT, KMAX, ACC_IN>(tab, n, n_elems, out, s);
+  if constexpr (KMAX == 8 && DT == DLA_F32) {
+    // 8 fp32 peers over >= 256 MiB: the row-major vector kernel at 16 workgroups per CU beats the
+    // big tile (8 x 25 M: 129.4 vs 134.7 us, profiles/r03ag)
+    if (l.auto_kernel && n == 8 && int64_t{n} * n_elems * 4 >= kMallBytes)
+      return launch_vec<DT, KMAX, ACC_IN>(tab, n, n_elems, out, s, vec_variant(n));
+  }
   if constexpr (KMAX == 8 && !ACC_IN && (DT == DLA_F32 || DT == DLA_F64)) {
     const int kind = l.auto_kernel ? use_bigtile(n_elems / Ops<DT>::E, Ops<DT>::E, n) : l.variant;
     if (kind == 16 || kind == 17) return launch_bigtile<DT, KMAX>(tab, n, n_elems, out, s, kind == 17);
@@ -1665,7 +1678,7 @@ hipError_t launch_multi_vec(const MultiIndex* idx, const MultiSeg* segs, int n_s
   std::memset(&wt, 0, sizeof(wt));
   for (int k = 0; k < pm; ++k) wt.w[k] = static_cast<W>(weights[k0 + k]);  // RNE double -> op-math
   const dim3 g(static_cast<unsigned>(grid)), bl(64);
-  const int wgs = vec_wgs_cap_rows(DT, pm, grid * 64);  // every workgroup folds 64 vectors
+  const int wgs = vec_wgs_cap_rows(DT, pm, grid * 64, true);  // every workgroup folds 64 vectors
   if (plain) {
     static const size_t st_lds = static_lds_of(&wsum_multi_vec_kernel<DT, KMAX, G, ACC_IN, true>);
     hipLaunchKernelGGL((wsum_multi_vec_kernel<DT, KMAX, G, ACC_IN, true>), g, bl, lds_pad_for(st_lds, wgs), s, idx,
@@ -2202,6 +2215,7 @@ const char* dla_select_kernel(int dtype, int n_peers, int64_t n_elems) {
       !(dtype == DLA_F32 && (first_pass == 16 || first_pass == 32) && use_bigtile(n_elems / e, e, n_peers)))
     return "wsum_vec_kernel";
   if (use_wide(n_elems / e, first_pass, e)) return "wsum_wide_kernel";
+  if (dtype == DLA_F32 && n_peers == 8 && int64_t{8} * n_elems * 4 >= kMallBytes) return "wsum_vec_kernel";
   if ((dtype == DLA_F32 || dtype == DLA_F64) && use_bigtile(n_elems / e, e, n_peers))
     return "wsum_bigtile_kernel";
   return "wsum_stream_kernel";

@@ -60,6 +60,8 @@ def main():
     ap.add_argument("--grids", default="0")
     ap.add_argument("--ns-tiles", default="", help="extra tile sizes (bytes) for the north star, tree build")
     ap.add_argument("--variants", default="", help="extra tree legs with these launch variants (e.g. 8,12,28)")
+    ap.add_argument("--rows", default="", help="also time the peers as separate row-major buffers: default + "
+                                               "these dla_wsum_ex variants (e.g. 9,12)")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
@@ -113,6 +115,19 @@ def main():
                 if rc != 0:
                     raise RuntimeError("dla_wsum_slab_tiled rc=%d" % rc)
             legs[lname] = fn
+        if args.rows:  # the same peers as separate row-major buffers (dla_wsum / dla_wsum_ex)
+            pitch = -(-p // 64) * 64
+            rows = torch.empty(n, pitch, dtype=dt, device=dev)
+            rows[:, :p].copy_(slab[: n_t * n * te].view(n_t, n, te).permute(1, 0, 2).reshape(n, -1)[:, :p])
+            rptrs = [rows[k].data_ptr() for k in range(n)]
+            for v in [0] + [int(x) for x in args.rows.split(",") if x]:
+                o = torch.empty(p, dtype=dt, device=dev)
+                lname = "rows v%d" % v if v else "rows default"
+                outs[lname] = o
+
+                def fn(v=v, o=o, rows=rows, rptrs=rptrs):
+                    _lib.wsum_ptrs(code, rptrs, w, p, o.data_ptr(), sp, _lib.LaunchCfg(v, 0, 0, 0) if v else None)
+                legs[lname] = fn
         for v in [int(x) for x in args.variants.split(",") if x]:
             cfg = _lib.LaunchCfg(v, 0, 0, 0)
             o = torch.empty(p, dtype=dt, device=dev)

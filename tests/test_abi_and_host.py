@@ -65,7 +65,8 @@ def test_library_version_and_argument_errors(lib_path):
     assert L.max_peers_per_pass == 128
     # kernel selection by shape (host-only query): north star, configs[3] share, configs[4] share,
     # configs[2], GNLeNet 8 peers, fp64 north-star shape, few peers, invalid arguments
-    assert _lib.select_kernel(0, 8, 25_000_000) == "wsum_bigtile_kernel"
+    assert _lib.select_kernel(0, 8, 25_000_000) == "wsum_vec_kernel"  # capped row-major (r03ag)
+    assert _lib.select_kernel(0, 16, 24_500_000) == "wsum_bigtile_kernel"
     assert _lib.select_kernel(0, 64, 21_339) == "wsum_vec_kernel"
     assert _lib.select_kernel(1, 128, 2_662_045) == "wsum_vec_kernel"
     assert _lib.select_kernel(0, 32, 1_690_046) == "wsum_vec_kernel"
@@ -78,7 +79,8 @@ def test_library_version_and_argument_errors(lib_path):
     # launch: the partial last round goes to segment workgroups)
     assert _lib.select_kernel(0, 16, 12_500_000) == "wsum_bigtile_kernel"
     assert _lib.select_kernel(0, 16, 21_296_355) == "wsum_bigtile_kernel"
-    assert _lib.select_kernel(0, 8, 21_300_000) == "wsum_bigtile_kernel"
+    assert _lib.select_kernel(0, 8, 21_300_000) == "wsum_vec_kernel"  # 8 fp32 peers: capped row-major
+    assert _lib.select_kernel(3, 8, 21_300_000) == "wsum_bigtile_kernel"  # fp64 keeps the big tile
     assert _lib.select_kernel(0, 8, 3_400_000) == "wsum_stream_kernel"
     assert _lib.select_kernel(0, 32, 3_000_000) == "wsum_vec_kernel"  # 0.72 of one round
     assert _lib.select_kernel(0, 32, 4_110_000) == "wsum_bigtile_kernel"
