@@ -1324,6 +1324,11 @@ int vec_wgs_cap(int dt, int n_peers, int64_t n_vecs) {
   (void)dt;  // f32 and bf16 measured alike
   const int64_t in_bytes = static_cast<int64_t>(n_peers) * n_vecs * 8;
   if (in_bytes < (int64_t{256} << 20)) return 0;
+  // passes of 32 and more peers over >= 1 GiB, with 16 (or, at 64 peers, 8) peers per round
+  // (tiled_variant): W = 8 (profiles/r03ai, us: 32 x 10 M f32 199.3 -> 191.5, 48 x 6 M f32 177.6 ->
+  // 171.1, 64 x 4.93 M f32 192.2 -> 184.3, 64 x 8 M f32 316.3 -> 300.8, 128 x 21.3 M bf16 813.8 ->
+  // 803.3); smaller ones (configs[4]'s 681 MB share, configs[3']'s 316 MB bucket) lose with a cap.
+  if (n_peers >= 32) return in_bytes >= (int64_t{1} << 30) ? 8 : 0;
   switch (n_peers) {
     case 4: return 26;
     case 8: return 14;
@@ -2928,10 +2933,10 @@ int dla_wsum_slab_tiled(int dtype, const void* base, int64_t tile_elems, int64_t
   if (!out) return fail(DLA_E_INVALID, "dla_wsum_slab_tiled: null out");
   int tshift = 0;
   while ((int64_t{1} << tshift) < tile_elems) ++tshift;
-  const int variant =
-      cfg && cfg->variant
-          ? cfg->variant
-          : vec_store_policy(vec_variant(n_peers < kMaxPeersPerPass ? n_peers : kMaxPeersPerPass), n_elems * es);
+  const int first_pass = n_peers < kMaxPeersPerPass ? n_peers : kMaxPeersPerPass;
+  int variant = cfg && cfg->variant ? cfg->variant : vec_store_policy(vec_variant(first_pass), n_elems * es);
+  if (!(cfg && cfg->variant) && first_pass >= 32 && int64_t{first_pass} * n_elems * es >= (int64_t{1} << 30))
+    variant = first_pass == 64 ? 8 : 12;  // fewer peers per round under the occupancy cap (vec_wgs_cap)
   if (variant != 8 && variant != 9 && variant != 12 && variant != 21 && variant != 28)
     return fail(DLA_E_CONFIG, "dla_wsum_slab_tiled: variant must be 0 (auto), 8, 9, 12, 21 or 28");
   const int64_t stride = slab_rows * tile_elems;

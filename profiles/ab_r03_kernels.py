@@ -95,6 +95,9 @@ def main():
     for key in args.shapes.split(","):
         if key.startswith("n") and key[1:].isdigit():  # nK: K peers x 25 M f32, 16 KiB tiles
             shapes[key] = ("%s x 25 M f32" % key[1:], int(key[1:]), 25_000_000, torch.float32, 16384)
+        if key.startswith("p") and "x" in key:  # pKxM: K peers x M million f32, 4 KiB tiles
+            k_, m_ = key[1:].split("x")
+            shapes[key] = ("%s x %s M f32" % (k_, m_), int(k_), int(float(m_) * 1e6), torch.float32, 4096)
         name, n, p, dt, tile_b = shapes[key]
         es = torch.tensor([], dtype=dt).element_size()
         te = tile_b // es
