@@ -2958,10 +2958,14 @@ int64_t dla_slab_tile_elems(int dtype, int slab_rows, int64_t n_elems) {
   // 16 rows (8 x 25 M f32 130.2 / 131.1 / 132.1 us for 16 / 4 / 1 KiB; 16 x 21.3 M bf16 106.3 /
   // 108.3 / 109.2), 1 KiB for rows under 1 MiB (128 x 85 354 f32 9.5 / 10.9 / 9.8), else 4 KiB
   // (128 x 21.3 M bf16 792 / 796 / 831; 64 x 1.23 M f32 47.5 / 55.2 / 48.5; within 2 % of the
-  // best elsewhere: 128 x 2.66 M bf16 103.6 vs 102.7, 32 x 1.69 M f32 33.5 vs 32.8).
+  // best elsewhere: 128 x 2.66 M bf16 103.6 vs 102.7, 32 x 1.69 M f32 33.5 vs 32.8).  Under the
+  // occupancy cap (round 3) 32 KiB tiles for up to 8 rows: 8 x 25 M f32 125.2-125.5 us against
+  // 125.8-126.0 for 16 KiB, 128.4-128.7 for 64 KiB, 129.8-130.2 for 4 KiB (profiles/r03ak, r03al).
   int64_t bytes = 4096;
   if (n_elems * es < (int64_t{1} << 20))
     bytes = 1024;
+  else if (slab_rows <= 8)
+    bytes = 32768;
   else if (slab_rows <= 16)
     bytes = 16384;
   return bytes / es;

@@ -90,7 +90,8 @@ def test_library_version_and_argument_errors(lib_path):
     assert _lib.select_kernel(2, 3, 1000) == "wsum_vec_kernel" and _lib.select_kernel(3, 3, 1000) != "wsum_vec_kernel"
     assert _lib.select_kernel(9, 8, 100) == "" and _lib.select_kernel(0, 0, 100) == ""
     # tile of the tile-interleaved PeerSlab (dla_slab_tile_elems, host-only)
-    assert _lib.slab_tile_elems(0, 8, 25_000_000) * 4 == 16384
+    assert _lib.slab_tile_elems(0, 8, 25_000_000) * 4 == 32768
+    assert _lib.slab_tile_elems(0, 16, 25_000_000) * 4 == 16384
     assert _lib.slab_tile_elems(1, 128, 2_662_045) * 2 == 4096
     assert _lib.slab_tile_elems(0, 128, 85_354) * 4 == 1024 and _lib.slab_tile_elems(0, 8, 1000) * 4 == 1024
     assert _lib.slab_tile_elems(9, 8, 100) == 0

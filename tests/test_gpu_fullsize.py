@@ -121,14 +121,14 @@ def _tiled(slab, n, numel, tile):
 
 def test_north_star_tiled_slab_dirichlet_every_element():
     """The headline's own kernel and layout at full size: 8 peers x 25 M fp32 in the
-    tile-interleaved slab with 16 KiB tiles (what dla_slab_tile_elems picks for it), reduced by
+    tile-interleaved slab with 32 KiB tiles (what dla_slab_tile_elems picks for it), reduced by
     dla_wsum_slab_tiled with NON-uniform (Dirichlet) weights — every element against the C oracle
     (the only full-size check of this path used uniform 1/8 weights)."""
     from accdfl_amd import _lib
 
     n, numel = 8, 25_000_000
     tile = _lib.slab_tile_elems(_lib.DLA_F32, n, numel)
-    assert tile * 4 == 16384
+    assert tile * 4 == 32768
     slab = _slab(n, numel, "f32", 8100)
     buf = _tiled(slab, n, numel, tile)
     host = slab[:, :numel].cpu()
