@@ -1315,11 +1315,16 @@ unsigned vec_lds_pad() {
 // faster at W 18-24 (profiles/r03ac).  2, 3, 5, 6 and 7 peers, 32 and more peers (register-limited
 // already) and launches that fit the Infinity Cache lose with any cap, so they run uncapped.
 // DLA_VEC_WGS_PER_CU=W overrides the policy (A/B sweeps).
-int vec_wgs_cap(int dt, int n_peers, int64_t n_vecs) {
+int vec_wgs_env() {
   static const int env = [] {
     const char* v = std::getenv("DLA_VEC_WGS_PER_CU");
     return v ? std::atoi(v) : -1;
   }();
+  return env;
+}
+
+int vec_wgs_cap(int dt, int n_peers, int64_t n_vecs) {
+  const int env = vec_wgs_env();
   if (env >= 0) return env;
   (void)dt;  // f32 and bf16 measured alike
   const int64_t in_bytes = static_cast<int64_t>(n_peers) * n_vecs * 8;
@@ -1373,8 +1378,7 @@ int vec_wgs_cap_rows(int dt, int n_peers, int64_t n_vecs, bool multi = false) {
   }();
   if (env == 1) return vec_wgs_cap(dt, n_peers, n_vecs);
   if (env == 0 || multi) return 0;
-  const char* forced = std::getenv("DLA_VEC_WGS_PER_CU");
-  if (forced) return std::atoi(forced);
+  if (vec_wgs_env() >= 0) return vec_wgs_env();
   return n_peers == 8 && static_cast<int64_t>(n_peers) * n_vecs * 8 >= (int64_t{256} << 20) ? 16 : 0;
 }
 

@@ -143,7 +143,7 @@ def main():
                 if rc != 0:
                     raise RuntimeError("dla_wsum_slab_tiled rc=%d" % rc)
             legs[lname] = fn
-        if key == "ns" and args.ns_tiles:
+        if args.ns_tiles:  # re-tiled copies of the same peers (any shape)
             for tb in [int(x) for x in args.ns_tiles.split(",")]:
                 t2 = tb // es
                 sl2 = torch.empty(-(-p // t2) * n * t2, dtype=dt, device=dev)
