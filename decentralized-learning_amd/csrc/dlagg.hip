@@ -932,9 +932,7 @@ struct WeightTable {
   W w[KMAX];
 };
 
-// BV: blocks of 64 vectors per workgroup (1, or 4 for large rounds: the tensor lookup and the peer
-// pointer row are paid once per 4 blocks).
-template <int DT, int KMAX, int G, bool ACC_IN, bool PLAIN_ST, int BV = 1>
+template <int DT, int KMAX, int G, bool ACC_IN, bool PLAIN_ST>
 __global__ __launch_bounds__(64) void wsum_multi_vec_kernel(const MultiIndex* __restrict__ idx,
                                                             const MultiSeg* __restrict__ segs, int n_seg, int k0,
                                                             int n_peers,
@@ -951,17 +949,15 @@ __global__ __launch_bounds__(64) void wsum_multi_vec_kernel(const MultiIndex* __
   const int64_t local = b - segs[lo].wg_begin;
   const PeerRef<typename O::w_t> tab{(ConstPeerTab)(segs[lo].ptrs + k0), wt.w};
   void* const out_v = segs[lo].out;
-  if (local >= (n_vecs + 64 * BV - 1) / (64 * BV)) {  // this tensor's ragged-tail workgroup
+  if (local >= (n_vecs + 63) / 64) {  // this tensor's ragged-tail workgroup
     fold_tail<DT, ACC_IN>(segs[lo].ptrs + k0, tab.w, n_peers, n_vecs * VW * WE, segs[lo].n_elems, out_v);
     return;
   }
-  V* out = static_cast<V*>(out_v);
-  __attribute__((address_space(1))) V* gout = (__attribute__((address_space(1))) V*)out_v;  // global_* access
-  for (int bb = 0; bb < BV; ++bb) {
-  const int64_t j = (local * BV + bb) * 64 + threadIdx.x;
-  if (BV > 1 && (local * BV + bb) * 64 >= n_vecs) break;  // uniform: past the tensor's last block
+  const int64_t j = local * 64 + threadIdx.x;
   const bool live = j < n_vecs;
   const int64_t i = live ? j : n_vecs - 1;  // clamped: loads stay unpredicated
+  V* out = static_cast<V*>(out_v);
+  __attribute__((address_space(1))) V* gout = (__attribute__((address_space(1))) V*)out_v;  // global_* access
   acc_t acc[VW][WE];
   if constexpr (ACC_IN) {
     const V o = gout[i];
@@ -987,7 +983,6 @@ __global__ __launch_bounds__(64) void wsum_multi_vec_kernel(const MultiIndex* __
       gout[i] = o;
     else
       store_vec_sc1(out + i, o);
-  }
   }
 }
 
@@ -1686,51 +1681,35 @@ int64_t multi_table_bytes(int n_tensors, int n_peers) {
 
 template <int DT, int KMAX, int G, bool ACC_IN>
 hipError_t launch_multi_vec(const MultiIndex* idx, const MultiSeg* segs, int n_seg, int64_t grid, int k0, int pm,
-                            const double* weights, bool plain, int bv, hipStream_t s) {
+                            const double* weights, bool plain, hipStream_t s) {
   using W = typename Ops<DT>::w_t;
   WeightTable<W, KMAX> wt;
   std::memset(&wt, 0, sizeof(wt));
   for (int k = 0; k < pm; ++k) wt.w[k] = static_cast<W>(weights[k0 + k]);  // RNE double -> op-math
   const dim3 g(static_cast<unsigned>(grid)), bl(64);
-  const int wgs = vec_wgs_cap_rows(DT, pm, grid * 64 * bv, true);  // every workgroup folds 64 x bv vectors
-#define DLA_MULTI_L(PST, BVV)                                                                                    \
-  do {                                                                                                          \
-    static const size_t st_lds = static_lds_of(&wsum_multi_vec_kernel<DT, KMAX, G, ACC_IN, PST, BVV>);          \
-    hipLaunchKernelGGL((wsum_multi_vec_kernel<DT, KMAX, G, ACC_IN, PST, BVV>), g, bl, lds_pad_for(st_lds, wgs), s, \
-                       idx, segs, n_seg, k0, pm, wt);                                                           \
-  } while (0)
+  const int wgs = vec_wgs_cap_rows(DT, pm, grid * 64, true);  // every workgroup folds 64 vectors
   if (plain) {
-    if (bv == 4) DLA_MULTI_L(true, 4); else DLA_MULTI_L(true, 1);
+    static const size_t st_lds = static_lds_of(&wsum_multi_vec_kernel<DT, KMAX, G, ACC_IN, true>);
+    hipLaunchKernelGGL((wsum_multi_vec_kernel<DT, KMAX, G, ACC_IN, true>), g, bl, lds_pad_for(st_lds, wgs), s, idx,
+                       segs, n_seg, k0, pm, wt);
   } else {
-    if (bv == 4) DLA_MULTI_L(false, 4); else DLA_MULTI_L(false, 1);
+    static const size_t st_lds = static_lds_of(&wsum_multi_vec_kernel<DT, KMAX, G, ACC_IN, false>);
+    hipLaunchKernelGGL((wsum_multi_vec_kernel<DT, KMAX, G, ACC_IN, false>), g, bl, lds_pad_for(st_lds, wgs), s, idx,
+                       segs, n_seg, k0, pm, wt);
   }
-#undef DLA_MULTI_L
   return hipGetLastError();
 }
 
 template <int DT, bool ACC_IN>
 hipError_t launch_multi_vec_pass(const MultiIndex* idx, const MultiSeg* segs, int n_seg, int64_t grid, int k0, int pm,
-                                 const double* weights, bool plain, int bv, hipStream_t s) {
+                                 const double* weights, bool plain, hipStream_t s) {
   // peers in flight per lane as the single-tensor vec kernel (vec_variant): 32 for passes of >= 32
   // peers, 16 above 8, else 8
   if (pm > 32)
-    return launch_multi_vec<DT, kMaxPeersPerPass, 32, ACC_IN>(idx, segs, n_seg, grid, k0, pm, weights, plain, bv, s);
-  if (pm == 32) return launch_multi_vec<DT, 32, 32, ACC_IN>(idx, segs, n_seg, grid, k0, pm, weights, plain, bv, s);
-  if (pm > 8) return launch_multi_vec<DT, 32, 16, ACC_IN>(idx, segs, n_seg, grid, k0, pm, weights, plain, bv, s);
-  return launch_multi_vec<DT, 8, 8, ACC_IN>(idx, segs, n_seg, grid, k0, pm, weights, plain, bv, s);
-}
-
-// Blocks of 64 vectors per workgroup of the many-tensor kernel: 4 for rounds of >= 256 MiB of input
-// (fewer, longer workgroups: one tensor lookup per 4 blocks), else 1 (small rounds need the
-// workgroups to fill the chip).  DLA_MULTI_BV=1 or 4 forces it (A/B).
-int multi_bv(int64_t in_bytes) {
-  static const int env = [] {
-    const char* v = std::getenv("DLA_MULTI_BV");
-    const int b = v ? std::atoi(v) : 0;
-    return b == 1 || b == 4 ? b : 0;
-  }();
-  if (env) return env;
-  return in_bytes >= (int64_t{256} << 20) ? 4 : 1;
+    return launch_multi_vec<DT, kMaxPeersPerPass, 32, ACC_IN>(idx, segs, n_seg, grid, k0, pm, weights, plain, s);
+  if (pm == 32) return launch_multi_vec<DT, 32, 32, ACC_IN>(idx, segs, n_seg, grid, k0, pm, weights, plain, s);
+  if (pm > 8) return launch_multi_vec<DT, 32, 16, ACC_IN>(idx, segs, n_seg, grid, k0, pm, weights, plain, s);
+  return launch_multi_vec<DT, 8, 8, ACC_IN>(idx, segs, n_seg, grid, k0, pm, weights, plain, s);
 }
 
 template <int DT>
@@ -1744,8 +1723,6 @@ hipError_t run_multi_table(const std::vector<int>& packed, const void* const* pe
   for (int i = 0; i < m; ++i) out_bytes += numels[packed[i]] * static_cast<int64_t>(sizeof(typename Ops<DT>::elem_t));
   // plain output stores for passes of >= 32 peers writing <= 8 MiB in all (vec_store_policy)
   const bool plain_ok = out_bytes <= (int64_t{8} << 20);
-  const int bv = multi_bv(out_bytes * n);
-  const int64_t blk = 64 * bv;
   struct Launch1 { int64_t off; int mc; int64_t grid; };
   std::vector<Launch1> launches;
   int64_t off = 0;
@@ -1765,7 +1742,7 @@ hipError_t run_multi_table(const std::vector<int>& packed, const void* const* pe
       segs[i].ptrs = reinterpret_cast<const void* const*>(td + ptab_off + static_cast<int64_t>(c0 + i) * n * 8);
       std::memcpy(ptab + static_cast<int64_t>(c0 + i) * n, peer_ptrs + static_cast<int64_t>(t) * n, sizeof(void*) * n);
       ix->fine[i] = static_cast<int32_t>(wg);
-      wg += (nv + blk - 1) / blk + (numels[t] > nv * per_vec ? 1 : 0);
+      wg += (nv + 63) / 64 + (numels[t] > nv * per_vec ? 1 : 0);
       if (wg > 0x7fffffff) return hipErrorInvalidValue;
     }
     for (int q = 0; q < 16; ++q) ix->coarse[q] = ix->fine[16 * q];
@@ -1779,8 +1756,8 @@ hipError_t run_multi_table(const std::vector<int>& packed, const void* const* pe
     for (const Launch1& L : launches) {
       const MultiIndex* ix = reinterpret_cast<const MultiIndex*>(td + L.off);
       const MultiSeg* segs = reinterpret_cast<const MultiSeg*>(td + L.off + sizeof(MultiIndex));
-      e = k0 > 0 ? launch_multi_vec_pass<DT, true>(ix, segs, L.mc, L.grid, k0, pm, weights, plain_ok && pm >= 32, bv, s)
-                 : launch_multi_vec_pass<DT, false>(ix, segs, L.mc, L.grid, k0, pm, weights, plain_ok && pm >= 32, bv, s);
+      e = k0 > 0 ? launch_multi_vec_pass<DT, true>(ix, segs, L.mc, L.grid, k0, pm, weights, plain_ok && pm >= 32, s)
+                 : launch_multi_vec_pass<DT, false>(ix, segs, L.mc, L.grid, k0, pm, weights, plain_ok && pm >= 32, s);
       if (e != hipSuccess) return e;
     }
   }
