@@ -1,5 +1,6 @@
 """Wire format (§8 f1/f3): decoding the reference's serialize_model bytes without
 executing the payload, and producing bytes in the same format."""
+import collections
 import io
 import json
 import os
@@ -99,6 +100,23 @@ def test_device_model_manager_wire_round():
     back = wire.loads_state_dict(mm.aggregate_serialized(weights))
     for name in names:
         assert same_bits(back[name].numpy(), want[name].numpy(), "f32"), name
+
+
+def test_device_source_entries_encode_like_tensors():
+    """wire.DeviceSource (aggregate_serialized's parameter entries): small entries go through the CPU
+    like any tensor, so a state dict whose entries are slices of one flat tensor encodes to exactly
+    the objects of the plain state dict (CPU: the flat tensor stands in for the averaged row)."""
+    from accdfl_amd.core import wire
+
+    flat = torch.randn(3 * 40 + 7, generator=torch.Generator().manual_seed(1))
+    sd_plain = collections.OrderedDict([("a", flat[:120].view(3, 40).clone()), ("b", flat[120:].clone()),
+                                        ("steps", torch.tensor(5))])
+    sd_dev = collections.OrderedDict([("a", wire.DeviceSource(flat, 0, (3, 40))), ("b", wire.DeviceSource(flat, 120, (7,))),
+                                      ("steps", torch.tensor(5))])
+    for got in (wire.loads_state_dict(wire.dumps_state_dict(sd_dev)), pickle.loads(wire.dumps_state_dict(sd_dev))):
+        assert list(got.keys()) == ["a", "b", "steps"]
+        for k in sd_plain:
+            assert torch.equal(got[k], sd_plain[k]), k
 
 
 class _ConvBN(nn.Module):
