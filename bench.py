@@ -1201,8 +1201,13 @@ def dfl_messages(n, p, seed=300):
 def dfl_round(msgs, p, device, reps=3):
     """§8 f1-f3 at north-star scale: one DFL aggregator round (accdfl/dfl/community.py:576-673)
     end to end — every message's EVA blocks split at model_data_len and decoded into page-locked
-    ingress buffers -> HBM PeerSlab (no b''.join, no slice copy, no create_model /
-    load_state_dict), the uniform average (:673), and its serialize_model bytes (:556-567)."""
+    ingress buffers -> HBM PeerSlab tiles (no b''.join, no slice copy, no create_model /
+    load_state_dict), the uniform average (:673), and its serialize_model bytes (:556-567).
+    ``phases`` splits the ingress (sums over the round's peers, medians over the reps): the wire
+    split, decode + gather into the page-locked buffers (of which the native gather), the stage
+    calls, the copy stream's own time for the peers' H2D (HIP events, ``copy_busy_ms``) and its idle
+    time between them, and ``wait_ms``: the copy stream draining after the loop (ingress_complete_ms =
+    ingress_ms + wait_ms: when the last peer is in HBM)."""
     from torch import nn
 
     from accdfl_amd.core import wire
@@ -1218,11 +1223,26 @@ def dfl_round(msgs, p, device, reps=3):
 
     def one():
         mm.reset_incoming_trained_models()
+        ph = mm.start_phases()
+        wire.GATHER_MS = []
+        t_split = 0.0
         t0 = time.perf_counter()
         for k, (blocks, ml) in enumerate(msgs):
+            ts = time.perf_counter()
             head, _ = wire.split_blocks(blocks, ml)
+            t_split += time.perf_counter() - ts
             mm.process_incoming_serialized(b"peer%d" % k, head)
         t1 = time.perf_counter()
+        mm.slab.copy_stream.synchronize()
+        tw = time.perf_counter()
+        gathers, wire.GATHER_MS = wire.GATHER_MS, None
+        mm.phases = None
+        ev = ph["copy_events"]
+        busy = sum(a.elapsed_time(b) for a, b in ev)
+        idle = sum(ev[i - 1][1].elapsed_time(ev[i][0]) for i in range(1, len(ev)))
+        phases = {"split_ms": t_split * 1e3, "decode_gather_ms": sum(ph["decode_gather_ms"]),
+                  "native_gather_ms": sum(gathers), "stage_issue_ms": sum(ph["stage_issue_ms"]),
+                  "copy_busy_ms": busy, "copy_idle_between_peers_ms": idle, "wait_ms": (tw - t1) * 1e3}
         out = mm.aggregate_trained_models()
         t2 = time.perf_counter()
         data = wire.serialize_model(out)
@@ -1233,22 +1253,29 @@ def dfl_round(msgs, p, device, reps=3):
         direct = mm.aggregate_serialized()
         t5 = time.perf_counter()
         assert len(direct) == len(data)
-        return t1 - t0, t2 - t1, t3 - t2, t3 - t0, t5 - t4
+        return (t1 - t0, t2 - tw, t3 - t2, t3 - t0, t5 - t4, tw - t0), phases
 
     one()
     runs = [one() for _ in range(reps)]
-    med = [statistics.median(r[i] for r in runs) for i in range(5)]
+    med = [statistics.median(r[0][i] for r in runs) for i in range(6)]
+    phases = {k: round(statistics.median(r[1][k] for r in runs), 2) for k in runs[0][1]}
+    h2d_bytes = n * p * 4
+    phases["copy_GBps"] = round(h2d_bytes / (phases["copy_busy_ms"] / 1e3) / 1e9, 2) if phases["copy_busy_ms"] else None
+    phases["gather_GBps"] = (round(h2d_bytes / (phases["native_gather_ms"] / 1e3) / 1e9, 2)
+                             if phases["native_gather_ms"] else None)
     return {"peers": n, "params": p, "eva_block_bytes": EVA_BLOCK,
-            "ingress_ms": round(med[0] * 1e3, 2), "aggregate_ms": round(med[1] * 1e3, 2),
+            "ingress_ms": round(med[0] * 1e3, 2), "ingress_complete_ms": round(med[5] * 1e3, 2),
+            "aggregate_ms": round(med[1] * 1e3, 2),
             "egress_serialize_ms": round(med[2] * 1e3, 2), "round_ms": round(med[3] * 1e3, 2),
             "round_GBps": round((n + 1) * p * 4 / med[3] / 1e9, 2),
             "aggregate_serialized_ms": round(med[4] * 1e3, 2),
+            "phases": phases,
             "aggregate_serialized_path": "DeviceModelManager.aggregate_serialized: the reduce, then the averaged row "
                                          "D2H in 32 MiB chunks through page-locked bounce buffers straight into "
                                          "the payload bytes (no result module; replaces aggregate + serialize)",
-            "path": "EVA blocks -> split at model_data_len -> restricted decode into page-locked ingress buffers "
-                    "-> async H2D into the tile-interleaved PeerSlab -> reduce -> D2H into the pooled result -> "
-                    "serialize_model bytes"}
+            "path": "EVA blocks -> split at model_data_len -> restricted decode, gather into page-locked ingress "
+                    "buffers -> one 2D H2D per peer straight into the tile-interleaved PeerSlab (dla_slab_stage) "
+                    "-> reduce -> D2H into the pooled result -> serialize_model bytes"}
 
 
 def dfl_round_reference_style(msgs, p, reps=2):

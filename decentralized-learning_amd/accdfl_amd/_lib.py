@@ -19,11 +19,15 @@ REPO_ROOT = os.path.dirname(PKG_ROOT)
 CSRC = os.path.join(PKG_ROOT, "csrc", "dlagg.hip")
 INCLUDE = os.path.join(REPO_ROOT, "include")
 HEADER = os.path.join(INCLUDE, "dlagg.h")
-LIB_PATH = os.environ.get("DLAGG_LIB", os.path.join(PKG_ROOT, "lib", "libdlagg.so"))
+# ACCDFL_AMD_TUNING=1 loads the tuning build (lib/libdlagg_tuning.so, -DDLA_TUNING=1: the same library
+# plus the A/B environment knobs the profiles/ scripts sweep); the product build reads no environment.
+TUNING = os.environ.get("ACCDFL_AMD_TUNING", "") == "1"
+LIB_PATH = os.environ.get("DLAGG_LIB", os.path.join(PKG_ROOT, "lib",
+                                                    "libdlagg_tuning.so" if TUNING else "libdlagg.so"))
 
 # dtype codes (include/dlagg.h)
 DLA_F32, DLA_BF16, DLA_F16, DLA_F64 = 0, 1, 2, 3
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 HIPCC_FLAGS = [
     "--offload-arch=gfx950",
@@ -65,6 +69,7 @@ EXPORTED = (
     "dla_host_reduce_join",
     "dla_wsum_multi_table_bytes",
     "dla_wsum_multi_table",
+    "dla_slab_stage",
 )
 
 
@@ -72,16 +77,19 @@ class DlaggError(RuntimeError):
     """A libdlagg call returned a non-zero status."""
 
 
-def source_build_id() -> str:
+def source_build_id(tuning: bool = False) -> str:
     """Hash of the sources and flags libdlagg.so is built from (csrc/dlagg.hip,
-    include/dlagg.h, HIPCC_FLAGS).  build() compiles it into the library, and lib()
-    refuses a library whose dla_build_id() differs from the tree's."""
+    include/dlagg.h, HIPCC_FLAGS; the tuning build's flag too).  build() compiles it into the
+    library, and lib() refuses a library whose dla_build_id() differs from the tree's."""
     h = hashlib.sha256()
     for path in (CSRC, HEADER):
         with open(path, "rb") as f:
             h.update(f.read())
-    h.update(" ".join(HIPCC_FLAGS).encode())
+    h.update(" ".join(HIPCC_FLAGS + (_TUNING_FLAGS if tuning else [])).encode())
     return h.hexdigest()[:20]
+
+
+_TUNING_FLAGS = ["-DDLA_TUNING=1"]
 
 
 _ID_PREFIX = b"dlagg-build-id:"
@@ -101,17 +109,18 @@ def file_build_id(path: str, prefix: bytes = _ID_PREFIX) -> Optional[str]:
     return data[i + len(prefix):j].decode(errors="replace")
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    """Compile csrc/dlagg.hip for gfx950 into lib/libdlagg.so (in-tree), unless the
-    library there already carries this tree's build id."""
-    out = os.path.join(PKG_ROOT, "lib", "libdlagg.so")
-    bid = source_build_id()
+def build(force: bool = False, verbose: bool = False, tuning: bool = False) -> str:
+    """Compile csrc/dlagg.hip for gfx950 into lib/libdlagg.so (in-tree; tuning=True: the A/B build,
+    lib/libdlagg_tuning.so), unless the library there already carries this tree's build id."""
+    out = os.path.join(PKG_ROOT, "lib", "libdlagg_tuning.so" if tuning else "libdlagg.so")
+    bid = source_build_id(tuning)
     if not force and file_build_id(out) == bid:
         return out
     os.makedirs(os.path.dirname(out), exist_ok=True)
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
     tmp = out + ".tmp"
-    cmd = [hipcc, *HIPCC_FLAGS, '-DDLA_BUILD_ID="%s"' % bid, "-I", INCLUDE, "-o", tmp, CSRC]
+    cmd = [hipcc, *HIPCC_FLAGS, *(_TUNING_FLAGS if tuning else []), '-DDLA_BUILD_ID="%s"' % bid, "-I", INCLUDE,
+           "-o", tmp, CSRC]
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)
@@ -313,6 +322,9 @@ class _Lib:
                                             ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_double),
                                             ctypes.c_int, vp, vp, vp]
         so.dla_wsum_multi_table.restype = ctypes.c_int
+        so.dla_slab_stage.argtypes = [ctypes.c_int, vp, ctypes.c_int64, ctypes.c_int64, ctypes.c_int, ctypes.c_int64,
+                                      vp, ctypes.c_int64, vp]
+        so.dla_slab_stage.restype = ctypes.c_int
         so.dla_plan_destroy.argtypes = [vp]
         so.dla_plan_destroy.restype = None
         v = so.dla_version()
@@ -320,7 +332,7 @@ class _Lib:
             raise RuntimeError("libdlagg ABI version %d, expected %d" % (v, ABI_VERSION))
         self.build_id = so.dla_build_id().decode()
         if os.path.exists(CSRC) and os.path.exists(HEADER):
-            want = source_build_id()
+            want = source_build_id(tuning=os.path.basename(path) == "libdlagg_tuning.so")
             if self.build_id != want:
                 raise RuntimeError(
                     "stale libdlagg.so at %s: built from sources %s, the tree's are %s — rebuild it "
@@ -578,6 +590,15 @@ def wsum_slab_tiled_ptr(dtype_code: int, base_ptr: int, tile_elems: int, slab_ro
     rc = L.so.dla_wsum_slab_tiled(dtype_code, base_ptr, tile_elems, slab_rows, _dbl_array(weights), len(weights),
                                   n_elems, out_ptr, stream_ptr, ctypes.byref(cfg) if cfg is not None else None)
     L.check(rc, "dla_wsum_slab_tiled")
+
+
+def slab_stage(dtype_code: int, base_ptr: int, tile_elems: int, slab_rows: int, row: int, dst_elem: int, src_ptr: int,
+               n_elems: int, stream_ptr: int) -> None:
+    """dla_slab_stage: n_elems elements at src_ptr (host or device) -> row `row` of a tile-interleaved
+    slab from flat element dst_elem on (one 2D copy for the whole tiles)."""
+    L = lib()
+    L.check(L.so.dla_slab_stage(dtype_code, base_ptr, tile_elems, slab_rows, row, dst_elem, src_ptr, n_elems,
+                                stream_ptr), "dla_slab_stage")
 
 
 def slab_tile_elems(dtype_code: int, slab_rows: int, n_elems: int) -> int:

@@ -149,27 +149,24 @@ def set_host_devices(devices) -> None:
 
 def _devices_for(device: torch.device, round_bytes: int = 0) -> List[torch.device]:
     """The GPUs a host-staged round of CPU models streams through, in bucket order:
-    * set_host_devices([...]), else ACCDFL_AMD_DEVICES: a comma list of device ids, "current" (only
-      the current device: the opt-out) or "all";
-    * by default, a round that moves at least _MIN_SHARD_BYTES per device over PCIe uses every visible
-      GPU, the current one first — each bucket crosses its own GPU's PCIe link, bit-identically —
-      unless the process is one rank of a multi-rank torch.distributed group (one process per GPU:
-      the other GPUs belong to the other ranks).  The caller trims the list to the round's size."""
+    * set_host_devices([...]), else ACCDFL_AMD_DEVICES: a comma list of device ids, "all" (every
+      visible GPU, the current one first: each bucket crosses its own GPU's PCIe link,
+      bit-identically) or "current";
+    * by default only the current device.  The reference runs every DFL / GL peer as its own ipv8
+      process, so an aggregator that spread its rounds over every visible GPU would open a context,
+      page-locked staging and HBM staging on GPUs other processes own and compete for their PCIe
+      links: the several-GPU host path is opt-in.  The caller trims the list to the
+      round's size (_MIN_SHARD_BYTES per device)."""
     if _host_devices:
         return list(_host_devices)
     env = os.environ.get("ACCDFL_AMD_DEVICES", "").strip().lower()
     if env and env not in ("all", "current"):
         return [torch.device("cuda", int(x)) for x in env.split(",") if x.strip()]
-    if env == "current" or round_bytes < 2 * _MIN_SHARD_BYTES:
+    if env != "all" or round_bytes < 2 * _MIN_SHARD_BYTES:
         return [device]
     count = torch.cuda.device_count()
     if count < 2:
         return [device]
-    if env != "all":
-        import torch.distributed as dist
-
-        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
-            return [device]
     return [device] + [torch.device("cuda", d) for d in range(count) if d != device.index]
 
 
@@ -255,7 +252,8 @@ def _reduce_host_small(device, dtype, center: List[torch.Tensor], peers: List[Li
 # the same de-duplication (pre-order over modules, a module or parameter seen before is skipped), without
 # named_modules' prefix strings and generator frames — the walk over every parameter of every model is
 # the host path's largest Python cost (128 google_speech ResNet-34 models: 14 080 parameters).
-_WALK_METHODS = ("parameters", "named_parameters", "named_modules", "_named_members", "modules")
+_WALK_METHODS = ("parameters", "named_parameters", "named_modules", "_named_members", "modules", "buffers",
+                 "named_buffers")
 _plain_walk_cls: Dict[type, bool] = {}
 
 
@@ -388,10 +386,62 @@ def _device_round(models: List[nn.Module], weights, layout) -> "nn.Module | None
     """The whole aggregate for device-resident models of one layout: deepcopy(models[0]) with fresh
     parameters (fedavg.py:20), then every parameter of every model folded straight into them by
     dla_wsum_multi(_table) from one pointer table — one launch per 128-peer pass for rounds of many
-    peers, whatever the tensor count (fedavg.py:23-25).  Stream-ordered like any torch op."""
+    peers, whatever the tensor count (fedavg.py:23-25).  Stream-ordered like any torch op.
+
+    The host work around the launch is batched (a 16-model ResNet-34 round spent 2 ms
+    of Python around a 0.13 ms reduce): the result's parameters are views of ONE device allocation
+    (each 256-byte aligned, as the table kernel wants), so the reduce is launched right after the walk;
+    models[0]'s device buffers are copied by one gather kernel per dtype into another allocation
+    (torch's flatten / unflatten of dense tensors) instead of one deepcopy dispatch per buffer; the
+    module tree is cloned while the kernel runs."""
     dtype, device, numels, table = layout
-    # the result's parameters first, the reduce into them next, the module tree last: the table's
-    # copy and the kernel run while the host clones the module (deepcopy of models[0], fedavg.py:20)
+    mod = _lib.walk_module()
+    objs = mod.tensors(models[0], _PLAIN_SET) if mod is not None else None
+    if objs is None or len(objs[0]) != len(numels) or any(type(p) is not nn.Parameter for p in objs[0]):
+        return _device_round_per_tensor(models, weights, layout)
+    p0, b0 = objs
+    esize = torch.empty((), dtype=dtype).element_size()
+    align = _ALIGN_BYTES // esize
+    offs, total = [], 0
+    for n_ in numels:
+        offs.append(total)
+        total += _round_up(max(n_, 1), align)
+    flat = torch.empty(total, dtype=dtype, device=device)
+    base = flat.data_ptr()
+    ptrs = (ctypes.c_void_p * table.size).from_buffer(table)
+    outs = (ctypes.c_void_p * len(numels))(*[base + o * esize for o in offs])
+    nums = (ctypes.c_int64 * len(numels))(*numels)
+    _wsum.wsum_multi_ptrs(dtype, ptrs, outs, nums, weights, device)
+    # while the reduce runs: the result's parameters over `flat`, models[0]'s buffers, the module tree
+    make = torch.Tensor._make_subclass  # what nn.Parameter(data, requires_grad) does for a plain tensor
+    memo = {id(p): make(nn.Parameter, flat.as_strided(p.size(), p.stride(), o), p.requires_grad)
+            for p, o in zip(p0, offs)}
+    _seed_buffers(b0, memo)
+    return _clone_value(models[0], memo)
+
+
+def _seed_buffers(buffers, memo: dict) -> None:
+    """deepcopy of models[0]'s device buffers (fedavg.py:20 copies them, it does not average them) in
+    one gather per (device, dtype) group: the copies are views of one fresh allocation each, seeded
+    into the deepcopy memo.  Buffers that are not plain dense tensors without grad keep the stock
+    deepcopy."""
+    groups: Dict[tuple, list] = {}
+    for b in buffers:
+        if (type(b) is torch.Tensor and b.is_cuda and not b.requires_grad and b.is_contiguous()
+                and id(b) not in memo):
+            groups.setdefault((b.device, b.dtype), []).append(b)
+    for bs in groups.values():
+        if len(bs) < 2:
+            continue
+        flat = torch._C._nn.flatten_dense_tensors(bs)
+        for b, c in zip(bs, torch._C._nn.unflatten_dense_tensors(flat, bs)):
+            memo[id(b)] = c
+
+
+def _device_round_per_tensor(models: List[nn.Module], weights, layout) -> "nn.Module | None":
+    """_device_round for module trees the walk extension cannot read (no extension, Parameter
+    subclasses): one fresh tensor per parameter, the stock deepcopy of every buffer."""
+    dtype, device, numels, table = layout
     memo = _fresh_params(models[0])
     params = [memo[id(p)] for p in models[0].parameters()] if len(memo) == len(numels) else []
     if len(params) != len(numels) or not all(c.is_contiguous() and c.device == device for c in params):

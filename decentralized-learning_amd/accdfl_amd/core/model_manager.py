@@ -14,6 +14,7 @@ from __future__ import annotations
 
 import collections
 import copy
+import time
 from typing import Dict, List, Optional
 
 import torch
@@ -98,6 +99,14 @@ class DeviceModelManager(ModelManager):
         # registry), so a registry entry removed mid-round never hands its slot — still viewed by
         # a live WirePeer — to the next arrival
         self._ingress_next = 0
+        # per-arrival phase record of process_incoming_serialized (None: off).  start_phases() turns it
+        # on: decode + gather into the ingress buffer (CPU), the stage call (CPU) and HIP timing events
+        # around each arrival's copies on the slab's copy stream (bench.py dfl_round's phase split)
+        self.phases: Optional[dict] = None
+
+    def start_phases(self) -> dict:
+        self.phases = {"decode_gather_ms": [], "stage_issue_ms": [], "copy_events": []}
+        return self.phases
 
     @staticmethod
     def _fingerprint(model) -> tuple:
@@ -168,15 +177,27 @@ class DeviceModelManager(ModelManager):
             self._ingress_next += 1
             n_tensors = len(self.template.state_dict())
             alloc = self._ingress_alloc(pos, sum(len(b) for b in data) + 256 * (n_tensors + 1))
+        ph = self.phases
+        t0 = time.perf_counter() if ph is not None else 0.0
         sd = wire.loads_state_dict(data, copy=False, alloc=alloc)  # views of `data` / the ingress buffer
         params = wire.parameter_tensors(sd, self.template)
         peer = WirePeer(sd)
         self.incoming_trained_models[peer_pk] = peer
         if self.slab is None:
             self.slab = self._slab_cls.for_model(self.template, capacity=self._capacity, device=self._device)
+        if ph is not None:
+            t1 = time.perf_counter()
+            ph["decode_gather_ms"].append((t1 - t0) * 1e3)
+            e0 = torch.cuda.Event(enable_timing=True)
+            e0.record(self.slab.copy_stream)
         if self.slab.matches(params) and len(self._staged) == self.slab.n:
             self.slab.stage(params)
             self._staged.append((peer_pk, peer, ()))
+        if ph is not None:
+            e1 = torch.cuda.Event(enable_timing=True)
+            e1.record(self.slab.copy_stream)
+            ph["stage_issue_ms"].append((time.perf_counter() - t1) * 1e3)
+            ph["copy_events"].append((e0, e1))
         if alloc is not None:
             ev = torch.cuda.Event()
             ev.record(self.slab.copy_stream)
@@ -251,19 +272,27 @@ class DeviceModelManager(ModelManager):
         # the module aggregate_trained_models returns: the template's structure with the first
         # arrival's buffers (wire peers), or deepcopy(models[0]) (module peers)
         structure = self.template if isinstance(first, WirePeer) else first
-        names = [name for name, _ in structure.named_parameters()]
-        state = structure.state_dict()
+        params = list(structure.parameters())
+        state = structure.state_dict(keep_vars=True)
         bufs = first.state_dict if isinstance(first, WirePeer) else state
-        if len(names) != len(self.slab.numels) or any(
-                k not in state or state[k].shape != s for k, s in zip(names, self.slab.shapes)):
+        # every state-dict key of a parameter — a tied parameter is listed once by parameters() but
+        # under each alias by state_dict() — maps to that parameter's averaged row, by identity
+        offsets = {id(p): (o, p.shape) for p, o in zip(params, self.slab._offsets())}
+        param_keys = {k for k, v in state.items() if id(v) in offsets}
+        if (len(params) != len(self.slab.numels) or any(p.shape != s for p, s in zip(params, self.slab.shapes))
+                or len(param_keys) < len(params)
+                # the payload must carry what serialize_model(aggregate_trained_models()) carries: its
+                # parameters are CPU tensors here (DeviceSource), so every other entry must be too
+                or any(v.device.type != "cpu" for v in state.values())
+                or any(bufs[k].device.type != "cpu" for k in state if k not in param_keys and k in bufs)):
             return wire.serialize_model(self.aggregate_trained_models(weights))
         with torch.no_grad():
             flat = self.slab._reduce_planned(weights)
-            offsets = dict(zip(names, self.slab._offsets()))
             sd = collections.OrderedDict()
             for k, v in state.items():
-                if k in offsets:
-                    sd[k] = wire.DeviceSource(flat, offsets[k], v.shape)
+                if k in param_keys:
+                    off, shape = offsets[id(v)]
+                    sd[k] = wire.DeviceSource(flat, off, shape)
                 elif k in bufs and bufs[k].shape == v.shape:
                     # the round's models[0] buffers (deepcopy, fedavg.py:20), in the structure's dtype
                     sd[k] = bufs[k].detach().to(v.dtype)

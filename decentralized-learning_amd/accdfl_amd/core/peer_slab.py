@@ -14,9 +14,12 @@ HBM layout.  fp32 / bf16 / f16 slabs are TILE-INTERLEAVED:
 ``buf[t, k]``, so the tiles of every peer at one offset are adjacent and the reduce
 (dla_wsum_slab_tiled) streams one region of HBM at a time instead of ``capacity`` regions
 100 MB apart: 8 x 25 M fp32 130.2 us against 135.6 for separate rows, 128 x 21.3 M bf16
-792 against 869 (profiles/r02d_ab_tiled.log).  ``tile`` is dla_slab_tile_elems (1-16 KiB).
-A row is staged contiguously on the device first and scattered into its tiles by one
-device copy (HBM speed, on the copy stream).  fp64 slabs keep one row per peer
+792 against 869 (profiles/r02d_ab_tiled.log).  ``tile`` is dla_slab_tile_elems (1-32 KiB).
+A row lands in its tiles directly: each source tensor (host memory, page-locked or pageable, or
+device memory) is one dla_slab_stage call on the copy stream — a 2D copy whose rows are tiles and
+whose destination pitch is ``capacity`` tiles, so the copy engine writes every tile in place (round
+3 staged a contiguous device row and scattered it: 2 x the row's bytes of extra HBM traffic, one
+more kernel and a row-sized buffer).  fp64 slabs keep one row per peer
 ([capacity, pitch], pitch = the parameter count rounded up to 256 bytes).  A 25 M-parameter
 fp32 model is a 100 MB row; 288 GB of HBM holds ~2800 of them, so capacity is never the
 constraint at accdfl's sample sizes.
@@ -59,7 +62,6 @@ class PeerSlab:
         self.copy_stream = torch.cuda.Stream(self.device)
         self._bounce = [None, None]
         self._bounce_ev = [None, None]
-        self._row_stage = None      # contiguous device row a tiled stage lands in before its scatter
         self._h_out = None
         self._flat = None          # device result of reduce_into (reused every round)
         self._plan = None          # prepared launch over (rows 0..n-1, _flat)
@@ -114,21 +116,13 @@ class PeerSlab:
                     new[:, : self.n, :].copy_(old[:, : self.n, :])
                 else:
                     for k in range(self.n):
-                        flat = self._tiles_of(old, k).reshape(-1)[: self.total]
-                        self._scatter(new, k, flat)
+                        flat = self._tiles_of(old, k).reshape(-1)[: self.total].contiguous()
+                        _lib.slab_stage(self.code, new.data_ptr(), self.tile, cap, k, 0, flat.data_ptr(),
+                                        self.total, int(self.copy_stream.cuda_stream))
+                        flat.record_stream(self.copy_stream)
         old.record_stream(self.copy_stream)
         self.buf = new
         self.capacity = cap
-
-    def _scatter(self, buf: torch.Tensor, k: int, flat: torch.Tensor):
-        """Contiguous row (``total`` elements, on the device) -> row k's tiles (copy stream)."""
-        full = self.total // self.tile
-        tiles = self._tiles_of(buf, k)
-        if full:
-            tiles[:full].copy_(flat[: full * self.tile].view(full, self.tile))
-        rest = self.total - full * self.tile
-        if rest:
-            tiles[full, :rest].copy_(flat[full * self.tile:])
 
     def _bounce_buffer(self, slot: int) -> torch.Tensor:
         ev = self._bounce_ev[slot]
@@ -159,20 +153,23 @@ class PeerSlab:
     # tensors are packed into the pinned bounce buffer and sent as one copy.
     DIRECT_BYTES = 1 << 20
 
+    def _put(self, row: int, off: int, src: torch.Tensor, n: int):
+        """``n`` elements at ``src`` (host or this device) -> row ``row`` from element ``off`` on, on the
+        copy stream.  Tiled slabs: dla_slab_stage, one 2D copy that writes every tile in place."""
+        if self.layout == "rows":
+            self.buf[row, off:off + n].copy_(src.view(-1)[:n], non_blocking=src.device.type == "cpu" and src.is_pinned())
+            return
+        _lib.slab_stage(self.code, self.buf.data_ptr(), self.tile, self.capacity, row, off, src.data_ptr(), n,
+                        int(self.copy_stream.cuda_stream))
+
     def _stage_flat_list(self, flat: List[torch.Tensor]) -> int:
         row = self.n
         if row >= self.capacity:
             self._grow(row + 1)
         cur = torch.cuda.current_stream(self.device)
         self.copy_stream.wait_stream(cur)
-        if self.layout == "rows":
-            dst_row = self.buf[row]
-        else:
-            if self._row_stage is None:
-                self._row_stage = torch.empty(self.pitch, dtype=self.dtype, device=self.device)
-            dst_row = self._row_stage
+        esize = self.buf.element_size()
         if all(t.device.type == "cpu" for t in flat):
-            esize = self.buf.element_size()
             slot = row & 1
             bounce = None
             run_start = None  # element offset where the current run of small tensors begins
@@ -184,7 +181,7 @@ class PeerSlab:
                     if not small and run_start is not None:  # flush the run of small tensors
                         _lib.host_copy_batch(*pending)
                         pending = ([], [], [])
-                        dst_row[run_start:off].copy_(bounce[run_start:off], non_blocking=True)
+                        self._put(row, run_start, bounce[run_start:off], off - run_start)
                         run_start = None
                     if t is None:
                         break
@@ -197,25 +194,24 @@ class PeerSlab:
                         pending[1].append(t.data_ptr())
                         pending[2].append(t.numel() * esize)
                     else:
-                        # H2D straight from where the tensor lives: pageable (no host copy) or a
-                        # page-locked ingress buffer (async; the caller keeps it until copy_stream passes)
-                        dst_row[off:off + t.numel()].copy_(t, non_blocking=t.is_pinned())
+                        # straight from where the tensor lives: pageable (no host copy) or a page-locked
+                        # ingress buffer (async; the caller keeps it until copy_stream passes)
+                        self._put(row, off, t, t.numel())
                     off += t.numel()
                 if bounce is not None:
                     ev = torch.cuda.Event()
                     ev.record(self.copy_stream)
                     self._bounce_ev[slot] = ev
         else:
-            dst = dst_row[: self.total]
             with torch.cuda.stream(self.copy_stream):
-                src = [t.to(self.device, non_blocking=True) for t in flat]
-                if len(src) == 1:
-                    dst.copy_(src[0])
-                else:
-                    torch.cat(src, out=dst)
-        if self.layout == "tiled":
-            with torch.cuda.stream(self.copy_stream):  # behind this row's H2D, before the next stage
-                self._scatter(self.buf, row, self._row_stage[: self.total])
+                off = 0
+                for t in flat:
+                    src = t if t.device == self.device else t.to(self.device, non_blocking=True)
+                    src = src.contiguous()
+                    self._put(row, off, src, src.numel())
+                    if src is not t:
+                        src.record_stream(self.copy_stream)  # a temporary: freed only after its copy
+                    off += t.numel()
         self.n = row + 1
         return row
 

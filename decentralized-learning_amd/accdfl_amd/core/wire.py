@@ -25,6 +25,7 @@ import io
 import os
 import pickle
 import threading
+import time
 from typing import Callable, Dict, List, Optional, Sequence
 
 import numpy as np
@@ -129,6 +130,10 @@ def _block_address(block) -> int:
 _INGRESS_NT = os.environ.get("ACCDFL_AMD_INGRESS_NT", "1") != "0"
 
 
+# When a list, _gather appends each gather's wall time in ms (bench.py dfl_round's phase split).
+GATHER_MS: Optional[list] = None
+
+
 def _gather(addrs, lens, dst: torch.Tensor) -> None:
     """Copy the pieces back to back into the host uint8 tensor ``dst`` (one native batched
     memcpy, threaded from 4 MiB: libdlagg's dla_host_copy_batch)."""
@@ -136,8 +141,11 @@ def _gather(addrs, lens, dst: torch.Tensor) -> None:
 
     if not lens:
         return
+    t0 = time.perf_counter() if GATHER_MS is not None else 0.0
     dsts = list(itertools.accumulate(lens[:-1], initial=dst.data_ptr()))
     _lib.host_copy_batch(dsts, addrs, lens, streaming=_INGRESS_NT and sum(lens) >= (4 << 20) and dst.is_pinned())
+    if GATHER_MS is not None:
+        GATHER_MS.append((time.perf_counter() - t0) * 1e3)
 
 
 def _parse_storage_blob(blob, alloc=None) -> torch.TypedStorage:

@@ -9,6 +9,7 @@ tensors' device and is NOT synchronised (torch stream semantics).
 from __future__ import annotations
 
 import os
+import threading
 from typing import List, Optional, Sequence
 
 import torch
@@ -157,11 +158,22 @@ class _TableRing:
     def __init__(self, device: torch.device):
         self.device = device
         self.slots = [None] * self.SLOTS  # (host uint8, device uint8, event or None)
+        self.busy = [False] * self.SLOTS  # taken and not yet done (another thread's call in flight)
         self.i = 0
+        self.lock = threading.Lock()
 
     def take(self, nbytes: int):
-        self.i = (self.i + 1) % self.SLOTS
-        slot = self.slots[self.i]
+        """(slot index, host buffer, device buffer); the caller passes the index to done()."""
+        with self.lock:
+            for _ in range(self.SLOTS):
+                self.i = (self.i + 1) % self.SLOTS
+                if not self.busy[self.i]:
+                    break
+            else:
+                raise RuntimeError("wsum_multi_table: more than %d concurrent calls on %s" % (self.SLOTS, self.device))
+            idx = self.i
+            self.busy[idx] = True
+            slot = self.slots[idx]
         if slot is not None and slot[2] is not None:
             slot[2].synchronize()
         if slot is None or slot[0].numel() < nbytes:
@@ -169,17 +181,20 @@ class _TableRing:
             size = 1 << (size - 1).bit_length()
             slot = (torch.empty(size, dtype=torch.uint8, pin_memory=True),
                     torch.empty(size, dtype=torch.uint8, device=self.device), None)
-            self.slots[self.i] = slot
-        return slot
+            self.slots[idx] = slot
+        return idx, slot[0], slot[1]
 
-    def done(self, stream: torch.cuda.Stream):
-        h, d, _ = self.slots[self.i]
+    def done(self, idx: int, stream: torch.cuda.Stream):
+        h, d, _ = self.slots[idx]
         ev = torch.cuda.Event()
         ev.record(stream)
-        self.slots[self.i] = (h, d, ev)
+        with self.lock:
+            self.slots[idx] = (h, d, ev)
+            self.busy[idx] = False
 
 
 _rings = {}
+_rings_lock = threading.Lock()
 
 
 def wsum_multi_ptrs(dtype: torch.dtype, ptrs, out_ptrs, numels, weights: Sequence[float], device: torch.device,
@@ -193,15 +208,16 @@ def wsum_multi_ptrs(dtype: torch.dtype, ptrs, out_ptrs, numels, weights: Sequenc
     table = n >= MULTI_TABLE_MIN_PEERS or (
         n > 8 and (n + 1) * sum(numels) * torch.empty((), dtype=dtype).element_size() >= MULTI_TABLE_MIN_BYTES)
     if table and dtype != torch.float64:
-        ring = _rings.get(device)
-        if ring is None:
-            ring = _rings[device] = _TableRing(device)
-        h, d, _ = ring.take(_lib.wsum_multi_table_bytes(len(out_ptrs), n))
+        with _rings_lock:
+            ring = _rings.get(device)
+            if ring is None:
+                ring = _rings[device] = _TableRing(device)
+        idx, h, d = ring.take(_lib.wsum_multi_table_bytes(len(out_ptrs), n))
         try:
             _lib.wsum_multi_table_ptrs(code, ptrs, out_ptrs, numels, weights, h.data_ptr(), d.data_ptr(),
                                        int(s.cuda_stream))
         finally:
-            ring.done(s)
+            ring.done(idx, s)
         return
     _lib.wsum_multi_ptrs(code, ptrs, out_ptrs, numels, weights, int(s.cuda_stream))
 

@@ -72,6 +72,16 @@ constexpr int kMaxPeersPerPass = 128; // pointer table in the kernel-argument bl
 
 thread_local std::string g_last_error;
 
+// A/B knobs (environment variables such as DLA_VEC_WGS_PER_CU) exist only in the tuning build
+// (-DDLA_TUNING=1 -> lib/libdlagg_tuning.so, loaded when ACCDFL_AMD_TUNING=1; profiles/ scripts
+// use it); the product library reads no environment and runs the measured policy.
+#ifndef DLA_TUNING
+#define DLA_TUNING 0
+#endif
+inline const char* tuning_env(const char* name) {
+  return DLA_TUNING ? std::getenv(name) : nullptr;
+}
+
 int fail(int code, const std::string& msg) {
   g_last_error = msg;
   return code;
@@ -1297,7 +1307,7 @@ hipError_t launch_wide(const PeerTable<typename Ops<DT>::w_t, KMAX>& tab, int n,
 // experiment (fewer waves, fewer DRAM pages open at once), nothing reads it.
 unsigned vec_lds_pad() {
   static const unsigned pad = [] {
-    const char* v = std::getenv("DLA_VEC_LDS_PAD");
+    const char* v = tuning_env("DLA_VEC_LDS_PAD");
     const long b = v ? std::atol(v) : 0;
     return static_cast<unsigned>(b < 0 ? 0 : b > 65536 ? 65536 : b);
   }();
@@ -1305,34 +1315,42 @@ unsigned vec_lds_pad() {
 }
 
 // Workgroups per CU the tiled vector kernel is capped at (0: uncapped), through dynamic LDS that only
-// W workgroups fit.  Uncapped, the one-wave workgroups fill a CU to the register limit (32 for the
-// 8-peer f32 instance); every wave holds n x 512 B of loads in flight, and past ~56-90 KiB per CU
-// more waves only keep more DRAM rows open at once.  Measured interleaved against the uncapped
-// kernel on HBM-sized launches (profiles/r03x, profiles/r03y, us): 8 x 25 M f32 (the north star)
-// 129.7 -> 125.8-126.3 at W = 14-15 (W 13: 131.0, W 12: 134.9, W 16: 127.6); 8 x 50 M bf16 130.0 ->
-// 125.1; 12 x 25 M f32 188.1 -> 183.7 at W 15; 16 x 25 M f32 245.4 -> 238.6 at W 9-10; 16 x 21.3 M
-// bf16 105.3 -> 101.8 at W 10; 4 x 25 M f32 73.6 -> 70.0 at W 26-28; 9-15 peers x 25 M f32 3.1-4.5 %
-// faster at W 18-24 (profiles/r03ac).  2, 3, 5, 6 and 7 peers, 32 and more peers (register-limited
-// already) and launches that fit the Infinity Cache lose with any cap, so they run uncapped.
-// DLA_VEC_WGS_PER_CU=W overrides the policy (A/B sweeps).
+// W workgroups fit.  Uncapped, the one-wave workgroups fill a CU to their register limit (32 for the
+// 8-peer f32 instance); past a certain number of 512-byte loads in flight per CU more waves only keep
+// more DRAM rows open at once (the counters: profiles/r03ab/pmc_summary.json — capped, the north star's
+// waves spend 6 % of their life waiting instead of 46 %, on the same bytes).  The rule (round 4,
+// replacing round 3's per-peer-count table): a wave's first fold round issues r1 loads of 512 B
+// (r1 = G, or the largest power of two <= the pass's peers when they are fewer than G: the tail splits
+// into rounds of G/2, G/4, ...), and
+//     W = round(Q / r1),  Q = 112 loads (56 KiB) per CU when the pass folds in ONE round,
+//                         Q = 192 loads (96 KiB) when it folds in several (its waves wait between rounds
+//                         with fewer loads out, so more of them are needed for the same bytes in flight),
+// applied to passes over more than the Infinity Cache (>= 256 MiB of input) whose W is below the
+// kernel's own register-limited occupancy.  It reproduces the sweeps it is fitted to (profiles/r03x,
+// r03y, r03ac, us): the north star 8 x 25 M f32 129.7 -> 125.8-126.3 at W = 14 (W 13: 131.0, 12: 134.9,
+// 16: 127.6), 8 x 50 M bf16 130.0 -> 125.1; 4 x 25 M f32 73.6 -> 70.0 (W 26-28; rule 28); 9-15 peers x 25 M
+// f32 (8 + smaller rounds, rule 24) 3.1-4.5 % faster (W 24 within 0.5 % of each count's best); 2, 3, 5, 6
+// and 7 peers (rule 56, 96, 48: at or above the register limit) uncapped, where every cap measured lost.
+// Exceptions, each an interleaved A/B against the rule (profiles/r04c): 16 peers in one round of 16,
+// and passes of >= 32 peers — register-limited at 16 waves per CU and holding 32 x 512 B per wave — which
+// over >= 1 GiB fold 16 peers per round under W = 8 (32 x 10 M f32 199.3 -> 191.5, 64 x 4.93 M f32 192.2
+// -> 184.3, 128 x 21.3 M bf16 813.8 -> 803.3, profiles/r03ai) and below it run uncapped (configs[4]'s
+// 681 MB share and configs[3']'s 316 MB bucket lose with any cap).
+// In the tuning build DLA_VEC_WGS_PER_CU=W overrides the policy and DLA_VEC_CAP_TABLE=1 restores the
+// round-3 table (A/B sweeps).
 int vec_wgs_env() {
   static const int env = [] {
-    const char* v = std::getenv("DLA_VEC_WGS_PER_CU");
+    const char* v = tuning_env("DLA_VEC_WGS_PER_CU");
     return v ? std::atoi(v) : -1;
   }();
   return env;
 }
 
-int vec_wgs_cap(int dt, int n_peers, int64_t n_vecs) {
-  const int env = vec_wgs_env();
-  if (env >= 0) return env;
-  (void)dt;  // f32 and bf16 measured alike
-  const int64_t in_bytes = static_cast<int64_t>(n_peers) * n_vecs * 8;
-  if (in_bytes < (int64_t{256} << 20)) return 0;
-  // passes of 32 and more peers over >= 1 GiB, with 16 (or, at 64 peers, 8) peers per round
-  // (tiled_variant): W = 8 (profiles/r03ai, us: 32 x 10 M f32 199.3 -> 191.5, 48 x 6 M f32 177.6 ->
-  // 171.1, 64 x 4.93 M f32 192.2 -> 184.3, 64 x 8 M f32 316.3 -> 300.8, 128 x 21.3 M bf16 813.8 ->
-  // 803.3); smaller ones (configs[4]'s 681 MB share, configs[3']'s 316 MB bucket) lose with a cap.
+constexpr int kLoadsPerCuOneRound = 112;
+constexpr int kLoadsPerCuRounds = 192;
+
+// Round 3's measured table (tuning build only: the A/B reference of the rule).
+int vec_wgs_cap_table(int n_peers, int64_t in_bytes) {
   if (n_peers >= 32) return in_bytes >= (int64_t{1} << 30) ? 8 : 0;
   switch (n_peers) {
     case 4: return 26;
@@ -1347,6 +1365,42 @@ int vec_wgs_cap(int dt, int n_peers, int64_t n_vecs) {
     case 16: return 10;
     default: return 0;
   }
+}
+
+// n_peers: the pass's peers; G: peers per fold round of the kernel instance; natural: the workgroups
+// per CU the instance reaches by its registers alone.
+int vec_wgs_cap(int n_peers, int G, int64_t n_vecs, int natural) {
+  const int env = vec_wgs_env();
+  if (env >= 0) return env;
+  const int64_t in_bytes = static_cast<int64_t>(n_peers) * n_vecs * 8;
+  if (in_bytes < (int64_t{256} << 20)) return 0;
+  static const bool table = [] {
+    const char* v = tuning_env("DLA_VEC_CAP_TABLE");
+    return v && std::atoi(v) == 1;
+  }();
+  if (table) return vec_wgs_cap_table(n_peers, in_bytes);
+  if (n_peers >= 32) return in_bytes >= (int64_t{1} << 30) ? 8 : 0;  // exception (see above)
+  if (n_peers > 16) return 0;                                        // 17-31 peers: never measured
+  if (n_peers == 16 && G == 16) return 10;                           // exception (see above)
+  int r1 = G;
+  if (n_peers < G) {
+    r1 = 1;
+    while (r1 * 2 <= n_peers) r1 *= 2;
+  }
+  const int q = n_peers == r1 ? kLoadsPerCuOneRound : kLoadsPerCuRounds;  // one fold round, or several
+  const int w = (q + r1 / 2) / r1;
+  return w < natural ? w : 0;
+}
+
+// Workgroups per CU a 64-thread kernel reaches without a cap (its register limit).
+template <class K>
+int natural_wgs_of(K kernel) {
+  int b = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kernel, 64, 0) != hipSuccess || b <= 0) {
+    (void)hipGetLastError();
+    return 32;
+  }
+  return b;
 }
 
 // Dynamic LDS per workgroup that caps a kernel whose own LDS is static_lds bytes at `wgs`
@@ -1373,10 +1427,10 @@ unsigned lds_pad_for(size_t static_lds, int wgs) {
 // uncapped (unmeasured at 8 peers).  DLA_VEC_CAP_ROWS=1 applies the whole tiled table, =0 none (A/B).
 int vec_wgs_cap_rows(int dt, int n_peers, int64_t n_vecs, bool multi = false) {
   static const int env = [] {
-    const char* v = std::getenv("DLA_VEC_CAP_ROWS");
+    const char* v = tuning_env("DLA_VEC_CAP_ROWS");
     return v ? std::atoi(v) : -1;
   }();
-  if (env == 1) return vec_wgs_cap(dt, n_peers, n_vecs);
+  if (env == 1) return vec_wgs_cap_table(n_peers, static_cast<int64_t>(n_peers) * n_vecs * 8);
   if (env == 0 || multi) return 0;
   if (vec_wgs_env() >= 0) return vec_wgs_env();
   return n_peers == 8 && static_cast<int64_t>(n_peers) * n_vecs * 8 >= (int64_t{256} << 20) ? 16 : 0;
@@ -1441,7 +1495,8 @@ hipError_t launch_vec_tiled(const PeerTable<typename Ops<DT>::w_t, KMAX>& tab, i
     if (n_elems > n_vecs * per_vec) ++grid;                                                                   \
     if (grid < 1 || grid > 0x7fffffff) return hipErrorInvalidValue;                                           \
     static const size_t st_lds = static_lds_of(&wsum_vec_kernel<DT, KMAX, G, VW_, ACC_IN, true, PST_>);     \
-    const unsigned lds_pad = lds_pad_for(st_lds, vec_wgs_cap(DT, n, n_vecs));                                  \
+    static const int natural = natural_wgs_of(wsum_vec_kernel<DT, KMAX, G, VW_, ACC_IN, true, PST_>);        \
+    const unsigned lds_pad = lds_pad_for(st_lds, vec_wgs_cap(n, G, n_vecs, natural));                         \
     hipLaunchKernelGGL((wsum_vec_kernel<DT, KMAX, G, VW_, ACC_IN, true, PST_>), dim3(static_cast<unsigned>(grid)),   \
                        dim3(64), lds_pad, s, tab, n, n_vecs, n_elems, out, tshift_e - vs, tstride_e / per_vec,    \
                        tshift_e, tstride_e);                                                                  \
@@ -2040,7 +2095,7 @@ int wsum_sharded_impl(int dtype, int n_shards, const int* dev_ids, const void* c
 // box's CPU share is 16); batches under 4 MiB stay on the calling thread.
 int copy_threads(int64_t total) {
   static const int cap = [] {
-    const char* e = std::getenv("DLA_COPY_THREADS");
+    const char* e = tuning_env("DLA_COPY_THREADS");
     const int v = e ? std::atoi(e) : 8;
     return v < 1 ? 1 : v > 64 ? 64 : v;
   }();
@@ -2136,7 +2191,7 @@ __attribute__((target("avx2"))) void stream_copy_avx2(char* d, const char* s, si
 // DLA_COPY_NT=0 turns the streaming stores off (A/B); they need AVX2 (every MI355X host has it).
 bool stream_copies() {
   static const bool on = [] {
-    const char* e = std::getenv("DLA_COPY_NT");
+    const char* e = tuning_env("DLA_COPY_NT");
     return !(e && std::atoi(e) == 0) && __builtin_cpu_supports("avx2");
   }();
   return on;
@@ -2569,7 +2624,7 @@ int host_reduce_impl(int dtype, int n_peers, int n_tensors, const void* const* t
   std::vector<int64_t> cs{begin};
   // DLA_HOST_RAMP=k: the first chunk is 1/k of chunk_elems (a power of two; default 4; A/B knob)
   static const int64_t ramp = [] {
-    const char* v = std::getenv("DLA_HOST_RAMP");
+    const char* v = tuning_env("DLA_HOST_RAMP");
     int64_t r = v ? std::atoll(v) : 4;
     if (r < 1) r = 1;
     int64_t p = 1;
@@ -2641,7 +2696,7 @@ int host_reduce_impl(int dtype, int n_peers, int n_tensors, const void* const* t
     copy_batch(dsts.data(), srcs.data(), bytes.data(), static_cast<int>(dsts.size()), false, min_threads);
   };
   // DLA_HOST_REDUCE_STATS=1: per-call phase times on stderr (host-path tuning)
-  static const bool stats = std::getenv("DLA_HOST_REDUCE_STATS") != nullptr;
+  static const bool stats = tuning_env("DLA_HOST_REDUCE_STATS") != nullptr;
   using clk = std::chrono::steady_clock;
   double t_wait = 0, t_pack = 0, t_issue = 0, t_unpack = 0, t_first = 0;
   auto secs = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double>(b - a).count(); };
@@ -2676,7 +2731,7 @@ int host_reduce_impl(int dtype, int n_peers, int n_tensors, const void* const* t
     // the copy queue is then not made to wait on the compute queue at all — a cross-queue wait in
     // front of every DMA stalls the copy engine between chunks.  DLA_HOST_WAIT_ALWAYS=1: always wait (A/B).
     if (c >= 2) {
-      static const bool always = std::getenv("DLA_HOST_WAIT_ALWAYS") != nullptr;
+      static const bool always = tuning_env("DLA_HOST_WAIT_ALWAYS") != nullptr;
       const hipError_t q = always ? hipErrorNotReady : hipEventQuery(red[buf]);
       if (q == hipErrorNotReady) {
         (void)hipGetLastError();
@@ -2874,7 +2929,7 @@ int dla_host_reduce_join(dla_host_job_t* job) {
     job->cv.wait(g, [job] { return job->done; });
   }
   if (job->th.joinable()) job->th.join();
-  static const bool stats = std::getenv("DLA_HOST_REDUCE_STATS") != nullptr;
+  static const bool stats = tuning_env("DLA_HOST_REDUCE_STATS") != nullptr;
   if (stats) {
     const auto now = std::chrono::steady_clock::now();
     auto ms = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
@@ -2952,6 +3007,44 @@ int dla_wsum_slab_tiled(int dtype, const void* base, int64_t tile_elems, int64_t
     default: e = run_tiled<DLA_F16>(base, tile_elems, tshift, stride, weights, n_peers, n_elems, out, s, variant); break;
   }
   if (e != hipSuccess) return fail(static_cast<int>(e), std::string("dla_wsum_slab_tiled: ") + hipGetErrorString(e));
+  return DLA_OK;
+}
+
+int dla_slab_stage(int dtype, void* base, int64_t tile_elems, int64_t slab_rows, int row, int64_t dst_elem,
+                   const void* src, int64_t n_elems, void* stream) {
+  g_last_error.clear();
+  const int es = elem_size(dtype);
+  if (es == 0) return fail(DLA_E_INVALID, "dla_slab_stage: unknown dtype");
+  if (!base || tile_elems < 1 || slab_rows < 1 || row < 0 || row >= slab_rows || dst_elem < 0 || n_elems < 0)
+    return fail(DLA_E_INVALID, "dla_slab_stage: need base, tile_elems >= 1 and 0 <= row < slab_rows");
+  if (n_elems == 0) return DLA_OK;
+  if (!src) return fail(DLA_E_INVALID, "dla_slab_stage: null src");
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const int64_t tb = tile_elems * es;  // bytes of one tile
+  char* b = static_cast<char*>(base);
+  const char* p = static_cast<const char*>(src);
+  int64_t pos = dst_elem, left = n_elems;
+  // element pos of the row lives at tile pos / tile_elems, slab row `row`, offset pos % tile_elems
+  auto at = [&](int64_t e) { return b + (((e / tile_elems) * slab_rows + row) * tile_elems + e % tile_elems) * es; };
+  auto failed = [](hipError_t e, const char* what) {
+    return fail(static_cast<int>(e), std::string("dla_slab_stage: ") + what + ": " + hipGetErrorString(e));
+  };
+  hipError_t e;
+  if (pos % tile_elems) {  // the partial tile the range starts in
+    const int64_t m = std::min(tile_elems - pos % tile_elems, left);
+    if ((e = hipMemcpyAsync(at(pos), p, static_cast<size_t>(m * es), hipMemcpyDefault, s)) != hipSuccess)
+      return failed(e, "head");
+    pos += m, left -= m, p += m * es;
+  }
+  const int64_t full = left / tile_elems;
+  if (full) {  // every whole tile in one 2D copy: rows of one tile, destination pitch = slab_rows tiles
+    if ((e = hipMemcpy2DAsync(at(pos), static_cast<size_t>(slab_rows * tb), p, static_cast<size_t>(tb),
+                              static_cast<size_t>(tb), static_cast<size_t>(full), hipMemcpyDefault, s)) != hipSuccess)
+      return failed(e, "tiles");
+    pos += full * tile_elems, left -= full * tile_elems, p += full * tb;
+  }
+  if (left && (e = hipMemcpyAsync(at(pos), p, static_cast<size_t>(left * es), hipMemcpyDefault, s)) != hipSuccess)
+    return failed(e, "tail");
   return DLA_OK;
 }
 

@@ -37,9 +37,10 @@ namespace {
 // Embedded as plain bytes too, so the build's id can be read from the file without loading it.
 __attribute__((used)) const char kWalkIdTag[] = "dlagg-walk-build-id:" DLA_WALK_BUILD_ID;
 
-// One model's parameters in nn.Module.parameters() order; false if a class is not plain.
+// One model's parameters in nn.Module.parameters() order (`which` = "_parameters"; "_buffers": its
+// buffers in nn.Module.buffers() order); false if a class is not plain.
 bool walk(PyObject* mod, PyObject* plain, std::unordered_set<PyObject*>& seen_m,
-          std::unordered_set<PyObject*>& seen_p, std::vector<PyObject*>& out) {
+          std::unordered_set<PyObject*>& seen_p, std::vector<PyObject*>& out, const char* which = "_parameters") {
   if (seen_m.count(mod)) return true;
   const int ok = PySet_Contains(plain, reinterpret_cast<PyObject*>(Py_TYPE(mod)));
   if (ok != 1) {
@@ -52,7 +53,7 @@ bool walk(PyObject* mod, PyObject* plain, std::unordered_set<PyObject*>& seen_m,
     PyErr_Clear();
     return false;
   }
-  PyObject* params = PyDict_GetItemString(d, "_parameters");  // borrowed
+  PyObject* params = PyDict_GetItemString(d, which);  // borrowed
   PyObject* mods = PyDict_GetItemString(d, "_modules");
   bool good = params && mods && PyDict_Check(params) && PyDict_Check(mods);
   if (good) {
@@ -66,7 +67,7 @@ bool walk(PyObject* mod, PyObject* plain, std::unordered_set<PyObject*>& seen_m,
     pos = 0;
     while (good && PyDict_Next(mods, &pos, &k, &v)) {
       if (v == Py_None) continue;
-      good = walk(v, plain, seen_m, seen_p, out);
+      good = walk(v, plain, seen_m, seen_p, out, which);
     }
   }
   Py_DECREF(d);
@@ -132,10 +133,28 @@ py::object layout(py::list models, int device, py::object plain, bool tensor_maj
   return py::make_tuple(py::str(dtype_name(dt)), numels, table, device);
 }
 
+// (parameters, buffers) of one model as lists, in parameters() / buffers() order, or None when its tree
+// holds a class outside `plain`: the result module's fresh tensors are made from these without another
+// Python walk of models[0] (fedavg._device_round).
+py::object tensors(py::object model, py::object plain) {
+  if (!PySet_Check(plain.ptr())) return py::none();
+  std::unordered_set<PyObject*> seen_m, seen_p;
+  std::vector<PyObject*> ps, bs;
+  if (!walk(model.ptr(), plain.ptr(), seen_m, seen_p, ps)) return py::none();
+  seen_m.clear();
+  seen_p.clear();
+  if (!walk(model.ptr(), plain.ptr(), seen_m, seen_p, bs, "_buffers")) return py::none();
+  py::list pl, bl;
+  for (PyObject* o : ps) pl.append(py::reinterpret_borrow<py::object>(o));
+  for (PyObject* o : bs) bl.append(py::reinterpret_borrow<py::object>(o));
+  return py::make_tuple(pl, bl);
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_dla_walk, m) {
   m.doc() = "accdfl_amd host plumbing: the per-round walk over every parameter of every model";
   m.def("layout", &layout, py::arg("models"), py::arg("device"), py::arg("plain"), py::arg("tensor_major"));
+  m.def("tensors", &tensors, py::arg("model"), py::arg("plain"));
   m.attr("build_id") = py::str(kWalkIdTag + sizeof("dlagg-walk-build-id:") - 1);
 }

@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define DLA_ABI_VERSION 9
+#define DLA_ABI_VERSION 10
 
 /* element dtypes of the peer buffers and of the output */
 #define DLA_F32 0
@@ -129,6 +129,19 @@ int dla_wsum_slab_tiled(int dtype, const void* base, int64_t tile_elems, int64_t
 /* The tile (in elements) the library recommends for a tile-interleaved slab of slab_rows rows of
  * n_elems elements (what PeerSlab uses); 0 for invalid arguments.  ABI v5. */
 int64_t dla_slab_tile_elems(int dtype, int slab_rows, int64_t n_elems);
+
+/* Stages n_elems elements of one peer into row `row` of a tile-interleaved slab (the layout
+ * dla_wsum_slab_tiled reads: [n_tiles][slab_rows][tile_elems]) at the row's flat element offset
+ * dst_elem — a received model's parameters landing in HBM (accdfl/core/model_manager.py:39-47 keeps
+ * them until fedavg.py:23-25 reads them; accdfl/util/eva/transfer/incoming.py:35 is where their bytes
+ * arrive).  `src` is host memory (page-locked or pageable) or device memory; the copy is ONE
+ * hipMemcpy2DAsync for the whole tiles (rows of one tile, destination pitch slab_rows tiles: the copy
+ * engine writes each tile in place) plus up to two plain copies for the partial tiles at either end,
+ * enqueued on `stream`.  No contiguous device row and no scatter pass.  The usual async-copy rules
+ * hold: page-locked sources must stay untouched until the stream passes the copy; pageable sources
+ * are consumed before the call returns.  ABI v10. */
+int dla_slab_stage(int dtype, void* base, int64_t tile_elems, int64_t slab_rows, int row, int64_t dst_elem,
+                   const void* src, int64_t n_elems, void* stream);
 
 /* Replaces the per-parameter inner loop of fedavg.py:24-25 for T parameter
  * tensors at once (one model = T tensors, parameters() order).

@@ -60,7 +60,7 @@ def test_library_version_and_argument_errors(lib_path):
     from accdfl_amd import _lib
 
     L = _lib.lib()
-    assert L.so.dla_version() == 9
+    assert L.so.dla_version() == 10
     assert L.build_id == _lib.source_build_id() == _lib.file_build_id(lib_path)
     assert L.max_peers_per_pass == 128
     # kernel selection by shape (host-only query): north star, configs[3] share, configs[4] share,
@@ -117,6 +117,14 @@ def test_library_version_and_argument_errors(lib_path):
     assert rc == -1 and b"tensor table" in L.so.dla_last_error()
     with pytest.raises(_lib.DlaggError, match="aliases peer 5"):
         _lib.wsum_multi_table_ptrs(0, ptrs, [ptrs[5]], [64], [1.0] * 130, 0, 0, 0)
+    # dla_slab_stage: argument errors caught before any copy (row outside the slab, null base / src)
+    rc = L.so.dla_slab_stage(0, 4096, 1024, 8, 8, 0, 8192, 100, None)
+    assert rc == -1 and b"row" in L.so.dla_last_error()
+    rc = L.so.dla_slab_stage(0, None, 1024, 8, 0, 0, 8192, 100, None)
+    assert rc == -1
+    rc = L.so.dla_slab_stage(0, 4096, 1024, 8, 0, 0, None, 100, None)
+    assert rc == -1 and b"src" in L.so.dla_last_error()
+    assert L.so.dla_slab_stage(0, 4096, 1024, 8, 0, 0, None, 0, None) == 0  # nothing to copy
     # launch knobs outside the built set are refused before any launch
     for bad in (_lib.LaunchCfg(3, 0, 0, 0), _lib.LaunchCfg(4, 3, 0, 0), _lib.LaunchCfg(4, 1, 0, 128),
                 _lib.LaunchCfg(10, 0, 0, 0), _lib.LaunchCfg(11, 0, 0, 0)):  # 16-byte vec forms: not built
@@ -528,6 +536,32 @@ def test_host_round_routing_and_chunks():
         assert n * c * esize >= min(fa._NATIVE_MIN_CHUNK_BYTES, n * bucket * esize) - n * align * esize
 
 
+def test_host_devices_default_is_the_current_gpu(monkeypatch):
+    """A round of CPU models stays on the current GPU unless the caller opts in (the
+    reference runs each peer as its own process, which must not take every GPU of the node)."""
+    from accdfl_amd.core.gradient_aggregation import fedavg as fa
+
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: 8)
+    monkeypatch.delenv("ACCDFL_AMD_DEVICES", raising=False)
+    cur = torch.device("cuda", 3)
+    big = 1 << 34
+    assert fa._devices_for(cur, big) == [cur]
+    monkeypatch.setenv("ACCDFL_AMD_DEVICES", "current")
+    assert fa._devices_for(cur, big) == [cur]
+    monkeypatch.setenv("ACCDFL_AMD_DEVICES", "all")
+    got = fa._devices_for(cur, big)
+    assert got[0] == cur and sorted(d.index for d in got) == list(range(8))
+    assert fa._devices_for(cur, 1 << 20) == [cur]  # too small to shard
+    monkeypatch.setenv("ACCDFL_AMD_DEVICES", "2,5")
+    assert fa._devices_for(cur, big) == [torch.device("cuda", 2), torch.device("cuda", 5)]
+    monkeypatch.delenv("ACCDFL_AMD_DEVICES")
+    fa.set_host_devices([1, 0])
+    try:
+        assert fa._devices_for(cur, big) == [torch.device("cuda", 1), torch.device("cuda", 0)]
+    finally:
+        fa.set_host_devices([])
+
+
 def test_fast_parameter_walk_is_parameters():
     """fedavg._parameters (the layout passes' walk) returns exactly list(m.parameters()): order, tied
     weights and shared submodules de-duplicated, None parameters skipped; a module class with its own
@@ -603,3 +637,12 @@ def test_native_walk_matches_the_python_walk():
     strided[0][0].weight = nn.Parameter(torch.zeros(4, 2, 3, 6)[..., ::2])  # not dense
     assert fa._native_layout(strided, -1, tensor_major=False) is None
     assert fa._native_layout(models, 0, tensor_major=False) is None  # CPU models asked for device 0
+    # tensors(): models[0]'s parameter and buffer objects in parameters() / buffers() order (the device
+    # round builds the result's fresh tensors from them)
+    m0 = models[0]
+    m0.register_buffer("none_buf", None)
+    m0.extra.register_buffer("shared_buf", m0[1].running_mean)  # the same buffer twice: listed once
+    ps, bs = _lib.walk_module().tensors(m0, fa._PLAIN_SET)
+    assert [id(p) for p in ps] == [id(p) for p in m0.parameters()]
+    assert [id(b) for b in bs] == [id(b) for b in m0.buffers()]
+    assert _lib.walk_module().tensors(m0, set()) is None  # a class outside the plain set

@@ -142,18 +142,24 @@ def test_north_star_tiled_slab_dirichlet_every_element():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n,dtype", [(4, "f32"), (9, "f32"), (12, "f32"), (16, "f32"), (16, "bf16"), (10, "bf16")])
-def test_occupancy_capped_tiled_passes_every_element(n, dtype):
-    """The occupancy-capped launches (vec_wgs_cap: passes of 4 and 8-16 peers over >= 256 MiB of
-    input get dynamic LDS so only W workgroups fit a CU) compute exactly what the uncapped kernel
-    does: n peers of just over 256 MiB / n of input each, 16 KiB tiles, Dirichlet weights, ragged
-    tail — every element against the C oracle."""
+@pytest.mark.parametrize("n,dtype,tile_bytes", [
+    (4, "f32", 16384), (9, "f32", 16384), (12, "f32", 16384), (16, "f32", 16384), (16, "bf16", 16384),
+    (10, "bf16", 16384),
+    # 32 KiB tiles: what PeerSlab uses for slabs of <= 8 rows (the GL merge N=2, small DFL rounds)
+    (2, "f32", 32768), (4, "f32", 32768), (6, "f32", 32768), (8, "f32", 32768), (4, "bf16", 32768),
+    (7, "bf16", 32768)])
+def test_occupancy_capped_tiled_passes_every_element(n, dtype, tile_bytes):
+    """The occupancy-capped launches (vec_wgs_cap: passes of 2-16 peers over >= 256 MiB of input
+    get dynamic LDS so only W workgroups fit a CU) compute exactly what the uncapped kernel does: n
+    peers of just over 256 MiB / n of input each, 16 and 32 KiB tiles, Dirichlet weights, a ragged
+    tail of several tiles plus a partial one — every element against the C oracle."""
     from accdfl_amd import _lib
 
     es = 4 if dtype == "f32" else 2
-    numel = (256 << 20) // (n * es) + 12_345  # past the cap's 256 MiB threshold, odd tail
+    tile = tile_bytes // es
+    # past the cap's 256 MiB threshold; the last 3 tiles + 12 345 elements are the ragged tail
+    numel = (256 << 20) // (n * es) // tile * tile + 3 * tile + 12_345
     code = _lib.DLA_F32 if dtype == "f32" else _lib.DLA_BF16
-    tile = 16384 // es
     slab = _slab(n, numel, dtype, 9100 + n)
     buf = _tiled(slab, n, numel, tile)
     host = slab[:, :numel].cpu()

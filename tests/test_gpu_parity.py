@@ -881,7 +881,7 @@ def _tiled_slab(peers, tile_elems, dtype):
 @pytest.mark.parametrize("dtype", ["f32", "bf16", "f16"])
 @pytest.mark.parametrize("n", [1, 3, 7, 8, 16, 31, 33, 130])
 @pytest.mark.parametrize("numel", [5, 4097, 300_007, 4096 * 9 + 3])
-@pytest.mark.parametrize("tile_bytes", [16, 1024, 4096, 16384])
+@pytest.mark.parametrize("tile_bytes", [16, 1024, 4096, 16384, 32768])
 def test_tiled_slab_bit_exact(dtype, n, numel, tile_bytes):
     """dla_wsum_slab_tiled (tile-interleaved PeerSlab layout): every kernel form, ragged tails
     (tiled addressing in the tail workgroup too), multi-pass peer counts, last rounds split into

@@ -131,24 +131,42 @@ class _ConvBN(nn.Module):
             self.bn.num_batches_tracked.fill_(seed)
 
 
+class _Tied(nn.Module):
+    """A module whose parameter is listed once by parameters() but under two state-dict keys."""
+
+    def __init__(self, seed, dtype):
+        super().__init__()
+        torch.manual_seed(seed)
+        self.enc = nn.Linear(300, 400).to(dtype)
+        self.dec = nn.Linear(400, 300, bias=False).to(dtype)
+        self.dec.weight = nn.Parameter(self.enc.weight.detach().t().contiguous())
+        self.head = nn.Module()
+        self.head.weight = self.enc.weight  # alias: state_dict lists it as enc.weight and head.weight
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("peers_as", ["wire", "modules"])
+@pytest.mark.parametrize("peers_as", ["wire", "modules", "device_modules", "tied"])
 def test_aggregate_serialized_straight_from_hbm(dtype, peers_as):
     """VERDICT r02 missing 4: aggregate_serialized copies the averaged parameters from HBM straight
     into the payload (wire.DeviceSource), without the result module; the payload decodes — with the
     reference's own pickle.loads too — to exactly serialize_model(aggregate_trained_models()): the
-    same keys in order, every parameter bit for bit, the first arrival's buffers."""
+    same keys in order, the same devices, every parameter bit for bit, the first arrival's buffers.
+    ADVICE r03: module peers already in HBM (the payload keeps their tensors' device) and tied
+    parameters (every alias key carries the average)."""
     from types import SimpleNamespace
 
     from accdfl_amd.core import wire
     from accdfl_amd.core.gradient_aggregation import GradientAggregationMethod
     from accdfl_amd.core.model_manager import DeviceModelManager
 
-    models = [_ConvBN(k + 1, dtype) for k in range(5)]
+    mk = _Tied if peers_as == "tied" else _ConvBN
+    models = [mk(k + 1, dtype) for k in range(5)]
+    if peers_as == "device_modules":
+        models = [m.cuda() for m in models]
     w = [float(x) for x in np.random.default_rng(7).dirichlet(np.ones(5))]
     mm = DeviceModelManager(None, SimpleNamespace(gradient_aggregation=GradientAggregationMethod.FEDAVG),
-                            template=_ConvBN(0, dtype), capacity=5)
+                            template=mk(0, dtype), capacity=5)
     for k, m in enumerate(models):
         if peers_as == "wire":
             mm.process_incoming_serialized(b"p%d" % k, wire.payload_blocks(wire.serialize_model(m), 60_000))
@@ -156,13 +174,26 @@ def test_aggregate_serialized_straight_from_hbm(dtype, peers_as):
             mm.process_incoming_trained_model(b"p%d" % k, m)
     assert mm._uniform()
     direct = mm.aggregate_serialized(w)
+    if peers_as == "device_modules":
+        want = pickle.loads(wire.serialize_model(mm.aggregate_trained_models(w)))
+        got = pickle.loads(direct)
+        assert list(got.keys()) == list(want.keys())
+        for k in want:
+            assert got[k].device == want[k].device, k
+            assert torch.equal(got[k].cpu().view(-1).view(torch.uint8), want[k].cpu().view(-1).view(torch.uint8)), k
+        return
     want = wire.loads_state_dict(wire.serialize_model(mm.aggregate_trained_models(w)))
     for got in (wire.loads_state_dict(direct), pickle.loads(direct)):
         assert list(got.keys()) == list(want.keys())
         for k in want:
             assert got[k].dtype == want[k].dtype and got[k].shape == want[k].shape, k
             assert torch.equal(got[k].view(-1).view(torch.uint8), want[k].view(-1).view(torch.uint8)), k
-    assert torch.equal(wire.loads_state_dict(direct)["bn.running_mean"], models[0].bn.running_mean)
+    if peers_as == "tied":
+        got = wire.loads_state_dict(direct)
+        assert torch.equal(got["head.weight"], got["enc.weight"])
+        assert not torch.equal(got["enc.weight"], models[0].enc.weight.detach())  # the average, not peer 0's
+    else:
+        assert torch.equal(wire.loads_state_dict(direct)["bn.running_mean"], models[0].bn.running_mean)
 
 
 @pytest.mark.gpu
