@@ -1502,6 +1502,22 @@ def strong_line(legs, name, rank, world, device, steps, warmup):
         ref = wsum.wsum(list(full), w)
         del full
         torch.cuda.empty_cache()
+    one_gpu_s = None
+    if world > 1 and rank == 0:
+        # the same whole model reduced on ONE GPU in the same run (rank 0's, the other GPUs idle), laid
+        # out and rotated as the N = 1 line does it: the in-run reference of the strong speedup
+        pw = max(128, (params + 127) // 128 * 128)
+        wcopies = 1 if (n + 1) * pw * es >= _ROTATE_BYTES else min(64, -(-_ROTATE_BYTES // ((n + 1) * pw * es)))
+        whole = [SlabInput(n, params, dt, device, 1000 + 131 * c, w) for c in range(wcopies)]
+        wctr = [0]
+
+        def step_whole():
+            whole[wctr[0] % len(whole)].launch(torch.cuda.current_stream().cuda_stream)
+            wctr[0] += 1
+        wall1, _ = time_kernel(step_whole, steps, warmup, 1)
+        one_gpu_s = wall1 / steps
+        del whole
+        torch.cuda.empty_cache()
     inputs = [SlabInput(n, m, dt, device, 1000 + 131 * c + 7 * rank, w) for c in range(copies)] if m else []
     sp = torch.cuda.current_stream().cuda_stream
     ctr = [0]
@@ -1542,6 +1558,11 @@ def strong_line(legs, name, rank, world, device, steps, warmup):
         row["with_allgather_value"] = round(total / (wall / steps + wall_g / 10) / 1e9, 2)
         if rank == 0:
             row["parity_ok"] = same_bits(full.to(device), ref)
+            row["one_gpu_ms_per_step"] = round(one_gpu_s * 1e3, 5)
+            row["one_gpu_value"] = round(total / one_gpu_s / 1e9, 2)
+            row["speedup_vs_one_gpu"] = round(one_gpu_s / (wall / steps), 3)
+            row["efficiency"] = round(one_gpu_s / (wall / steps) / world, 3)
+            row["speedup_with_allgather"] = round(one_gpu_s / (wall / steps + wall_g / 10), 3)
     del inputs
     torch.cuda.empty_cache()
     return row
@@ -1579,8 +1600,34 @@ def dry_run(args, rank, world, cpu_group):
         want = [_rank_content(r, length, torch.float32, torch.device("cpu")) for r in range(world)]
         return {"elems_per_rank": length, "parity_ok": all(same_bits(a, b) for a, b in zip(got, want))}
 
+    def strong_gather(L, name, scale=64):
+        # the strong line's exchange without a GPU: every rank's bucket of the fixed model (1/scale of
+        # its parameters, same split rule), filled with rank-seeded content, all-gathered over gloo and
+        # checked element for element against the whole model rebuilt from the seeds
+        n_, params, dts = STRONG[name]
+        small = max(1, params // scale)
+        bounds = bucket_bounds(small, world, 256 // (4 if dts == "f32" else 2))
+        s_, e_ = bounds[rank]
+        mine = _rank_content(rank, max(e_ - s_, 0), torch.float32, torch.device("cpu"))
+        L.go()
+        t0 = time.perf_counter()
+        got = gather_all(mine, max(e - s for s, e in bounds), torch.device("cpu")) if world > 1 else [mine]
+        ms = (time.perf_counter() - t0) * 1e3
+        L.settled()
+        ok = all(same_bits(g[: e - s], _rank_content(r, e - s, torch.float32, torch.device("cpu")))
+                 for r, (g, (s, e)) in enumerate(zip(got, bounds)))
+        return {"buckets": world, "params_scaled": small, "allgather_ms_gloo": round(ms, 3), "parity_ok": ok,
+                "value": None, "speedup_vs_one_gpu": None, "efficiency": None}
+
     rows = {"rendezvous": legs.run("rendezvous", rendezvous), "gloo_allgather": legs.run("gloo_allgather",
                                                                                           gloo_allgather)}
+    strong = {"scaling": "strong", "n_gpus": world, "dry_run": "bucket split + gloo all-gather of scaled models; "
+                                                               "no GPU, so no rates"}
+    for key, name in (("north_star", "north star, 8 peers x 25 M f32"),
+                      ("configs3_resnet8", "configs[3'] CIFAR-10 ResNet-8, 64 peers"),
+                      ("configs4_resnet34_bf16", "configs[4] google_speech ResNet-34, 128 peers, bf16")):
+        strong[key] = legs.run("strong: " + name, strong_gather, name)
+    result["strong_headline"] = strong
     result["buckets"] = rows["rendezvous"].pop("buckets", None)
     result["legs"] = rows
     result["legs_failed"] = legs.failed
@@ -1914,6 +1961,20 @@ def main():
             if world > 1:
                 parity["strong: " + name] = lines[name].get("parity_ok")
         result["strong_scaling"] = {"scaling": "strong", "lines": lines}
+        # BASELINE's fixed-model multi-GPU configs as top-level figures: the north star
+        # split N ways, configs[3'] (64 ResNet-8 models; configs[3] names 4 GPUs) and configs[4] (128
+        # ResNet-34 bf16; 8 GPUs), each against the same model on one GPU of this run
+        strong = result["strong_headline"] = {"scaling": "strong", "n_gpus": world}
+        for key, name in (("north_star", "north star, 8 peers x 25 M f32"),
+                          ("configs3_resnet8", "configs[3'] CIFAR-10 ResNet-8, 64 peers"),
+                          ("configs4_resnet34_bf16", "configs[4] google_speech ResNet-34, 128 peers, bf16")):
+            ln = lines.get(name) or {}
+            strong[key] = {k: ln.get(k) for k in ("value", "ms_per_step", "one_gpu_value", "speedup_vs_one_gpu",
+                                                  "efficiency", "allgather_ms", "with_allgather_value",
+                                                  "speedup_with_allgather", "parity_ok", "skipped", "error")
+                           if k in ln}
+            if world == 1 and "value" in ln:
+                strong[key].update(one_gpu_value=ln["value"], speedup_vs_one_gpu=1.0, efficiency=1.0)
     if world > 1 and not args.no_collectives:
         coll_p = args.coll_params or (p if dist.get_backend() == "nccl" else min(p, 1 << 21))
         coll = result["collectives"] = {}

@@ -95,3 +95,20 @@ def test_rank_count_mismatch_fails_loudly():
                        capture_output=True, text=True, timeout=240, env=e, cwd=ROOT)
     assert p.returncode != 0
     assert "process group has 1 rank" in p.stderr
+
+
+def test_four_ranks_report_the_fixed_model_strong_lines():
+    """at N > 1 the line carries BASELINE's fixed-model multi-GPU configs as
+    top-level ``strong_headline`` rows (north star, configs[3'] ResNet-8 x 64, configs[4] ResNet-34 x 128
+    bf16), each with its own parity flag agreed by every rank.  Without a GPU the dry run splits each
+    model (scaled) into 4 buckets and checks the gloo all-gather that reassembles it; the GPU run fills
+    value / speedup_vs_one_gpu / efficiency / allgather_ms on the same keys."""
+    p, res = _run("--gpus", "4", "--dist-backend", "gloo", "--dry-run")
+    assert p.returncode == 0, p.stderr[-2000:]
+    sh = res["strong_headline"]
+    assert sh["n_gpus"] == 4 and sh["scaling"] == "strong"
+    for key in ("north_star", "configs3_resnet8", "configs4_resnet34_bf16"):
+        row = sh[key]
+        assert row["parity_ok"] is True and row["buckets"] == 4, (key, row)
+        assert {"value", "speedup_vs_one_gpu", "efficiency"} <= set(row)
+    assert res["legs_failed"] == []
