@@ -1,0 +1,25 @@
+#!/bin/bash
+# r04a: first GPU pass of the round-4 tree (dla_slab_stage 2D staging, the occupancy-cap rule, batched
+# device-round result, DFL phase split): the GPU suite + smoke, the default N=1 bench, the copy probe
+# (2D vs contiguous H2D), the DFL round phase split, and the rocprofv3 trace + FETCH/WRITE of the headline.
+set -o pipefail
+export TMPDIR=/tmp
+out=gpurun_out/r04a
+mkdir -p $out
+run() {
+  local t=$1; shift
+  echo "$(date +%T) start: $*" >> $out/steps.log
+  timeout -k 10 "$t" "$@"
+  local rc=$?
+  echo "$(date +%T) rc=$rc: $*" >> $out/steps.log
+  case $rc in 124|137|134|139) exit $rc;; esac
+  return 0
+}
+run 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $out/gpu_tests.log 2>&1
+run 120 python -u -c "import __graft_entry__ as g; g.smoke()" > $out/smoke.log 2>&1
+run 900 python -u bench.py > $out/bench.log 2>&1
+run 300 python -u profiles/r04_copy_probe.py > $out/copy_probe.log 2>&1
+run 300 python -u profiles/r04_dfl_phases.py > $out/dfl_phases.log 2>&1
+run 1000 bash profiles/collect.sh r04a --steps 20 --warmup 5 --no-cpu-baseline --no-host-inclusive --no-small
+cp gpurun_out/prof_r04a/summary/* gpurun_out/prof_r04a/trace.log $out/ 2>/dev/null
+rm -rf gpurun_out/prof_r04a
