@@ -27,7 +27,7 @@ LIB_PATH = os.environ.get("DLAGG_LIB", os.path.join(PKG_ROOT, "lib",
 
 # dtype codes (include/dlagg.h)
 DLA_F32, DLA_BF16, DLA_F16, DLA_F64 = 0, 1, 2, 3
-ABI_VERSION = 10
+ABI_VERSION = 11
 
 HIPCC_FLAGS = [
     "--offload-arch=gfx950",
@@ -70,6 +70,7 @@ EXPORTED = (
     "dla_wsum_multi_table_bytes",
     "dla_wsum_multi_table",
     "dla_slab_stage",
+    "dla_host_in_place_rounds",
 )
 
 
@@ -325,6 +326,8 @@ class _Lib:
         so.dla_slab_stage.argtypes = [ctypes.c_int, vp, ctypes.c_int64, ctypes.c_int64, ctypes.c_int, ctypes.c_int64,
                                       vp, ctypes.c_int64, vp]
         so.dla_slab_stage.restype = ctypes.c_int
+        so.dla_host_in_place_rounds.argtypes = []
+        so.dla_host_in_place_rounds.restype = ctypes.c_int64
         so.dla_plan_destroy.argtypes = [vp]
         so.dla_plan_destroy.restype = None
         v = so.dla_version()
@@ -599,6 +602,11 @@ def slab_stage(dtype_code: int, base_ptr: int, tile_elems: int, slab_rows: int, 
     L = lib()
     L.check(L.so.dla_slab_stage(dtype_code, base_ptr, tile_elems, slab_rows, row, dst_elem, src_ptr, n_elems,
                                 stream_ptr), "dla_slab_stage")
+
+
+def host_in_place_rounds() -> int:
+    """dla_host_in_place_rounds: host rounds whose page-locked peer rows the kernel read in place."""
+    return int(lib().so.dla_host_in_place_rounds())
 
 
 def slab_tile_elems(dtype_code: int, slab_rows: int, n_elems: int) -> int:

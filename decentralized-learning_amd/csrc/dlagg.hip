@@ -35,6 +35,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdint>
 #include <cstdio>
@@ -1967,6 +1968,46 @@ bool is_device_ptr(const void* p) {
   return ok;
 }
 
+// Page-locked host memory mapped into the device address space at the same address (hipHostMalloc,
+// torch pin_memory): a kernel can read / write it across PCIe through the host pointer itself.
+bool is_mapped_host_ptr(const void* p) {
+  hipPointerAttribute_t a;
+  const bool ok = hipPointerGetAttributes(&a, p) == hipSuccess && a.type == hipMemoryTypeHost && a.devicePointer == p;
+  if (!ok) (void)hipGetLastError();
+  return ok;
+}
+
+std::atomic<int64_t> g_host_in_place{0};  // host rounds whose peers the kernel read in place (dla_host_in_place_rounds)
+
+// Peers whose flat parameter vectors are page-locked ROWS (a model decoded into a
+// page-locked ingress buffer, DeviceModelManager's EVA gather, holds its tensors back to back in one
+// pinned row): true when, for every peer k, every non-empty tensor t sits at row_k + start[t] bytes,
+// row_k + begin is 16-byte aligned, and the row's bytes [begin, end) are page-locked and device-mapped.
+// rows[k] then holds row_k (the address of flat element 0).  The host path lets the kernel read such
+// rows across PCIe where they are — no pack into staging, no staging DMA (the kernel's own PCIe reads
+// run at the DMA rate on this link, 53.9-54.8 GB/s).  The first peer that does not
+// qualify ends the check (the reference's pageable peers cost one pointer query).
+bool mapped_peer_rows(int es, int n_peers, int n_tensors, const void* const* tensors, const int64_t* start,
+                      int64_t begin, int64_t end, std::vector<const char*>& rows) {
+  rows.assign(n_peers, nullptr);
+  for (int k = 0; k < n_peers; ++k) {
+    const char* base = nullptr;
+    for (int t = 0; t < n_tensors; ++t) {
+      if (start[t + 1] == start[t]) continue;
+      const char* b = static_cast<const char*>(tensors[static_cast<size_t>(k) * n_tensors + t]) - start[t] * es;
+      if (!base) {
+        base = b;
+      } else if (b != base) {
+        return false;
+      }
+    }
+    if (!base || (reinterpret_cast<uintptr_t>(base + begin * es) & 15u)) return false;
+    if (!is_mapped_host_ptr(base + begin * es) || !is_mapped_host_ptr(base + end * es - 1)) return false;
+    rows[k] = base;
+  }
+  return true;
+}
+
 // Let `dev` read / write memory owned by `owner` (caller holds g_shard_mu; device set to dev).
 hipError_t ensure_peer_access(int dev, int owner) {
   if (dev == owner || owner < 0 || g_peer_enabled.count({dev, owner})) return hipSuccess;
@@ -2510,6 +2551,16 @@ int dla_host_round_start(int dtype, int n_peers, int n_tensors, const void* cons
     if (!tensors[i] && numels[i % n_tensors] > 0)
       return fail(DLA_E_INVALID, "dla_host_round_start: null tensor pointer at " + std::to_string(i));
   if (total == 0) return DLA_OK;
+  {  // peers that already are page-locked rows: the kernel reads them where they are (no pack)
+    std::vector<int64_t> start(n_tensors + 1, 0);
+    for (int t = 0; t < n_tensors; ++t) start[t + 1] = start[t] + numels[t];
+    std::vector<const char*> in_place;
+    if (mapped_peer_rows(es, n_peers, n_tensors, tensors, start.data(), 0, total, in_place)) {
+      g_host_in_place.fetch_add(1, std::memory_order_relaxed);
+      std::vector<const void*> ptrs(in_place.begin(), in_place.end());
+      return wsum_impl(dtype, ptrs.data(), weights, n_peers, total, result, stream, nullptr);
+    }
+  }
   // pack: tensor t of peer k -> row k at the tensor's flat offset (the zip order of fedavg.py:24)
   std::vector<void*> dsts(static_cast<size_t>(n_peers) * n_tensors);
   std::vector<const void*> srcs(dsts.size());
@@ -2609,6 +2660,12 @@ int host_reduce_impl(int dtype, int n_peers, int n_tensors, const void* const* t
     return fail(DLA_E_INVALID, "dla_host_reduce: d_stage / d_out must be device memory");
   const hipStream_t cs_ = static_cast<hipStream_t>(stream);
   const hipStream_t xs = static_cast<hipStream_t>(copy_stream);
+  // Page-locked peer rows are read in place by the reduce (mapped_peer_rows: no pack, no H2D); its
+  // output then goes straight into the page-locked h_out across PCIe when that is device-mapped too.
+  std::vector<const char*> in_place;
+  const bool mapped = mapped_peer_rows(es, n_peers, n_tensors, tensors, start.data(), begin, end, in_place);
+  const bool out_mapped = mapped && is_mapped_host_ptr(h_out);
+  if (mapped) g_host_in_place.fetch_add(1, std::memory_order_relaxed);
   Events ev;  // h2d[2], red[2], d2h[2]
   hipError_t e = ev.create();
   if (e != hipSuccess) return fail(static_cast<int>(e), std::string("dla_host_reduce: ") + hipGetErrorString(e));
@@ -2711,6 +2768,23 @@ int host_reduce_impl(int dtype, int n_peers, int n_tensors, const void* const* t
     char* ds = static_cast<char*>(d_stage) + buf * buf_bytes;
     char* dout = static_cast<char*>(d_out) + buf * row_bytes;
     char* hout = static_cast<char*>(h_out) + buf * row_bytes;
+    if (mapped) {
+      // the reduce reads chunk c of every peer's page-locked row across PCIe; h_out[buf] is free again
+      // (chunk c-2's unpack ran on this thread during the previous iteration)
+      for (int k = 0; k < n_peers; ++k) rows[k] = in_place[k] + c0 * es;
+      const int rc = wsum_impl(dtype, rows.data(), weights, n_peers, m, out_mapped ? hout : dout, stream, nullptr);
+      if (rc != DLA_OK) {
+        (void)hipStreamSynchronize(cs_);
+        return rc;
+      }
+      if (!out_mapped && !check(hipMemcpyAsync(hout, dout, m * es, hipMemcpyDeviceToHost, cs_), "D2H")) break;
+      if (!check(hipEventRecord(d2h[buf], cs_), "record")) break;
+      const auto t3 = clk::now();
+      if (c == 0) t_first = secs(t_start, t3);
+      if (c >= 1) unpack(c - 1, 1);  // overlaps chunk c's reduce
+      t_issue += secs(t0, t3), t_unpack += secs(t3, clk::now());
+      continue;
+    }
     // pack chunk c of every peer into row k of staging buffer `buf`, once the H2D of chunk c-2 has read it
     if (c >= 2 && !check(hipEventSynchronize(h2d[buf]), "H2D")) break;
     const auto t1 = clk::now();
@@ -2762,9 +2836,10 @@ int host_reduce_impl(int dtype, int n_peers, int n_tensors, const void* const* t
   if (e == hipSuccess) unpack(n_chunks - 1, 4);  // nothing left to overlap: spread it
   if (stats)
     std::fprintf(stderr,
-                 "dla_host_reduce: %d peers x %lld elems, %lld chunks of <= %lld: total %.2f ms, first pack %.2f, "
+                 "dla_host_reduce%s: %d peers x %lld elems, %lld chunks of <= %lld: total %.2f ms, first pack %.2f, "
                  "wait-h2d %.2f, pack %.2f (%.1f GB/s), issue %.2f, unpack+wait-d2h %.2f, last unpack %.2f\n",
-                 n_peers, static_cast<long long>(end - begin), static_cast<long long>(n_chunks),
+                 mapped ? " (peers read in place)" : "", n_peers, static_cast<long long>(end - begin),
+                 static_cast<long long>(n_chunks),
                  static_cast<long long>(chunk_elems), secs(t_start, clk::now()) * 1e3, t_first * 1e3, t_wait * 1e3,
                  t_pack * 1e3, t_pack > 0 ? double(end - begin) * es * n_peers / t_pack / 1e9 : 0.0, t_issue * 1e3,
                  t_unpack * 1e3, secs(t_loop, clk::now()) * 1e3);
@@ -2777,6 +2852,8 @@ int host_reduce_impl(int dtype, int n_peers, int n_tensors, const void* const* t
   return DLA_OK;
 }
 }  // namespace
+
+int64_t dla_host_in_place_rounds(void) { return g_host_in_place.load(std::memory_order_relaxed); }
 
 int dla_host_reduce(int dtype, int n_peers, int n_tensors, const void* const* tensors, const int64_t* numels,
                     const double* weights, void* const* outs, int64_t begin, int64_t end, int64_t chunk_elems,

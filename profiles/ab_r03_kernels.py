@@ -60,6 +60,9 @@ def main():
     ap.add_argument("--grids", default="0")
     ap.add_argument("--ns-tiles", default="", help="extra tile sizes (bytes) for the north star, tree build")
     ap.add_argument("--variants", default="", help="extra tree legs with these launch variants (e.g. 8,12,28)")
+    ap.add_argument("--auto-tile", action="store_true", help="tile every shape as PeerSlab does "
+                                                                "(dla_slab_tile_elems) instead of its fixed tile")
+    ap.add_argument("--no-ldsdma", action="store_true", help="skip the LDS-DMA probe legs of the north star")
     ap.add_argument("--rows", default="", help="also time the peers as separate row-major buffers: default + "
                                                "these dla_wsum_ex variants (e.g. 9,12)")
     args = ap.parse_args()
@@ -70,9 +73,10 @@ def main():
     libs = {"tree": bind_tiled(_lib.lib().so)}
     if args.base and os.path.exists(args.base):
         libs["base"] = bind_tiled(ctypes.CDLL(os.path.abspath(args.base)))
-    probe = ctypes.CDLL(_lib.build_probe())
-    probe.dlp_ldsdma_tiled8.argtypes = [vp, ctypes.POINTER(ctypes.c_float), i64, vp, ctypes.c_int, ctypes.c_int, vp]
-    probe.dlp_ldsdma_tiled8.restype = ctypes.c_int
+    probe = None if args.no_ldsdma else ctypes.CDLL(_lib.build_probe())
+    if probe is not None:
+        probe.dlp_ldsdma_tiled8.argtypes = [vp, ctypes.POINTER(ctypes.c_float), i64, vp, ctypes.c_int, ctypes.c_int, vp]
+        probe.dlp_ldsdma_tiled8.restype = ctypes.c_int
     shapes = {
         "ns": ("north star 8 x 25 M f32", 8, 25_000_000, torch.float32, 16384),
         "c4share": ("configs[4] share 128 x 2 662 045 bf16", 128, 2_662_045, torch.bfloat16, 4096),
@@ -101,6 +105,9 @@ def main():
         name, n, p, dt, tile_b = shapes[key]
         es = torch.tensor([], dtype=dt).element_size()
         te = tile_b // es
+        if args.auto_tile:
+            te = _lib.slab_tile_elems({torch.float32: 0, torch.bfloat16: 1}[dt], n, p)
+            name += " (%d KiB tiles)" % (te * es >> 10)
         n_t = -(-p // te)
         slab = torch.empty(n_t * n * te, dtype=dt, device=dev)
         slab.normal_(0, 0.05)
@@ -164,7 +171,7 @@ def main():
                     if rc != 0:
                         raise RuntimeError("dla_wsum_slab_tiled rc=%d" % rc)
                 legs[lname] = fn
-        if key == "ns":
+        if key == "ns" and not args.no_ldsdma:
             w8 = (ctypes.c_float * 8)(*[float(torch.tensor(x, dtype=torch.float32)) for x in w])
             for s in [int(x) for x in args.stages.split(",") if x]:
                 for gr in [int(x) for x in args.grids.split(",")]:

@@ -2,6 +2,9 @@
 dla_wsum_slab_tiled per shape from the library at --lib (default: the tree's), after a short
 settle.  Shapes as profiles/ab_r03_kernels.py: ns (8 x 25 M f32, 16 KiB tiles), c4share
 (128 x 2 662 045 bf16, 4 KiB tiles), c4whole (128 x 21 296 355 bf16, 4 KiB).
+Device-module shapes (r04, VERDICT r03 next 3: wsum_multi_vec_kernel's counters): r34x16 / r34x128 —
+16 / 128 google_speech ResNet-34 bf16 models as separate device tensors (the reference layout,
+tests/golden/layouts.json) through wsum_multi_ptrs (dla_wsum_multi_table, one launch per pass).
 Usage: rocprofv3 --pmc ... -- python3 profiles/pmc_driver.py [--lib PATH] ns,c4share"""
 import argparse
 import ctypes
@@ -20,6 +23,35 @@ SHAPES = {"ns": (8, 25_000_000, torch.float32, 16384), "c4share": (128, 2_662_04
           "c4whole": (128, 21_296_355, torch.bfloat16, 4096)}
 
 
+MODULE_SHAPES = {"r34x16": ("google_speech_resnet34", 16), "r34x128": ("google_speech_resnet34", 128)}
+
+
+def module_round(key, reps, dev):
+    import json
+
+    import numpy as np
+
+    from accdfl_amd.core import wsum
+
+    lay, n = MODULE_SHAPES[key]
+    shapes = [s for _, s, _ in json.load(open(os.path.join(ROOT, "tests", "golden", "layouts.json")))[lay]["params"]]
+    numels = [int(np.prod(s)) if s else 1 for s in shapes]
+    base = torch.randn(sum(numels), device=dev) * 0.05
+    peers = [[t.clone() for t in (base * (1.0 + 0.001 * k)).to(torch.bfloat16).split(numels)] for k in range(n)]
+    outs = [torch.empty(m, dtype=torch.bfloat16, device=dev) for m in numels]
+    ptrs = (ctypes.c_void_p * (n * len(numels)))(*[peers[k][t].data_ptr() for t in range(len(numels))
+                                                   for k in range(n)])
+    out_p = (ctypes.c_void_p * len(numels))(*[o.data_ptr() for o in outs])
+    nums = (ctypes.c_int64 * len(numels))(*numels)
+    w = [float(x) for x in np.random.default_rng(n).dirichlet(np.ones(n))]
+    for _ in range(reps):
+        wsum.wsum_multi_ptrs(torch.bfloat16, ptrs, out_p, nums, w, dev)
+    torch.cuda.synchronize()
+    print("%s: %d launches (%d tensors x %d peers)" % (key, reps, len(numels), n), flush=True)
+    del peers, outs
+    torch.cuda.empty_cache()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("shapes")
@@ -30,6 +62,9 @@ def main():
     so = bind_tiled(ctypes.CDLL(os.path.abspath(args.lib)) if args.lib else _lib.lib().so)
     sp = torch.cuda.current_stream(dev).cuda_stream
     for key in args.shapes.split(","):
+        if key in MODULE_SHAPES:
+            module_round(key, args.reps, dev)
+            continue
         n, p, dt, tile_b = SHAPES[key]
         es = torch.tensor([], dtype=dt).element_size()
         te = tile_b // es

@@ -23,3 +23,13 @@ run 300 python -u profiles/r04_dfl_phases.py > $out/dfl_phases.log 2>&1
 run 1000 bash profiles/collect.sh r04a --steps 20 --warmup 5 --no-cpu-baseline --no-host-inclusive --no-small
 cp gpurun_out/prof_r04a/summary/* gpurun_out/prof_r04a/trace.log $out/ 2>/dev/null
 rm -rf gpurun_out/prof_r04a
+# wsum_multi_vec_kernel counters: 16 x ResNet-34 bf16 device modules, one launch per call
+P1="SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_VMEM_RD SQ_WAIT_INST_ANY SQ_WAIT_ANY GRBM_GUI_ACTIVE GRBM_COUNT"
+P2="SQ_LEVEL_WAVES SQ_ACTIVE_INST_ANY SQ_BUSY_CU_CYCLES SQ_INSTS_SALU SQ_INST_LEVEL_VMEM SQ_INSTS_SMEM SQ_INSTS_VMEM_WR SQ_CYCLES"
+run 120 rocprofv3 --pmc $P1 --output-format csv -d $out/pmc_p1 -o run -- python3 profiles/pmc_driver.py r34x16,r34x128,ns > $out/pmc_p1.log 2>&1
+run 120 rocprofv3 --pmc $P2 --output-format csv -d $out/pmc_p2 -o run -- python3 profiles/pmc_driver.py r34x16,r34x128,ns > $out/pmc_p2.log 2>&1
+run 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $out/pmc_fetch -o run -- python3 profiles/pmc_driver.py r34x16,r34x128,ns > $out/pmc_fetch.log 2>&1
+run 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $out/pmc_write -o run -- python3 profiles/pmc_driver.py r34x16,r34x128,ns > $out/pmc_write.log 2>&1
+run 180 rocprofv3 --kernel-trace --stats --output-format csv -d $out/pmc_trace -o run -- python3 profiles/pmc_driver.py r34x16,r34x128,ns > $out/pmc_trace.log 2>&1
+run 60 python3 profiles/pmc_summary.py $out/pmc_summary.json $out/pmc_p1 $out/pmc_p2 $out/pmc_fetch $out/pmc_write
+rm -rf $out/pmc_p1 $out/pmc_p2 $out/pmc_fetch $out/pmc_write

@@ -601,6 +601,89 @@ def test_native_host_reduce_chunks(dtype, pinned, chunk_bytes):
     assert torch.equal(out.running_mean, models[0].running_mean)
 
 
+@pytest.mark.parametrize("shards", [1, 3])
+@pytest.mark.parametrize("chunk_bytes", [1 << 16, 32 << 20])
+@pytest.mark.parametrize("dtype", ["f32", "bf16", "f16", "f64"])
+def test_page_locked_peer_rows_read_in_place(dtype, chunk_bytes, shards):
+    """Peers whose tensors are views of ONE page-locked row each (a model decoded into a page-locked
+    ingress buffer): dla_host_reduce lets the kernel read the rows in place across PCIe (no pack, no
+    H2D; ABI v11) — bit-exact through chunk boundaries that cut tensors, bucket shards that start mid-row,
+    a ragged last chunk, 11 peers.  Rows that do not qualify (one pageable peer, a row whose base is not
+    16-byte aligned) take the pack path and are bit-exact too; the in-place counter tells them apart."""
+    from torch import nn
+
+    from accdfl_amd import _lib
+    from accdfl_amd.core.gradient_aggregation import fedavg as fa
+
+    shapes = [(700_001,), (3, 333_333), (5,), (1_200_000,), (64, 3, 3, 3), (77,)]
+    numels = [int(np.prod(s)) for s in shapes]
+    g = torch.Generator().manual_seed(53)
+
+    def peer(k, kind):
+        flat = (torch.randn(sum(numels) + 4, generator=g) * 0.05).to(TDT[dtype])
+        if kind == "pinned":
+            flat = flat.pin_memory()
+        elif kind == "pinned_odd":  # base 1 element (2-8 bytes) past a 16-byte boundary
+            flat = flat.pin_memory()[1:]
+        m = nn.Module()
+        m.ps = nn.ParameterList([nn.Parameter(t.view(s)) for t, s in zip(flat[: sum(numels)].split(numels), shapes)])
+        m.register_buffer("running_mean", torch.full((7,), float(k)))
+        return m
+
+    w = [float(x) for x in np.random.default_rng(13).dirichlet(np.ones(11))]
+    old, small = fa._NATIVE_CHUNK_BYTES, fa._SMALL_ROUND_BYTES
+    fa._NATIVE_CHUNK_BYTES = chunk_bytes
+    fa._SMALL_ROUND_BYTES = 0
+    if shards > 1:
+        fa.set_host_devices(["cuda:0"] * shards)
+    try:
+        for kinds, in_place in ((["pinned"] * 11, True), (["pinned"] * 10 + ["pageable"], False),
+                                (["pinned"] * 5 + ["pinned_odd"] + ["pinned"] * 5, False)):
+            models = [peer(k, kind) for k, kind in enumerate(kinds)]
+            before = _lib.host_in_place_rounds()
+            out = fa.FedAvg.aggregate(models, w)
+            used = _lib.host_in_place_rounds() - before
+            assert (used > 0) == in_place, (kinds, used)
+            for i, p in enumerate(out.parameters()):
+                want = fedavg_bits([gc.as_float(_bits(list(m.parameters())[i].detach().reshape(-1), dtype), dtype)
+                                    for m in models], w, dtype)
+                assert same_bits(gc.as_float(_bits(p.detach().reshape(-1), dtype), dtype), want, dtype), (kinds, i)
+            assert torch.equal(out.running_mean, models[0].running_mean)
+    finally:
+        fa._NATIVE_CHUNK_BYTES, fa._SMALL_ROUND_BYTES = old, small
+        fa.set_host_devices([])
+        fa.release_staging()
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+def test_small_round_page_locked_rows_in_place(dtype):
+    """The small-round path (dla_host_round_start: rounds under 96 MB, e.g. the GL merge of N=2) reads
+    page-locked peer rows in place instead of packing them; bit-exact for 2 and 9 peers."""
+    from torch import nn
+
+    from accdfl_amd import _lib
+    from accdfl_amd.core.gradient_aggregation import fedavg as fa
+
+    shapes = [(32, 3, 5, 5), (32,), (64, 32, 5, 5), (64,), (10, 576), (10,)]
+    numels = [int(np.prod(s)) for s in shapes]
+    g = torch.Generator().manual_seed(59)
+    for n in (2, 9):
+        models = []
+        for _ in range(n):
+            flat = (torch.randn(sum(numels), generator=g) * 0.05).to(TDT[dtype]).pin_memory()
+            m = nn.Module()
+            m.ps = nn.ParameterList([nn.Parameter(t.view(s)) for t, s in zip(flat.split(numels), shapes)])
+            models.append(m)
+        w = [float(x) for x in np.random.default_rng(n).dirichlet(np.ones(n))]
+        before = _lib.host_in_place_rounds()
+        out = fa.FedAvg.aggregate(models, w)
+        assert _lib.host_in_place_rounds() > before
+        for i, p in enumerate(out.parameters()):
+            want = fedavg_bits([gc.as_float(_bits(list(m.parameters())[i].detach().reshape(-1), dtype), dtype)
+                                for m in models], w, dtype)
+            assert same_bits(gc.as_float(_bits(p.detach().reshape(-1), dtype), dtype), want, dtype), (n, i)
+
+
 @pytest.mark.parametrize("delay_s", [0.0, 0.02])
 def test_host_reduce_deferred_outputs(delay_s):
     """dla_host_reduce_deferred (ABI v9): the call starts with no outputs; they are published from
