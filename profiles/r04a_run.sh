@@ -33,3 +33,6 @@ run 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $out/pmc_write -o run 
 run 180 rocprofv3 --kernel-trace --stats --output-format csv -d $out/pmc_trace -o run -- python3 profiles/pmc_driver.py r34x16,r34x128,ns > $out/pmc_trace.log 2>&1
 run 60 python3 profiles/pmc_summary.py $out/pmc_summary.json $out/pmc_p1 $out/pmc_p2 $out/pmc_fetch $out/pmc_write
 rm -rf $out/pmc_p1 $out/pmc_p2 $out/pmc_fetch $out/pmc_write
+# occupancy cap: the round-4 rule (product library) against round 3's per-peer-count table (the tuning build with
+# DLA_VEC_CAP_TABLE=1), interleaved, PeerSlab's own tiles (one box of the two-box A/B)
+run 400 env DLA_VEC_CAP_TABLE=1 python -u profiles/ab_r03_kernels.py --base decentralized-learning_amd/lib/libdlagg_tuning.so --auto-tile --no-ldsdma --shapes ns,ns4,n9,ns12,ns16,b8,b16,ns2,ns6,c4share --rounds 5 --reps 20 > $out/cap_ab.log 2>&1
