@@ -36,3 +36,5 @@ rm -rf $out/pmc_p1 $out/pmc_p2 $out/pmc_fetch $out/pmc_write
 # occupancy cap: the round-4 rule (product library) against round 3's per-peer-count table (the tuning build with
 # DLA_VEC_CAP_TABLE=1), interleaved, PeerSlab's own tiles (one box of the two-box A/B)
 run 400 env DLA_VEC_CAP_TABLE=1 python -u profiles/ab_r03_kernels.py --base decentralized-learning_amd/lib/libdlagg_tuning.so --auto-tile --no-ldsdma --shapes ns,ns4,n9,ns12,ns16,b8,b16,ns2,ns6,c4share --rounds 5 --reps 20 > $out/cap_ab.log 2>&1
+# many-tensor table kernel: one block per workgroup against the pipelined 2- / 4-block variant (tuning A/B library)
+run 300 python -u profiles/r04_multi_pipe_ab.py > $out/multi_pipe_ab.log 2>&1
