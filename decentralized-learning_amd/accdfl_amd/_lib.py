@@ -14,6 +14,8 @@ import subprocess
 import threading
 from typing import Optional, Sequence
 
+import numpy as np
+
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))  # decentralized-learning_amd/
 REPO_ROOT = os.path.dirname(PKG_ROOT)
 CSRC = os.path.join(PKG_ROOT, "csrc", "dlagg.hip")
@@ -469,8 +471,15 @@ def host_copy_batch(dst_ptrs: Sequence[int], src_ptrs: Sequence[int], nbytes: Se
     ``streaming``: non-temporal stores (destinations only the GPU reads next)."""
     L = lib()
     m = len(nbytes)
-    rc = L.so.dla_host_copy_batch_ex((ctypes.c_void_p * m)(*dst_ptrs), (ctypes.c_void_p * m)(*src_ptrs),
-                                     (ctypes.c_int64 * m)(*nbytes), m, DLA_COPY_STREAMING if streaming else 0)
+    if isinstance(nbytes, np.ndarray):  # int64 arrays (wire's EVA block gathers): no per-element conversion
+        arrs = [np.ascontiguousarray(a, dtype=np.int64) for a in (dst_ptrs, src_ptrs, nbytes)]
+        vpp = ctypes.POINTER(ctypes.c_void_p)
+        rc = L.so.dla_host_copy_batch_ex(arrs[0].ctypes.data_as(vpp), arrs[1].ctypes.data_as(vpp),
+                                         arrs[2].ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), m,
+                                         DLA_COPY_STREAMING if streaming else 0)
+    else:
+        rc = L.so.dla_host_copy_batch_ex((ctypes.c_void_p * m)(*dst_ptrs), (ctypes.c_void_p * m)(*src_ptrs),
+                                         (ctypes.c_int64 * m)(*nbytes), m, DLA_COPY_STREAMING if streaming else 0)
     if rc != 0:
         L.check(rc, "dla_host_copy_batch")
 

@@ -412,10 +412,10 @@ def _device_round(models: List[nn.Module], weights, layout) -> "nn.Module | None
     outs = (ctypes.c_void_p * len(numels))(*[base + o * esize for o in offs])
     nums = (ctypes.c_int64 * len(numels))(*numels)
     _wsum.wsum_multi_ptrs(dtype, ptrs, outs, nums, weights, device)
-    # while the reduce runs: the result's parameters over `flat`, models[0]'s buffers, the module tree
-    make = torch.Tensor._make_subclass  # what nn.Parameter(data, requires_grad) does for a plain tensor
-    memo = {id(p): make(nn.Parameter, flat.as_strided(p.size(), p.stride(), o), p.requires_grad)
-            for p, o in zip(p0, offs)}
+    # while the reduce runs: the result's parameters over `flat` (nn.Parameter views made natively: what
+    # torch.Tensor._make_subclass(nn.Parameter, flat.as_strided(...), requires_grad) makes), models[0]'s
+    # buffers, the module tree
+    memo = dict(zip(map(id, p0), mod.param_views(flat, p0, offs)))
     _seed_buffers(b0, memo)
     return _clone_value(models[0], memo)
 

@@ -26,7 +26,7 @@ import os
 import pickle
 import threading
 import time
-from typing import Callable, Dict, List, Optional, Sequence
+from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 
@@ -66,14 +66,14 @@ class _BlobUnpickler(pickle.Unpickler):
 
 class _Span:
     """A byte range of a block list (EVA's ``data_list``) that crosses block boundaries, kept
-    as (host address, length) pieces of the blocks — never joined unless asked.  ``owner``
-    keeps the blocks alive."""
+    as (host address, length) pieces of the blocks — int64 arrays, never joined unless asked.
+    ``owner`` keeps the blocks alive."""
     __slots__ = ("addrs", "lens", "n", "owner", "_starts")
 
-    def __init__(self, addrs, lens, owner):
+    def __init__(self, addrs: np.ndarray, lens: np.ndarray, owner):
         self.addrs = addrs
         self.lens = lens
-        self.n = sum(lens)
+        self.n = int(lens.sum())
         self.owner = owner
         self._starts = None
 
@@ -81,17 +81,17 @@ class _Span:
         return self.n
 
     def sub(self, a: int, b: int):
-        """(addresses, lengths) of the pieces covering [a, b) of this span (list slices located
-        by bisection: no per-piece Python work)."""
+        """(addresses, lengths) of the pieces covering [a, b) of this span, as int64 arrays
+        (located by binary search: no per-piece Python work)."""
         if a >= b:
-            return [], []
+            return np.zeros(0, np.int64), np.zeros(0, np.int64)
         if self._starts is None:
-            self._starts = list(itertools.accumulate(self.lens[:-1], initial=0))
+            self._starts = np.concatenate(([0], np.cumsum(self.lens[:-1])))
         st = self._starts
-        i = bisect.bisect_right(st, a) - 1
-        j = bisect.bisect_right(st, b - 1) - 1
-        addrs = self.addrs[i:j + 1]
-        lens = self.lens[i:j + 1]
+        i = int(np.searchsorted(st, a, side="right")) - 1
+        j = int(np.searchsorted(st, b - 1, side="right")) - 1
+        addrs = self.addrs[i:j + 1].copy()
+        lens = self.lens[i:j + 1].copy()
         lens[-1] = b - st[j]
         d = a - st[i]
         addrs[0] += d
@@ -101,7 +101,7 @@ class _Span:
     def read(self, a: int, b: int) -> bytes:
         import ctypes
 
-        return b"".join(ctypes.string_at(q, ln) for q, ln in zip(*self.sub(a, b)))
+        return b"".join(ctypes.string_at(int(q), int(ln)) for q, ln in zip(*self.sub(a, b)))
 
 
 _BYTES_DATA = bytes.__basicsize__ - 1  # CPython: offset of a bytes object's payload
@@ -125,6 +125,32 @@ def _block_address(block) -> int:
     return np.frombuffer(block, dtype=np.uint8).__array_interface__["data"][0]
 
 
+# A 100 MB model is ~1 700 EVA blocks: the per-block bookkeeping (addresses, lengths) comes from one
+# native call (csrc/walk.cpp block_table, a few ns per block) or, without the extension, from C-level
+# map operations; round 3 spent 0.5-0.65 ms per 100 MB peer in Python loops over the blocks (bench.py
+# dfl_round phases, profiles/r04a).
+
+def _block_table(blocks: list) -> Tuple[np.ndarray, np.ndarray]:
+    """(addresses, byte lengths) of every block, as int64 arrays."""
+    from accdfl_amd import _lib
+
+    mod = _lib.walk_module()
+    if mod is not None:
+        return mod.block_table(blocks)
+    lens = np.fromiter(map(len, blocks), dtype=np.int64, count=len(blocks))
+    if _BYTES_ADDR_OK:
+        addrs = np.fromiter(map(id, blocks), dtype=np.int64, count=len(blocks))
+        addrs += _BYTES_DATA
+    else:
+        addrs = np.zeros(len(blocks), dtype=np.int64)
+    if not _BYTES_ADDR_OK or set(map(type, blocks)) != {bytes}:
+        for i, b in enumerate(blocks):
+            if type(b) is not bytes or not _BYTES_ADDR_OK:
+                addrs[i] = _block_address(b)
+                lens[i] = memoryview(b).nbytes
+    return addrs, lens
+
+
 # Gathers into a page-locked ingress buffer (read next by the H2D DMA, not by the CPU) use streaming
 # stores (dla_host_copy_batch_ex, DLA_COPY_STREAMING); ACCDFL_AMD_INGRESS_NT=0 turns them off (A/B).
 _INGRESS_NT = os.environ.get("ACCDFL_AMD_INGRESS_NT", "1") != "0"
@@ -139,11 +165,14 @@ def _gather(addrs, lens, dst: torch.Tensor) -> None:
     memcpy, threaded from 4 MiB: libdlagg's dla_host_copy_batch)."""
     from accdfl_amd import _lib
 
-    if not lens:
+    if not len(lens):
         return
     t0 = time.perf_counter() if GATHER_MS is not None else 0.0
-    dsts = list(itertools.accumulate(lens[:-1], initial=dst.data_ptr()))
-    _lib.host_copy_batch(dsts, addrs, lens, streaming=_INGRESS_NT and sum(lens) >= (4 << 20) and dst.is_pinned())
+    dsts = np.empty(len(lens), dtype=np.int64)
+    dsts[0] = dst.data_ptr()
+    np.cumsum(lens[:-1], out=dsts[1:])
+    dsts[1:] += dsts[0]
+    _lib.host_copy_batch(dsts, addrs, lens, streaming=_INGRESS_NT and int(lens.sum()) >= (4 << 20) and dst.is_pinned())
     if GATHER_MS is not None:
         GATHER_MS.append((time.perf_counter() - t0) * 1e3)
 
@@ -247,18 +276,19 @@ class _BlockReader:
     a long read's pieces are list slices, so no Python code runs per block."""
 
     def __init__(self, blocks):
-        self.blocks = []
-        self.lens = []
-        for b in blocks:
-            ln = len(b) if type(b) is bytes else memoryview(b).nbytes
-            if ln:
-                self.blocks.append(b)
-                self.lens.append(ln)
-        self.starts = list(itertools.accumulate(self.lens[:-1], initial=0)) if self.lens else []
+        blocks = blocks if type(blocks) is list else list(blocks)
+        addrs, lens = _block_table(blocks)
+        if len(lens) and not lens.all():  # drop empty blocks
+            keep = np.flatnonzero(lens)
+            blocks = [blocks[i] for i in keep.tolist()]
+            addrs, lens = addrs[keep], lens[keep]
+        self.blocks = blocks
+        self.addrs, self.lens_np = addrs, lens
+        self.lens = lens.tolist()
+        self.starts = [0] + np.cumsum(lens[:-1]).tolist() if len(lens) else []
         self.views = [None] * len(self.blocks)
-        self.addrs = None
         self.pos = 0
-        self.n = sum(self.lens)
+        self.n = int(lens.sum())
 
     @property
     def left(self) -> int:
@@ -289,12 +319,8 @@ class _BlockReader:
             pieces += [self._view(q) for q in range(i + 1, j)]
             pieces.append(self._view(j)[:b - st[j]])
             return b"".join(pieces)
-        if self.addrs is None:
-            ok = _BYTES_ADDR_OK
-            self.addrs = [id(x) + _BYTES_DATA if ok and type(x) is bytes else _block_address(x)
-                          for x in self.blocks]
-        addrs = self.addrs[i:j + 1]
-        out_lens = lens[i:j + 1]
+        addrs = self.addrs[i:j + 1].copy()
+        out_lens = self.lens_np[i:j + 1].copy()
         addrs[0] += o
         out_lens[0] -= o
         out_lens[-1] = b - st[j]
@@ -748,23 +774,20 @@ def split_blocks(blocks: Sequence, n: int):
     at ``model_data_len`` (accdfl/dfl/community.py:587-588) with no copy: blocks that fall
     wholly on one side are passed through as they are (so a ``bytes`` block keeps its cheap
     address), the block holding byte n becomes two memoryview slices."""
-    head: List = []
-    tail: List = []
-    off = 0
-    for b in blocks:
-        ln = len(b) if type(b) is bytes else memoryview(b).nbytes
-        if off + ln <= n:
-            head.append(b)
-        elif off >= n:
-            tail.append(b)
-        else:
-            v = memoryview(b).cast("B")
-            head.append(v[:n - off])
-            tail.append(v[n - off:])
-        off += ln
-    if off < n:
-        raise ValueError("split_blocks: the blocks hold %d bytes, fewer than %d" % (off, n))
-    return head, tail
+    blocks = blocks if type(blocks) is list else list(blocks)
+    if n <= 0:
+        return [], blocks
+    lens = _block_table(blocks)[1]
+    ends = np.cumsum(lens)
+    total = int(ends[-1]) if len(ends) else 0
+    if total < n:
+        raise ValueError("split_blocks: the blocks hold %d bytes, fewer than %d" % (total, n))
+    k = int(np.searchsorted(ends, n))  # the first block that ends at or past byte n
+    if int(ends[k]) == n:
+        return blocks[:k + 1], blocks[k + 1:]
+    start = int(ends[k] - lens[k])
+    v = memoryview(blocks[k]).cast("B")
+    return blocks[:k] + [v[:n - start]], [v[n - start:]] + blocks[k + 1:]
 
 
 def payload_blocks(data: bytes, block_size: int) -> List[bytes]:

@@ -36,8 +36,9 @@ def module_round(key, reps, dev):
     lay, n = MODULE_SHAPES[key]
     shapes = [s for _, s, _ in json.load(open(os.path.join(ROOT, "tests", "golden", "layouts.json")))[lay]["params"]]
     numels = [int(np.prod(s)) if s else 1 for s in shapes]
-    base = torch.randn(sum(numels), device=dev) * 0.05
-    peers = [[t.clone() for t in (base * (1.0 + 0.001 * k)).to(torch.bfloat16).split(numels)] for k in range(n)]
+    # separate allocations, uninitialised (no fill kernels: under --pmc every dispatch is serialised and
+    # 14 080 fills would take minutes; the values do not change the reduce's timing or its traffic)
+    peers = [[torch.empty(m, dtype=torch.bfloat16, device=dev) for m in numels] for _ in range(n)]
     outs = [torch.empty(m, dtype=torch.bfloat16, device=dev) for m in numels]
     ptrs = (ctypes.c_void_p * (n * len(numels)))(*[peers[k][t].data_ptr() for t in range(len(numels))
                                                    for k in range(n)])

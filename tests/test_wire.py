@@ -1,6 +1,7 @@
 """Wire format (§8 f1/f3): decoding the reference's serialize_model bytes without
 executing the payload, and producing bytes in the same format."""
 import collections
+import ctypes
 import io
 import json
 import os
@@ -350,6 +351,43 @@ def test_dfl_split_without_copies():
     assert torch.equal(sd2["bias"], m.bias.detach())
     with pytest.raises(ValueError):
         wire.split_blocks([b"abc"], 10)
+
+
+def test_block_table_and_split_edges(monkeypatch):
+    """The per-block bookkeeping (native block_table, or the Python fallback without the extension) on
+    mixed blocks — bytes, empty bytes, memoryview halves, bytearray — and split_blocks at every kind of
+    boundary: 0, inside a block, exactly at a block end, the total; decoding a payload cut into blocks
+    with empty blocks in between still matches the joined bytes."""
+    from accdfl_amd import _lib
+    from accdfl_amd.core import wire
+
+    data = bytes(range(256)) * 40
+    mv = memoryview(data[:1000]).cast("B")
+    blocks = [data[1000:1500], b"", mv[:300], bytearray(data[2000:2100]), mv[300:], data[5000:6000]]
+    want_lens = [500, 0, 300, 100, 700, 1000]
+    joined = b"".join(bytes(b) for b in blocks)
+    for native in (True, False):
+        if not native:
+            monkeypatch.setattr(_lib, "walk_module", lambda: None)
+        elif _lib.walk_module() is None:
+            continue
+        addrs, lens = wire._block_table(blocks)
+        assert lens.tolist() == want_lens
+        for a, ln, b in zip(addrs.tolist(), lens.tolist(), blocks):
+            if ln:
+                assert ctypes.string_at(a, ln) == bytes(b)
+        for n in (0, 1, 499, 500, 800, 900, 1600, len(joined) - 1, len(joined)):
+            head, tail = wire.split_blocks(blocks, n)
+            assert b"".join(bytes(b) for b in head) == joined[:n], n
+            assert b"".join(bytes(b) for b in tail) == joined[n:], n
+        with pytest.raises(ValueError):
+            wire.split_blocks(blocks, len(joined) + 1)
+        m = nn.Linear(64, 33)
+        payload = wire.serialize_model(m)
+        cut = wire.payload_blocks(payload, 97)
+        cut = [x for b in cut for x in (b, b"")]  # empty blocks between every two
+        sd = wire.loads_state_dict(cut, copy=True)
+        assert torch.equal(sd["weight"], m.weight.detach()) and torch.equal(sd["bias"], m.bias.detach())
 
 
 def test_block_list_refuses_foreign_globals():
