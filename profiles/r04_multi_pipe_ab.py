@@ -1,14 +1,17 @@
-"""r04: the many-tensor table kernel (dla_wsum_multi_table, device-resident module rounds) one block of 64
-vectors per workgroup (the product's wsum_multi_vec_kernel) against the software-pipelined variant
-(wsum_multi_pipe_kernel: BLK = 2 or 4 blocks per workgroup, block i+1's loads issued before block i's
-fold; one tensor lookup per BLK blocks) — VERDICT r03 next 3 (16 x ResNet-34 bf16 at 0.68 of peak).
-
-The A/B library is a tuning build (lib/ab/libdlagg_pipe.so, DLA_MULTI_PIPE read per call), loaded with
-ctypes beside nothing else; legs interleave in one process, HIP events on the launch stream, and every
-leg's output is compared bit for bit with the one-block kernel's.  Layouts: the reference models as
+"""r04: A/B legs of the many-tensor table kernel (dla_wsum_multi_table, device-resident module rounds;
+VERDICT r03 next 3: 16 x ResNet-34 bf16 at 0.68 of peak), each leg one setting of a tuning-build
+environment knob read per call:
+  * DLA_MULTI_PIPE=0/2/4 (lib/ab/libdlagg_pipe.so): the one-block kernel against the software-
+    pipelined variant (BLK blocks of 64 vectors per workgroup, block i+1's loads issued before block
+    i's fold; one tensor lookup per BLK blocks);
+  * DLA_MULTI_VW=2/4 (lib/ab/libdlagg_vw.so): 8-byte against 16-byte loads per lane (512 B against
+    1 KiB of each peer per wave).
+Legs interleave in one process, HIP events on the launch stream, and every leg's output is compared
+bit for bit with the first leg's.  Layouts: the reference models as
 separate device tensors (tests/golden/layouts.json), at their BASELINE peer counts where a pass is
 8 / 16 / 32 peers.
-Usage on the GPU box: python profiles/r04_multi_pipe_ab.py [--lib PATH] -> one JSON line per leg."""
+Usage on the GPU box: python profiles/r04_multi_pipe_ab.py [--lib PATH] [--knob DLA_MULTI_VW --values 2,4]
+-> one JSON line per leg."""
 import argparse
 import ctypes
 import json
@@ -35,6 +38,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--lib", default=os.path.join(ROOT, "decentralized-learning_amd", "lib", "ab", "libdlagg_pipe.so"))
     ap.add_argument("--shapes", default="r34x16,r34x32,r8x16,r8x32,femx32,femx8")
+    ap.add_argument("--knob", default="DLA_MULTI_PIPE")
+    ap.add_argument("--values", default="0,2,4")
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--reps", type=int, default=20)
     args = ap.parse_args()
@@ -62,7 +67,8 @@ def main():
         code = 0 if dt == torch.float32 else 1
         es = 4 if dt == torch.float32 else 2
         legs, outs = {}, {}
-        for blk in ("0", "2", "4"):
+        values = args.values.split(",")
+        for blk in values:
             o = [torch.empty(m, dtype=dt, device=dev) for m in numels]
             op = (vp * t_n)(*[x.data_ptr() for x in o])
             th = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
@@ -70,7 +76,7 @@ def main():
             outs[blk] = o
 
             def fn(blk=blk, op=op, th=th, td=td):
-                os.environ["DLA_MULTI_PIPE"] = blk
+                os.environ[args.knob] = blk
                 rc = so.dla_wsum_multi_table(code, t_n, ptrs, op, nums, w, n, th.data_ptr(), td.data_ptr(), sp)
                 if rc != 0:
                     raise RuntimeError("dla_wsum_multi_table rc=%d" % rc)
@@ -94,11 +100,11 @@ def main():
         for b in legs:
             same = all(torch.equal(x.view(torch.int16 if es == 2 else torch.int32),
                                    y.view(torch.int16 if es == 2 else torch.int32))
-                       for x, y in zip(outs[b], outs["0"]))
+                       for x, y in zip(outs[b], outs[values[0]]))
             t = statistics.median(res[b])
-            print(json.dumps({"shape": key, "peers": n, "tensors": t_n, "blocks_per_wg": int(b) or 1,
+            print(json.dumps({"shape": key, "peers": n, "tensors": t_n, args.knob: b,
                               "us": round(t, 2), "min_us": round(min(res[b]), 2), "GB/s": round(byts / t / 1e3, 1),
-                              "frac_8TBs": round(byts / t / 1e3 / 8000, 4), "bit_exact_vs_one_block": same}),
+                              "frac_8TBs": round(byts / t / 1e3 / 8000, 4), "bit_exact_vs_first_leg": same}),
                   flush=True)
         del peers, outs, legs
         torch.cuda.empty_cache()
