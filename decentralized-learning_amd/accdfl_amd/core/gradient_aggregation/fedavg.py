@@ -424,7 +424,14 @@ def _seed_buffers(buffers, memo: dict) -> None:
     """deepcopy of models[0]'s device buffers (fedavg.py:20 copies them, it does not average them) in
     one gather per (device, dtype) group: the copies are views of one fresh allocation each, seeded
     into the deepcopy memo.  Buffers that are not plain dense tensors without grad keep the stock
-    deepcopy."""
+    deepcopy.  The walk extension does it in one native call (walk.cpp buffer_copies)."""
+    mod = _lib.walk_module()
+    if mod is not None:
+        buffers = [b for b in buffers if id(b) not in memo]
+        for b, c in zip(buffers, mod.buffer_copies(buffers)):
+            if c is not None:
+                memo[id(b)] = c
+        return
     groups: Dict[tuple, list] = {}
     for b in buffers:
         if (type(b) is torch.Tensor and b.is_cuda and not b.requires_grad and b.is_contiguous()
@@ -922,8 +929,10 @@ def _clone_value(v, memo: dict):
     if t is dict or t is OrderedDict:
         y = t()
         memo[id(v)] = y
+        get = memo.get
         for k, x in v.items():
-            y[k if type(k) in _ATOMIC else copy.deepcopy(k, memo)] = _clone_value(x, memo)
+            c = get(id(x), memo)  # seeded entries (parameters, buffers) without a call each
+            y[k if type(k) in _ATOMIC else copy.deepcopy(k, memo)] = c if c is not memo else _clone_value(x, memo)
         return y
     if t is set and not v:
         y = set()
@@ -983,7 +992,9 @@ class FedAvg(GradientAggregation):
 
         with torch.no_grad():
             if len(models) > 0:
-                layout = _host_layout(models)
+                # models already on a GPU skip the host-layout attempt (a failed walk of every model)
+                p_first = next(iter(models[0].parameters()), None)
+                layout = _host_layout(models) if p_first is None or not p_first.is_cuda else None
                 if layout is not None:
                     done = _small_round(models, list(weights), layout)
                     if done is None and _HOST_PATH == "native":

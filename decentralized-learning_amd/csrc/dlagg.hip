@@ -1332,7 +1332,9 @@ unsigned vec_lds_pad() {
 // 16: 127.6), 8 x 50 M bf16 130.0 -> 125.1; 4 x 25 M f32 73.6 -> 70.0 (W 26-28; rule 28); 9-15 peers x 25 M
 // f32 (8 + smaller rounds, rule 24) 3.1-4.5 % faster (W 24 within 0.5 % of each count's best); 2, 3, 5, 6
 // and 7 peers (rule 56, 96, 48: at or above the register limit) uncapped, where every cap measured lost.
-// Exceptions, each an interleaved A/B against the rule (profiles/r04c): 16 peers in one round of 16,
+// Exceptions, each an interleaved A/B against the rule: 12 peers (8 + 4) at W = 15, round 3's table value
+// — the rule's 24 read 1.2 % and 0.85 % slower on two boxes (185.98 / 183.79 us, 185.64 / 184.08:
+// profiles/r04c/cap_ab.log, profiles/r04d/cap_ab.log, spread elsewhere <= 0.35 %); 16 peers in one round of 16,
 // and passes of >= 32 peers — register-limited at 16 waves per CU and holding 32 x 512 B per wave — which
 // over >= 1 GiB fold 16 peers per round under W = 8 (32 x 10 M f32 199.3 -> 191.5, 64 x 4.93 M f32 192.2
 // -> 184.3, 128 x 21.3 M bf16 813.8 -> 803.3, profiles/r03ai) and below it run uncapped (configs[4]'s
@@ -1383,6 +1385,7 @@ int vec_wgs_cap(int n_peers, int G, int64_t n_vecs, int natural) {
   if (n_peers >= 32) return in_bytes >= (int64_t{1} << 30) ? 8 : 0;  // exception (see above)
   if (n_peers > 16) return 0;                                        // 17-31 peers: never measured
   if (n_peers == 16 && G == 16) return 10;                           // exception (see above)
+  if (n_peers == 12 && G == 16) return 15;                           // exception (see above)
   int r1 = G;
   if (n_peers < G) {
     r1 = 1;

@@ -27,6 +27,7 @@
 #include <cstdint>
 #include <stdexcept>
 #include <string>
+#include <unordered_map>
 #include <unordered_set>
 #include <vector>
 
@@ -202,6 +203,71 @@ py::list param_views(const at::Tensor& flat, py::list params, const std::vector<
   return out;
 }
 
+// deepcopy of models[0]'s device buffers (fedavg.py:20 copies them, it does not average them) in one
+// gather per (device, dtype): for each entry of `buffers`, a copy that is a view of one fresh allocation
+// per group (at::cat of the group, then views), or None for an entry that is not a plain dense CUDA
+// tensor without grad (the caller deep-copies those) or is alone in its group.  An object listed twice
+// gets one copy (deepcopy's memo).  Replaces a Python pass over every buffer (108 BN buffers of a
+// google_speech ResNet-34: ~0.15 ms per round).
+py::list buffer_copies(py::list buffers) {
+  const py::ssize_t n = PyList_GET_SIZE(buffers.ptr());
+  std::vector<int> group(n, -1);
+  std::vector<std::pair<int, int>> keys;  // (device index, scalar type) of each group
+  std::vector<std::vector<py::ssize_t>> members;
+  std::unordered_map<PyObject*, py::ssize_t> first_of;
+  std::vector<py::ssize_t> alias(n, -1);
+  for (py::ssize_t i = 0; i < n; ++i) {
+    PyObject* o = PyList_GET_ITEM(buffers.ptr(), i);
+    if (Py_TYPE(o) != reinterpret_cast<PyTypeObject*>(THPVariableClass)) continue;
+    auto it = first_of.find(o);
+    if (it != first_of.end()) {
+      alias[i] = it->second;
+      continue;
+    }
+    first_of.emplace(o, i);
+    const at::Tensor& t = THPVariable_Unpack(o);
+    if (!t.is_cuda() || t.requires_grad() || !t.is_contiguous() || !t.has_storage()) continue;
+    const std::pair<int, int> key{t.get_device(), static_cast<int>(t.scalar_type())};
+    size_t g = 0;
+    while (g < keys.size() && keys[g] != key) ++g;
+    if (g == keys.size()) {
+      keys.push_back(key);
+      members.emplace_back();
+    }
+    group[i] = static_cast<int>(g);
+    members[g].push_back(i);
+  }
+  py::list out(n);
+  for (py::ssize_t i = 0; i < n; ++i) PyList_SET_ITEM(out.ptr(), i, py::none().release().ptr());
+  for (const auto& mem : members) {
+    if (mem.size() < 2) continue;
+    std::vector<at::Tensor> flat_in;
+    flat_in.reserve(mem.size());
+    for (py::ssize_t i : mem) flat_in.push_back(THPVariable_Unpack(PyList_GET_ITEM(buffers.ptr(), i)).reshape({-1}));
+    const at::Tensor flat = at::cat(flat_in);
+    int64_t off = 0;
+    for (py::ssize_t i : mem) {
+      const at::Tensor& t = THPVariable_Unpack(PyList_GET_ITEM(buffers.ptr(), i));
+      at::Tensor c = flat.narrow(0, off, t.numel()).view(t.sizes());
+      off += t.numel();
+      PyObject* w = THPVariable_Wrap(c);
+      if (!w) throw py::error_already_set();
+      PyObject* old = PyList_GET_ITEM(out.ptr(), i);
+      PyList_SET_ITEM(out.ptr(), i, w);
+      Py_DECREF(old);
+    }
+  }
+  for (py::ssize_t i = 0; i < n; ++i)
+    if (alias[i] >= 0) {
+      PyObject* c = PyList_GET_ITEM(out.ptr(), alias[i]);
+      Py_INCREF(c);
+      PyObject* old = PyList_GET_ITEM(out.ptr(), i);
+      PyList_SET_ITEM(out.ptr(), i, c);
+      Py_DECREF(old);
+    }
+  return out;
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_dla_walk, m) {
@@ -210,5 +276,6 @@ PYBIND11_MODULE(_dla_walk, m) {
   m.def("tensors", &tensors, py::arg("model"), py::arg("plain"));
   m.def("block_table", &block_table, py::arg("blocks"));
   m.def("param_views", &param_views, py::arg("flat"), py::arg("params"), py::arg("offsets"));
+  m.def("buffer_copies", &buffer_copies, py::arg("buffers"));
   m.attr("build_id") = py::str(kWalkIdTag + sizeof("dlagg-walk-build-id:") - 1);
 }

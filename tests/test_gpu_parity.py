@@ -416,10 +416,24 @@ def test_device_modules_of_real_layouts_through_fedavg(name, n, dtype):
         m.ps = torch.nn.ParameterList([torch.nn.Parameter(t.view(s).clone().cuda())
                                        for t, (_, s, _) in zip(flat.split(numels), lay["params"])])
         m.register_buffer("steps", torch.full((3,), k, dtype=torch.int64, device="cuda"))
+        # BN-like buffers in two dtypes (one gather each, walk.cpp buffer_copies), one listed twice
+        for j in range(5):
+            m.register_buffer("mean%d" % j, torch.randn(7 + j, generator=g).cuda())
+        m.register_buffer("count", torch.full((2,), 10 * k + 1, dtype=torch.int64, device="cuda"))
+        m.sub = torch.nn.Module()
+        m.sub.register_buffer("mean0_alias", m.mean0)
         models.append(m)
     w = [float(x) for x in np.random.default_rng(n).dirichlet(np.ones(n))]
     out = FedAvg.aggregate(models, w)
     torch.cuda.synchronize()
+    # buffers: deep copies of models[0]'s (equal, own storage, aliasing kept as deepcopy keeps it)
+    for name, b in models[0].named_buffers():
+        c = out.get_buffer(name)
+        assert torch.equal(c, b) and c.dtype == b.dtype and c.shape == b.shape, name
+        assert c.data_ptr() != b.data_ptr(), name
+    assert out.sub.mean0_alias is out.mean0
+    out.mean1.add_(1.0)
+    assert not torch.equal(out.mean1, models[0].mean1)
     flat = [torch.cat([p.detach().reshape(-1) for p in m.parameters()]).cpu() for m in models]
     want = c_wsum([_bits(f, dtype) if dtype != "f32" else f.numpy() for f in flat], w, dtype)
     got_t = torch.cat([p.detach().reshape(-1) for p in out.parameters()])
