@@ -2669,6 +2669,12 @@ int host_reduce_impl(int dtype, int n_peers, int n_tensors, const void* const* t
   const bool mapped = mapped_peer_rows(es, n_peers, n_tensors, tensors, start.data(), begin, end, in_place);
   const bool out_mapped = mapped && is_mapped_host_ptr(h_out);
   if (mapped) g_host_in_place.fetch_add(1, std::memory_order_relaxed);
+  // Pageable peers are packed into h_stage; when h_stage and h_out are device-mapped the reduce then
+  // reads the packed rows across PCIe itself and writes h_out directly (no staging DMA either way; the
+  // kernel's own PCIe reads ran at 57.3-57.6 GB/s against 51.7-57.0 for DMAs, profiles/r04a/
+  // copy_probe.log).  Tuning build: DLA_HOST_STAGE_DMA=1 keeps the staging H2D / D2H DMAs (A/B).
+  static const bool stage_dma = tuning_env("DLA_HOST_STAGE_DMA") != nullptr;
+  const bool stage_read = !mapped && !stage_dma && is_mapped_host_ptr(h_stage) && is_mapped_host_ptr(h_out);
   Events ev;  // h2d[2], red[2], d2h[2]
   hipError_t e = ev.create();
   if (e != hipSuccess) return fail(static_cast<int>(e), std::string("dla_host_reduce: ") + hipGetErrorString(e));
@@ -2789,11 +2795,12 @@ int host_reduce_impl(int dtype, int n_peers, int n_tensors, const void* const* t
       continue;
     }
     // pack chunk c of every peer into row k of staging buffer `buf`, once the H2D of chunk c-2 has read it
-    if (c >= 2 && !check(hipEventSynchronize(h2d[buf]), "H2D")) break;
+    // (stage_read: once chunk c-2's reduce has; its unpack, which waited for it, ran last iteration)
+    if (c >= 2 && !check(hipEventSynchronize(stage_read ? d2h[buf] : h2d[buf]), "H2D")) break;
     const auto t1 = clk::now();
     dsts.clear(), srcs.clear(), bytes.clear();
     for (int k = 0; k < n_peers; ++k) {
-      rows[k] = ds + k * rp;
+      rows[k] = (stage_read ? hs : ds) + k * rp;
       pieces(c0, c1, [&](int t, int64_t a, int64_t b) {
         dsts.push_back(hs + k * rp + (a - c0) * es);
         srcs.push_back(static_cast<const char*>(tensors[static_cast<size_t>(k) * n_tensors + t]) + (a - start[t]) * es);
@@ -2803,6 +2810,19 @@ int host_reduce_impl(int dtype, int n_peers, int n_tensors, const void* const* t
     copy_batch(dsts.data(), srcs.data(), bytes.data(), static_cast<int>(dsts.size()), /*nt=*/true);
     const auto t2 = clk::now();
     if (c == 0) t_first = secs(t_start, t2);
+    if (stage_read) {  // the reduce reads the packed rows in h_stage[buf] and writes h_out[buf], across PCIe
+      const int rc = wsum_impl(dtype, rows.data(), weights, n_peers, m, hout, stream, nullptr);
+      if (rc != DLA_OK) {
+        (void)hipStreamSynchronize(cs_);
+        return rc;
+      }
+      if (!check(hipEventRecord(d2h[buf], cs_), "record")) break;
+      const auto t3 = clk::now();
+      if (c >= 1) unpack(c - 1, 1);  // overlaps chunk c's reduce
+      const auto t4 = clk::now();
+      t_wait += secs(t0, t1), t_pack += secs(t1, t2), t_issue += secs(t2, t3), t_unpack += secs(t3, t4);
+      continue;
+    }
     // ONE H2D of the chunk's rows on the copy stream, once the reduce of chunk c-2 is done with d_stage[buf].
     // That reduce has normally finished long before (it is a few microseconds of a chunk's DMA time):
     // the copy queue is then not made to wait on the compute queue at all — a cross-queue wait in
@@ -2841,7 +2861,7 @@ int host_reduce_impl(int dtype, int n_peers, int n_tensors, const void* const* t
     std::fprintf(stderr,
                  "dla_host_reduce%s: %d peers x %lld elems, %lld chunks of <= %lld: total %.2f ms, first pack %.2f, "
                  "wait-h2d %.2f, pack %.2f (%.1f GB/s), issue %.2f, unpack+wait-d2h %.2f, last unpack %.2f\n",
-                 mapped ? " (peers read in place)" : "", n_peers, static_cast<long long>(end - begin),
+                 mapped ? " (peers read in place)" : stage_read ? " (packed rows read in place)" : "", n_peers, static_cast<long long>(end - begin),
                  static_cast<long long>(n_chunks),
                  static_cast<long long>(chunk_elems), secs(t_start, clk::now()) * 1e3, t_first * 1e3, t_wait * 1e3,
                  t_pack * 1e3, t_pack > 0 ? double(end - begin) * es * n_peers / t_pack / 1e9 : 0.0, t_issue * 1e3,

@@ -291,7 +291,10 @@ int dla_host_round_finish(int dtype, int n_tensors, const int64_t* numels, const
  * slower): when every peer's tensors lie back to back in one page-locked, device-mapped row (16-byte
  * aligned at `begin`), steps 1-2 are skipped — the reduce reads chunk c of every row in place across
  * PCIe — and, when h_out is device-mapped too, writes h_out[buf] directly (no D2H DMA); h_stage and
- * d_stage are then unused.  The result is the same bits. */
+ * d_stage are then unused.  Other peers are packed as in step 1; when h_stage and h_out are both
+ * device-mapped (hipHostMalloc, torch pin_memory) the reduce reads the packed rows in h_stage[buf] and
+ * writes h_out[buf] across PCIe in place of steps 2-3's DMAs (d_stage and d_out unused).  The result
+ * is the same bits. */
 int dla_host_reduce(int dtype, int n_peers, int n_tensors, const void* const* tensors, const int64_t* numels,
                     const double* weights, void* const* outs, int64_t begin, int64_t end, int64_t chunk_elems,
                     void* h_stage, void* d_stage, void* h_out, void* d_out, void* stream, void* copy_stream);
