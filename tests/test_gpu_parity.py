@@ -669,6 +669,52 @@ def test_page_locked_peer_rows_read_in_place(dtype, chunk_bytes, shards):
         fa.release_staging()
 
 
+_STAGE_CHILD = r"""
+import sys, numpy as np, torch
+from torch import nn
+sys.path.insert(0, sys.argv[1])
+from accdfl_amd.core.gradient_aggregation import fedavg as fa
+from accdfl_amd import _lib
+assert _lib.TUNING
+shapes = [(700_001,), (3, 333_333), (5,), (1_200_000,), (77,)]
+g = torch.Generator().manual_seed(61)
+models = []
+for k in range(7):
+    models.append(nn.ParameterList([nn.Parameter(torch.randn(s, generator=g) * 0.05) for s in shapes]))
+w = [float(x) for x in np.random.default_rng(7).dirichlet(np.ones(7))]
+fa._NATIVE_CHUNK_BYTES = 1 << 20
+fa._SMALL_ROUND_BYTES = 0
+out = fa.FedAvg.aggregate(models, w)
+np.save(sys.argv[2], torch.cat([p.detach().reshape(-1) for p in out.parameters()]).numpy())
+np.save(sys.argv[3], np.stack([torch.cat([p.detach().reshape(-1) for p in m]).numpy() for m in models]))
+"""
+
+
+def test_host_reduce_staging_dma_path(tmp_path):
+    """dla_host_reduce's staging-DMA form (packed rows H2D on the copy stream, reduce, D2H) — what runs
+    when the staging is not device-mapped; the product reads mapped staging in place.  The tuning build
+    selects the DMA form (DLA_HOST_STAGE_DMA=1): a child process runs a chunked round through it
+    (DLA_HOST_REDUCE_STATS names the form on stderr) and the result is checked bit for bit here.
+    Skipped when the tuning build is absent or not built from this tree."""
+    import subprocess
+    import sys
+
+    from accdfl_amd import _lib
+
+    tuning = os.path.join(_lib.PKG_ROOT, "lib", "libdlagg_tuning.so")
+    if not os.path.exists(tuning) or _lib.file_build_id(tuning) != _lib.source_build_id(tuning=True):
+        pytest.skip("tuning build absent or stale")
+    env = dict(os.environ, ACCDFL_AMD_TUNING="1", DLA_HOST_STAGE_DMA="1", DLA_HOST_REDUCE_STATS="1")
+    out_f, in_f = str(tmp_path / "out.npy"), str(tmp_path / "in.npy")
+    r = subprocess.run([sys.executable, "-c", _STAGE_CHILD, _lib.PKG_ROOT, out_f, in_f], env=env,
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "dla_host_reduce: 7 peers" in r.stderr and "read in place" not in r.stderr, r.stderr[-2000:]
+    got, peers = np.load(out_f), np.load(in_f)
+    w = [float(x) for x in np.random.default_rng(7).dirichlet(np.ones(7))]
+    assert same_bits(got, fedavg_bits(list(peers), w, "f32"), "f32")
+
+
 @pytest.mark.parametrize("dtype", ["f32", "bf16"])
 def test_small_round_page_locked_rows_in_place(dtype):
     """The small-round path (dla_host_round_start: rounds under 96 MB, e.g. the GL merge of N=2) reads
