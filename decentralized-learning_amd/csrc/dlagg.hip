@@ -2675,6 +2675,13 @@ int host_reduce_impl(int dtype, int n_peers, int n_tensors, const void* const* t
   // copy_probe.log).  Tuning build: DLA_HOST_STAGE_DMA=1 keeps the staging H2D / D2H DMAs (A/B).
   static const bool stage_dma = tuning_env("DLA_HOST_STAGE_DMA") != nullptr;
   const bool stage_read = !mapped && !stage_dma && is_mapped_host_ptr(h_stage) && is_mapped_host_ptr(h_out);
+  // A reduce that reads host memory runs the vector-per-lane kernel (n x 512 B of loads in flight per
+  // wave): the shape-based choice for 8 fp32 peers over a 32 MiB chunk is the 16-byte stream kernel,
+  // whose fewer loads in flight suit HBM, not PCIe round trips (r04e: 8 x 25 M host round 17.9-20.4 ms
+  // reading the packed rows with it, against 15.4-15.6 through the staging DMA).
+  dla_launch_cfg_t host_cfg{};
+  host_cfg.variant = vec_variant(n_peers);
+  const dla_launch_cfg_t* read_cfg = dtype == DLA_F64 ? nullptr : &host_cfg;
   Events ev;  // h2d[2], red[2], d2h[2]
   hipError_t e = ev.create();
   if (e != hipSuccess) return fail(static_cast<int>(e), std::string("dla_host_reduce: ") + hipGetErrorString(e));
@@ -2781,7 +2788,7 @@ int host_reduce_impl(int dtype, int n_peers, int n_tensors, const void* const* t
       // the reduce reads chunk c of every peer's page-locked row across PCIe; h_out[buf] is free again
       // (chunk c-2's unpack ran on this thread during the previous iteration)
       for (int k = 0; k < n_peers; ++k) rows[k] = in_place[k] + c0 * es;
-      const int rc = wsum_impl(dtype, rows.data(), weights, n_peers, m, out_mapped ? hout : dout, stream, nullptr);
+      const int rc = wsum_impl(dtype, rows.data(), weights, n_peers, m, out_mapped ? hout : dout, stream, read_cfg);
       if (rc != DLA_OK) {
         (void)hipStreamSynchronize(cs_);
         return rc;
@@ -2811,7 +2818,7 @@ int host_reduce_impl(int dtype, int n_peers, int n_tensors, const void* const* t
     const auto t2 = clk::now();
     if (c == 0) t_first = secs(t_start, t2);
     if (stage_read) {  // the reduce reads the packed rows in h_stage[buf] and writes h_out[buf], across PCIe
-      const int rc = wsum_impl(dtype, rows.data(), weights, n_peers, m, hout, stream, nullptr);
+      const int rc = wsum_impl(dtype, rows.data(), weights, n_peers, m, hout, stream, read_cfg);
       if (rc != DLA_OK) {
         (void)hipStreamSynchronize(cs_);
         return rc;
