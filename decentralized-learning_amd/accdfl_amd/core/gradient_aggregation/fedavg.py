@@ -382,6 +382,31 @@ def _device_layout(models: List[nn.Module]):
     return dtype, torch.device("cuda", dev), [p.numel() for p in p0], table
 
 
+_flat_plans: Dict[tuple, tuple] = {}
+
+
+def _flat_plan(dtype, numels: List[int]):
+    """(element offsets, total elements, byte offsets as uint64, numels as a ctypes int64 array) of one
+    allocation holding a layout's tensors each 256-byte aligned, cached per (dtype, layout): a device
+    round of one architecture computes it once, not every round."""
+    key = (dtype, tuple(numels))
+    plan = _flat_plans.get(key)
+    if plan is None:
+        import numpy as np
+
+        esize = torch.empty((), dtype=dtype).element_size()
+        align = _ALIGN_BYTES // esize
+        offs, total = [], 0
+        for n_ in numels:
+            offs.append(total)
+            total += _round_up(max(n_, 1), align)
+        if len(_flat_plans) > 64:
+            _flat_plans.clear()
+        plan = _flat_plans[key] = (offs, total, np.array(offs, dtype=np.uint64) * np.uint64(esize),
+                                   (ctypes.c_int64 * len(numels))(*numels))
+    return plan
+
+
 def _device_round(models: List[nn.Module], weights, layout) -> "nn.Module | None":
     """The whole aggregate for device-resident models of one layout: deepcopy(models[0]) with fresh
     parameters (fedavg.py:20), then every parameter of every model folded straight into them by
@@ -400,17 +425,10 @@ def _device_round(models: List[nn.Module], weights, layout) -> "nn.Module | None
     if objs is None or len(objs[0]) != len(numels) or any(type(p) is not nn.Parameter for p in objs[0]):
         return _device_round_per_tensor(models, weights, layout)
     p0, b0 = objs
-    esize = torch.empty((), dtype=dtype).element_size()
-    align = _ALIGN_BYTES // esize
-    offs, total = [], 0
-    for n_ in numels:
-        offs.append(total)
-        total += _round_up(max(n_, 1), align)
+    offs, total, byte_offs, nums = _flat_plan(dtype, numels)
     flat = torch.empty(total, dtype=dtype, device=device)
-    base = flat.data_ptr()
     ptrs = (ctypes.c_void_p * table.size).from_buffer(table)
-    outs = (ctypes.c_void_p * len(numels))(*[base + o * esize for o in offs])
-    nums = (ctypes.c_int64 * len(numels))(*numels)
+    outs = (ctypes.c_void_p * len(numels)).from_buffer(byte_offs + flat.data_ptr())
     _wsum.wsum_multi_ptrs(dtype, ptrs, outs, nums, weights, device)
     # while the reduce runs: the result's parameters over `flat` (nn.Parameter views made natively: what
     # torch.Tensor._make_subclass(nn.Parameter, flat.as_strided(...), requires_grad) makes), models[0]'s
