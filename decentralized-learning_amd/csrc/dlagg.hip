@@ -1972,10 +1972,15 @@ bool is_device_ptr(const void* p) {
 }
 
 // Page-locked host memory mapped into the device address space at the same address (hipHostMalloc,
-// torch pin_memory): a kernel can read / write it across PCIe through the host pointer itself.
+// torch pin_memory): a kernel can read / write it across PCIe through the host pointer itself.  Only
+// memory the runtime associates with the CURRENT device counts: a kernel on another GPU of the node
+// reading a buffer mapped for device 0 is not something this library assumes (the host path over several
+// GPUs then keeps its staging DMAs on those GPUs, which any page-locked memory serves).
 bool is_mapped_host_ptr(const void* p) {
   hipPointerAttribute_t a;
-  const bool ok = hipPointerGetAttributes(&a, p) == hipSuccess && a.type == hipMemoryTypeHost && a.devicePointer == p;
+  int cur = -1;
+  const bool ok = hipPointerGetAttributes(&a, p) == hipSuccess && a.type == hipMemoryTypeHost &&
+                  a.devicePointer == p && hipGetDevice(&cur) == hipSuccess && a.device == cur;
   if (!ok) (void)hipGetLastError();
   return ok;
 }
