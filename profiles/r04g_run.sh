@@ -23,3 +23,5 @@ cp gpurun_out/prof_r04g/summary/* gpurun_out/prof_r04g/trace.log $out/ 2>/dev/nu
 rm -rf gpurun_out/prof_r04g
 run 300 python -u profiles/r04_device_round_probe.py > $out/device_round.log 2>&1
 run 900 python -u bench.py --gpus 4 --dist-backend gloo --steps 20 --warmup 5 > $out/gloo4.log 2>&1
+# the table kernel under an occupancy cap of W workgroups per CU (0 = none, the product's choice): A/B build
+run 300 python -u profiles/r04_multi_pipe_ab.py --lib decentralized-learning_amd/lib/ab/libdlagg_wgs.so --knob DLA_MULTI_WGS --values 0,12,16,20,24 --shapes r34x16,r34x32,r8x16,r8x32,femx32 > $out/multi_wgs_ab.log 2>&1
