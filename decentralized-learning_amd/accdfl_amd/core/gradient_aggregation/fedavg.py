@@ -451,9 +451,14 @@ def _seed_buffers(buffers, memo: dict) -> None:
                 memo[id(b)] = c
         return
     groups: Dict[tuple, list] = {}
+    uses: Dict[int, int] = {}
+    for b in {id(b): b for b in buffers}.values():
+        if type(b) is torch.Tensor:
+            key = b.untyped_storage().data_ptr()
+            uses[key] = uses.get(key, 0) + 1
     for b in buffers:
         if (type(b) is torch.Tensor and b.is_cuda and not b.requires_grad and b.is_contiguous()
-                and id(b) not in memo):
+                and id(b) not in memo and uses[b.untyped_storage().data_ptr()] == 1):
             groups.setdefault((b.device, b.dtype), []).append(b)
     for bs in groups.values():
         if len(bs) < 2:

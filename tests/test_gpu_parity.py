@@ -422,6 +422,7 @@ def test_device_modules_of_real_layouts_through_fedavg(name, n, dtype):
         m.register_buffer("count", torch.full((2,), 10 * k + 1, dtype=torch.int64, device="cuda"))
         m.sub = torch.nn.Module()
         m.sub.register_buffer("mean0_alias", m.mean0)
+        m.sub.register_buffer("mean2_view", m.mean2[1:4])  # shares mean2's storage
         models.append(m)
     w = [float(x) for x in np.random.default_rng(n).dirichlet(np.ones(n))]
     out = FedAvg.aggregate(models, w)
@@ -432,6 +433,9 @@ def test_device_modules_of_real_layouts_through_fedavg(name, n, dtype):
         assert torch.equal(c, b) and c.dtype == b.dtype and c.shape == b.shape, name
         assert c.data_ptr() != b.data_ptr(), name
     assert out.sub.mean0_alias is out.mean0
+    # storage sharing kept as deepcopy keeps it (those buffers are left to the stock deepcopy)
+    assert out.sub.mean2_view.untyped_storage().data_ptr() == out.mean2.untyped_storage().data_ptr()
+    assert out.mean2.untyped_storage().data_ptr() != models[0].mean2.untyped_storage().data_ptr()
     out.mean1.add_(1.0)
     assert not torch.equal(out.mean1, models[0].mean1)
     flat = [torch.cat([p.detach().reshape(-1) for p in m.parameters()]).cpu() for m in models]
