@@ -719,6 +719,46 @@ def test_host_reduce_staging_dma_path(tmp_path):
     assert same_bits(got, fedavg_bits(list(peers), w, "f32"), "f32")
 
 
+@pytest.mark.parametrize("large", [False, True])
+@pytest.mark.parametrize("dtype", ["f32", "bf16", "f16"])
+def test_page_locked_rows_in_place_many_peers(dtype, large):
+    """130 page-locked peer rows (two passes of the reduce: the second folds peers 128-129 into the
+    running sum it reads back from the page-locked output across PCIe), through the small-round call and
+    through dla_host_reduce's chunks; IEEE specials; bit-exact."""
+    from torch import nn
+
+    from accdfl_amd import _lib
+    from accdfl_amd.core.gradient_aggregation import fedavg as fa
+
+    shapes = [(1000, 3), (7,), (4099,)]
+    numels = [int(np.prod(s)) for s in shapes]
+    g = torch.Generator().manual_seed(67)
+    models = []
+    for k in range(130):
+        flat = (torch.randn(sum(numels), generator=g) * 0.05).to(TDT[dtype])
+        if k == 5:
+            flat[:4] = torch.tensor([float("inf"), -0.0, float("nan"), 65504.0]).to(TDT[dtype])
+        flat = flat.pin_memory()
+        m = nn.Module()
+        m.ps = nn.ParameterList([nn.Parameter(t.view(s)) for t, s in zip(flat.split(numels), shapes)])
+        models.append(m)
+    w = [float(x) for x in np.random.default_rng(130).dirichlet(np.ones(130))]
+    old, small = fa._NATIVE_CHUNK_BYTES, fa._SMALL_ROUND_BYTES
+    if large:
+        fa._NATIVE_CHUNK_BYTES, fa._SMALL_ROUND_BYTES = 1 << 16, 0
+    try:
+        before = _lib.host_in_place_rounds()
+        out = fa.FedAvg.aggregate(models, w)
+        assert _lib.host_in_place_rounds() > before
+    finally:
+        fa._NATIVE_CHUNK_BYTES, fa._SMALL_ROUND_BYTES = old, small
+        fa.release_staging()
+    for i, p in enumerate(out.parameters()):
+        want = fedavg_bits([gc.as_float(_bits(list(m.parameters())[i].detach().reshape(-1), dtype), dtype)
+                            for m in models], w, dtype)
+        assert same_bits(gc.as_float(_bits(p.detach().reshape(-1), dtype), dtype), want, dtype), i
+
+
 @pytest.mark.parametrize("dtype", ["f32", "bf16"])
 def test_small_round_page_locked_rows_in_place(dtype):
     """The small-round path (dla_host_round_start: rounds under 96 MB, e.g. the GL merge of N=2) reads
