@@ -457,7 +457,7 @@ def _seed_buffers(buffers, memo: dict) -> None:
             key = b.untyped_storage().data_ptr()
             uses[key] = uses.get(key, 0) + 1
     for b in buffers:
-        if (type(b) is torch.Tensor and b.is_cuda and not b.requires_grad and b.is_contiguous()
+        if (type(b) is torch.Tensor and not b.requires_grad and b.is_contiguous()
                 and id(b) not in memo and uses[b.untyped_storage().data_ptr()] == 1):
             groups.setdefault((b.device, b.dtype), []).append(b)
     for bs in groups.values():
@@ -981,8 +981,14 @@ def _center_copy(model0: nn.Module, large: bool = True) -> nn.Module:
     of a 2-model ResNet-8 round; ``large=False`` allocates every parameter fresh).
     Buffers and every other attribute are deep-copied exactly as in the reference (the module
     tree through _clone_value, deepcopy's protocol without its per-object dispatch: the GL
-    merge of two GNLeNet models builds this copy every round)."""
-    return _clone_value(model0, _fresh_params(model0, large))
+    merge of two GNLeNet models builds this copy every round); the buffers of each (device, dtype) are
+    copied by one gather into one fresh allocation (_seed_buffers) instead of a deepcopy each."""
+    memo = _fresh_params(model0, large)
+    mod = _lib.walk_module()
+    objs = mod.tensors(model0, _PLAIN_SET) if mod is not None else None
+    if objs is not None and len(objs[1]) > 1:
+        _seed_buffers(objs[1], memo)
+    return _clone_value(model0, memo)
 
 
 def _fresh_params(model0: nn.Module, large: bool = True) -> dict:

@@ -291,6 +291,23 @@ def test_center_copy_is_a_deepcopy():
     assert all(p is not q for p, q in zip(got.parameters(), m.parameters()))
     got.seq(torch.zeros(1, 3, 5, 5))
     got.rnn(torch.zeros(2, 1, 4))
+    # the same with the module classes classified first, as every aggregate does (the walk extension then
+    # lists the buffers and _center_copy copies them by one gather per dtype): buffers equal, in their own
+    # storage, a buffer sharing another's storage left to deepcopy (sharing kept)
+    from accdfl_amd.core.gradient_aggregation import fedavg as fa
+
+    m = _OddModule()
+    m.register_buffer("mean_view", m.seq[1].running_mean[1:3])  # shares the BN buffer's storage
+    for cls in {type(x) for x in m.modules()}:
+        fa._plain_walk(cls)
+    want = copy.deepcopy(m)
+    got = _center_copy(m, large=False)
+    _same_structure(want, got, set())
+    for (name, b), c in zip(m.named_buffers(), got.buffers()):
+        assert torch.equal(b, c) and b.untyped_storage().data_ptr() != c.untyped_storage().data_ptr(), name
+    assert got.mean_view.untyped_storage().data_ptr() == got.seq[1].running_mean.untyped_storage().data_ptr()
+    got.seq[1].running_var.add_(1.0)
+    assert not torch.equal(got.seq[1].running_var, m.seq[1].running_var)
     # a parametrized module (its generated class has its own __deepcopy__: the stock path, same memo)
     from torch.nn.utils import parametrizations
 
