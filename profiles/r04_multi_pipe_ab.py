@@ -5,7 +5,10 @@ environment knob read per call:
     pipelined variant (BLK blocks of 64 vectors per workgroup, block i+1's loads issued before block
     i's fold; one tensor lookup per BLK blocks);
   * DLA_MULTI_VW=2/4 (lib/ab/libdlagg_vw.so): 8-byte against 16-byte loads per lane (512 B against
-    1 KiB of each peer per wave).
+    1 KiB of each peer per wave);
+  * DLA_MULTI_WGS=W (lib/ab/libdlagg_wgs.so): an occupancy cap of W workgroups per CU (0 = none);
+  * DLA_MULTI_G=8/16 (lib/ab/libdlagg_g.so): fold rounds of 8 peers for 9-32-peer passes, of 16 for
+    larger passes, instead of 16 / 32 (0 = the product's).
 Legs interleave in one process, HIP events on the launch stream, and every leg's output is compared
 bit for bit with the first leg's.  Layouts: the reference models as
 separate device tensors (tests/golden/layouts.json), at their BASELINE peer counts where a pass is
@@ -31,6 +34,8 @@ SHAPES = {  # name: (layout, peers, dtype)
     "r8x32": ("cifar10_resnet8", 32, torch.float32),
     "femx32": ("femnist_cnn", 32, torch.float32),
     "femx8": ("femnist_cnn", 8, torch.float32),
+    "r34x128": ("google_speech_resnet34", 128, torch.bfloat16),
+    "r8x64": ("cifar10_resnet8", 64, torch.float32),
 }
 
 

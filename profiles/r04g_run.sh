@@ -25,3 +25,6 @@ run 300 python -u profiles/r04_device_round_probe.py > $out/device_round.log 2>&
 run 900 python -u bench.py --gpus 4 --dist-backend gloo --steps 20 --warmup 5 > $out/gloo4.log 2>&1
 # the table kernel under an occupancy cap of W workgroups per CU (0 = none, the product's choice): A/B build
 run 300 python -u profiles/r04_multi_pipe_ab.py --lib decentralized-learning_amd/lib/ab/libdlagg_wgs.so --knob DLA_MULTI_WGS --values 0,12,16,20,24 --shapes r34x16,r34x32,r8x16,r8x32,femx32 > $out/multi_wgs_ab.log 2>&1
+# the table kernel with narrower fold rounds (8 peers for 9-32-peer passes, 16 above): A/B build
+run 300 python -u profiles/r04_multi_pipe_ab.py --lib decentralized-learning_amd/lib/ab/libdlagg_g.so --knob DLA_MULTI_G --values 0,8 --shapes r34x16,r34x32,r8x16,r8x32,femx32 > $out/multi_g8_ab.log 2>&1
+run 300 python -u profiles/r04_multi_pipe_ab.py --lib decentralized-learning_amd/lib/ab/libdlagg_g.so --knob DLA_MULTI_G --values 0,16 --shapes r34x128,r8x64 > $out/multi_g16_ab.log 2>&1
