@@ -452,13 +452,14 @@ def _seed_buffers(buffers, memo: dict) -> None:
         return
     groups: Dict[tuple, list] = {}
     uses: Dict[int, int] = {}
-    for b in {id(b): b for b in buffers}.values():
-        if type(b) is torch.Tensor:
-            key = b.untyped_storage().data_ptr()
-            uses[key] = uses.get(key, 0) + 1
-    for b in buffers:
-        if (type(b) is torch.Tensor and not b.requires_grad and b.is_contiguous()
-                and id(b) not in memo and uses[b.untyped_storage().data_ptr()] == 1):
+    dense = [b for b in {id(b): b for b in buffers}.values()
+             if type(b) is torch.Tensor and b.layout is torch.strided and b.device.type in ("cpu", "cuda")]
+    for b in dense:
+        key = b.untyped_storage().data_ptr()
+        uses[key] = uses.get(key, 0) + 1
+    for b in dense:
+        if (not b.requires_grad and b.is_contiguous() and id(b) not in memo
+                and uses[b.untyped_storage().data_ptr()] == 1):
             groups.setdefault((b.device, b.dtype), []).append(b)
     for bs in groups.values():
         if len(bs) < 2:
