@@ -15,11 +15,13 @@ HBM layout.  fp32 / bf16 / f16 slabs are TILE-INTERLEAVED:
 (dla_wsum_slab_tiled) streams one region of HBM at a time instead of ``capacity`` regions
 100 MB apart: 8 x 25 M fp32 130.2 us against 135.6 for separate rows, 128 x 21.3 M bf16
 792 against 869 (profiles/r02d_ab_tiled.log).  ``tile`` is dla_slab_tile_elems (1-32 KiB).
-A row lands in its tiles directly: each source tensor (host memory, page-locked or pageable, or
-device memory) is one dla_slab_stage call on the copy stream — a 2D copy whose rows are tiles and
-whose destination pitch is ``capacity`` tiles, so the copy engine writes every tile in place (round
-3 staged a contiguous device row and scattered it: 2 x the row's bytes of extra HBM traffic, one
-more kernel and a row-sized buffer).  fp64 slabs keep one row per peer
+A row lands in its tiles directly: each page-locked host or device source tensor is one
+dla_slab_stage call on the copy stream — a 2D copy whose rows are tiles and whose destination pitch
+is ``capacity`` tiles, so the copy engine writes every tile in place (round 3 staged a contiguous
+device row and scattered it: 2 x the row's bytes of extra HBM traffic, one more kernel and a
+row-sized buffer).  Pageable host sources go through two 16 MiB device chunks (a
+contiguous H2D, then the 2D copy from the chunk: the runtime stages a 2D copy from pageable memory
+one row at a time).  fp64 slabs keep one row per peer
 ([capacity, pitch], pitch = the parameter count rounded up to 256 bytes).  A 25 M-parameter
 fp32 model is a 100 MB row; 288 GB of HBM holds ~2800 of them, so capacity is never the
 constraint at accdfl's sample sizes.
@@ -62,6 +64,7 @@ class PeerSlab:
         self.copy_stream = torch.cuda.Stream(self.device)
         self._bounce = [None, None]
         self._bounce_ev = [None, None]
+        self._dev_chunks = None    # device staging of pageable host sources (_put_pageable)
         self._h_out = None
         self._flat = None          # device result of reduce_into (reused every round)
         self._plan = None          # prepared launch over (rows 0..n-1, _flat)
@@ -153,14 +156,38 @@ class PeerSlab:
     # tensors are packed into the pinned bounce buffer and sent as one copy.
     DIRECT_BYTES = 1 << 20
 
+    # Pageable host sources of a tiled slab go through device chunks of this size (two, reused in
+    # stream order): a contiguous H2D, then a 2D D2D copy into the tiles.  A 2D copy straight from
+    # pageable memory is staged by the runtime row by row — one tile at a time — and moved a 100 MB
+    # wire payload at 5.7 GB/s (bench.py wire_ingress, profiles/r04a-r04g) against 51.8 for round 3's
+    # contiguous H2D; the D2D pass costs ~2 % (2.1 TB/s, profiles/r04a/copy_probe.log).
+    PAGEABLE_CHUNK_BYTES = 16 << 20
+
     def _put(self, row: int, off: int, src: torch.Tensor, n: int):
         """``n`` elements at ``src`` (host or this device) -> row ``row`` from element ``off`` on, on the
-        copy stream.  Tiled slabs: dla_slab_stage, one 2D copy that writes every tile in place."""
+        copy stream.  Tiled slabs: dla_slab_stage, one 2D copy that writes every tile in place (from
+        page-locked host or device memory; pageable host memory through _put_pageable)."""
         if self.layout == "rows":
             self.buf[row, off:off + n].copy_(src.view(-1)[:n], non_blocking=src.device.type == "cpu" and src.is_pinned())
             return
+        if src.device.type == "cpu" and not src.is_pinned():
+            self._put_pageable(row, off, src, n)
+            return
         _lib.slab_stage(self.code, self.buf.data_ptr(), self.tile, self.capacity, row, off, src.data_ptr(), n,
                         int(self.copy_stream.cuda_stream))
+
+    def _put_pageable(self, row: int, off: int, src: torch.Tensor, n: int):
+        chunk = max(1, self.PAGEABLE_CHUNK_BYTES // self.buf.element_size())
+        if self._dev_chunks is None:
+            self._dev_chunks = [torch.empty(chunk, dtype=self.dtype, device=self.device) for _ in range(2)]
+        flat = src.view(-1)
+        with torch.cuda.stream(self.copy_stream):
+            for i, s0 in enumerate(range(0, n, chunk)):
+                m = min(chunk, n - s0)
+                buf = self._dev_chunks[i & 1][:m]
+                buf.copy_(flat[s0:s0 + m], non_blocking=True)  # pageable: consumed before this returns
+                _lib.slab_stage(self.code, self.buf.data_ptr(), self.tile, self.capacity, row, off + s0, buf.data_ptr(),
+                                m, int(self.copy_stream.cuda_stream))
 
     def _stage_flat_list(self, flat: List[torch.Tensor]) -> int:
         row = self.n
