@@ -1019,6 +1019,39 @@ def test_peer_slab_mixed_direct_and_bounced_tensors():
         assert torch.equal(slab.row(k).cpu(), torch.cat([p.reshape(-1) for p in pl]))
 
 
+@pytest.mark.parametrize("source", ["pageable", "pinned", "bytes", "device"])
+def test_peer_slab_sources_across_chunks(source):
+    """Every kind of source a peer arrives in, staged into the tiled slab: pageable host tensors (two
+    16 MiB device chunks: contiguous H2D + 2D copy), page-locked ones and device ones (one 2D copy),
+    and a wire payload decoded as views of the pageable bytes; tensors that span several chunks and
+    start inside a tile (offsets 3 and 5 000 004), with the slab growing past its capacity; each row
+    and the reduce bit-exact."""
+    from accdfl_amd.core import wire
+    from accdfl_amd.core.peer_slab import PeerSlab
+
+    shapes = [(3,), (5_000_001,), (4_200_000,), (77,)]
+    g = torch.Generator().manual_seed(71)
+    models = [[(torch.randn(s, generator=g) * 0.05) for s in shapes] for _ in range(5)]
+    slab = PeerSlab(shapes, torch.float32, capacity=2)
+    for pl in models:
+        if source == "pinned":
+            slab.stage([p.pin_memory() for p in pl])
+        elif source == "device":
+            slab.stage([p.cuda() for p in pl])
+        elif source == "bytes":
+            m = torch.nn.ParameterList([torch.nn.Parameter(p) for p in pl])
+            sd = wire.loads_state_dict(wire.serialize_model(m), copy=False)  # views of the payload bytes
+            slab.stage([sd[k] for k in sd])
+        else:
+            slab.stage(pl)
+    slab.copy_stream.synchronize()
+    for k, pl in enumerate(models):
+        assert torch.equal(slab.row(k).cpu(), torch.cat([p.reshape(-1) for p in pl])), k
+    w = [float(x) for x in np.random.default_rng(5).dirichlet(np.ones(5))]
+    want = fedavg_bits([torch.cat([p.reshape(-1) for p in pl]).numpy() for pl in models], w, "f32")
+    assert same_bits(_bits(slab.reduce(w), "f32"), want, "f32")
+
+
 def test_tied_parameters_and_structure_preserved():
     """A parameter registered in two submodules (tied weights) appears once in
     parameters(); the result keeps the tie, like deepcopy(models[0]) does."""
