@@ -65,6 +65,12 @@ class PeerSlab:
         self._bounce = [None, None]
         self._bounce_ev = [None, None]
         self._dev_chunks = None    # device staging of pageable host sources (_put_pageable)
+        self._held: List[torch.Tensor] = []  # page-locked sources of the stage call in progress
+        # page-locked host sources of copies still in flight, with the copy stream's event after them:
+        # dla_slab_stage's DMAs are not seen by torch's pinned-memory allocator (a torch copy_ records an
+        # event there), so the slab keeps the tensors — and their blocks out of the allocator's reuse —
+        # until the copy stream has passed them
+        self._inflight: List[tuple] = []
         self._h_out = None
         self._flat = None          # device result of reduce_into (reused every round)
         self._plan = None          # prepared launch over (rows 0..n-1, _flat)
@@ -170,9 +176,11 @@ class PeerSlab:
         if self.layout == "rows":
             self.buf[row, off:off + n].copy_(src.view(-1)[:n], non_blocking=src.device.type == "cpu" and src.is_pinned())
             return
-        if src.device.type == "cpu" and not src.is_pinned():
-            self._put_pageable(row, off, src, n)
-            return
+        if src.device.type == "cpu":
+            if not src.is_pinned():
+                self._put_pageable(row, off, src, n)
+                return
+            self._held.append(src)
         _lib.slab_stage(self.code, self.buf.data_ptr(), self.tile, self.capacity, row, off, src.data_ptr(), n,
                         int(self.copy_stream.cuda_stream))
 
@@ -189,7 +197,24 @@ class PeerSlab:
                 _lib.slab_stage(self.code, self.buf.data_ptr(), self.tile, self.capacity, row, off + s0, buf.data_ptr(),
                                 m, int(self.copy_stream.cuda_stream))
 
+    def _release_inflight(self):
+        """Drop the page-locked sources whose copies the copy stream has passed."""
+        while self._inflight and self._inflight[0][0].query():
+            self._inflight.pop(0)
+
     def _stage_flat_list(self, flat: List[torch.Tensor]) -> int:
+        self._release_inflight()
+        self._held: List[torch.Tensor] = []
+        try:
+            return self._stage_flat_list_held(flat)
+        finally:
+            if self._held:
+                ev = torch.cuda.Event()
+                ev.record(self.copy_stream)
+                self._inflight.append((ev, self._held))
+            self._held = []
+
+    def _stage_flat_list_held(self, flat: List[torch.Tensor]) -> int:
         row = self.n
         if row >= self.capacity:
             self._grow(row + 1)

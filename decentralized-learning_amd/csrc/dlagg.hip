@@ -2529,6 +2529,19 @@ int dla_host_copy_batch_ex(void* const* dsts, const void* const* srcs, const int
   return DLA_OK;
 }
 
+// The launch of a reduce that reads host memory across PCIe: the vector-per-lane kernel (n x 512 B of
+// loads in flight per wave) — the shape-based choice (the 16-byte stream kernel for few fp32 peers) is
+// tuned for HBM (r04e/r04f, dla_host_reduce).  fp64 keeps the shape-based choice (no vector kernel).
+// Tuning build: DLA_HOST_AUTO_KERNEL=1 keeps the shape-based choice for host reads (A/B).
+static const dla_launch_cfg_t* host_read_cfg(int dtype, int n_peers) {
+  static const bool automatic = tuning_env("DLA_HOST_AUTO_KERNEL") != nullptr;
+  if (automatic || dtype == DLA_F64) return nullptr;
+  static thread_local dla_launch_cfg_t cfg;
+  cfg = dla_launch_cfg_t{};
+  cfg.variant = vec_variant(n_peers);
+  return &cfg;
+}
+
 int dla_host_round_start(int dtype, int n_peers, int n_tensors, const void* const* tensors, const int64_t* numels,
                          const double* weights, void* rows, int64_t pitch_elems, void* result, void* stream) {
   g_last_error.clear();
@@ -2566,7 +2579,7 @@ int dla_host_round_start(int dtype, int n_peers, int n_tensors, const void* cons
     if (mapped_peer_rows(es, n_peers, n_tensors, tensors, start.data(), 0, total, in_place)) {
       g_host_in_place.fetch_add(1, std::memory_order_relaxed);
       std::vector<const void*> ptrs(in_place.begin(), in_place.end());
-      return wsum_impl(dtype, ptrs.data(), weights, n_peers, total, result, stream, nullptr);
+      return wsum_impl(dtype, ptrs.data(), weights, n_peers, total, result, stream, host_read_cfg(dtype, n_peers));
     }
   }
   // pack: tensor t of peer k -> row k at the tensor's flat offset (the zip order of fedavg.py:24)
@@ -2587,7 +2600,7 @@ int dla_host_round_start(int dtype, int n_peers, int n_tensors, const void* cons
     }
   }
   copy_batch(dsts.data(), srcs.data(), bytes.data(), static_cast<int>(dsts.size()), /*nt=*/true);
-  const int rc = wsum_impl(dtype, row_ptrs.data(), weights, n_peers, total, result, stream, nullptr);
+  const int rc = wsum_impl(dtype, row_ptrs.data(), weights, n_peers, total, result, stream, host_read_cfg(dtype, n_peers));
   return rc;
 }
 
@@ -2684,9 +2697,7 @@ int host_reduce_impl(int dtype, int n_peers, int n_tensors, const void* const* t
   // wave): the shape-based choice for 8 fp32 peers over a 32 MiB chunk is the 16-byte stream kernel,
   // whose fewer loads in flight suit HBM, not PCIe round trips (r04e: 8 x 25 M host round 17.9-20.4 ms
   // reading the packed rows with it, against 15.4-15.6 through the staging DMA).
-  dla_launch_cfg_t host_cfg{};
-  host_cfg.variant = vec_variant(n_peers);
-  const dla_launch_cfg_t* read_cfg = dtype == DLA_F64 ? nullptr : &host_cfg;
+  const dla_launch_cfg_t* read_cfg = host_read_cfg(dtype, n_peers);
   Events ev;  // h2d[2], red[2], d2h[2]
   hipError_t e = ev.create();
   if (e != hipSuccess) return fail(static_cast<int>(e), std::string("dla_host_reduce: ") + hipGetErrorString(e));
