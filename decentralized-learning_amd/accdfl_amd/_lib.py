@@ -29,7 +29,7 @@ LIB_PATH = os.environ.get("DLAGG_LIB", os.path.join(PKG_ROOT, "lib",
 
 # dtype codes (include/dlagg.h)
 DLA_F32, DLA_BF16, DLA_F16, DLA_F64 = 0, 1, 2, 3
-ABI_VERSION = 11
+ABI_VERSION = 12
 
 HIPCC_FLAGS = [
     "--offload-arch=gfx950",
@@ -73,6 +73,7 @@ EXPORTED = (
     "dla_wsum_multi_table",
     "dla_slab_stage",
     "dla_host_in_place_rounds",
+    "dla_wsum_multi_table_acc",
 )
 
 
@@ -325,6 +326,10 @@ class _Lib:
                                             ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_double),
                                             ctypes.c_int, vp, vp, vp]
         so.dla_wsum_multi_table.restype = ctypes.c_int
+        so.dla_wsum_multi_table_acc.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(vp), ctypes.POINTER(vp),
+                                                ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_double),
+                                                ctypes.c_int, ctypes.c_int, vp, vp, vp]
+        so.dla_wsum_multi_table_acc.restype = ctypes.c_int
         so.dla_slab_stage.argtypes = [ctypes.c_int, vp, ctypes.c_int64, ctypes.c_int64, ctypes.c_int, ctypes.c_int64,
                                       vp, ctypes.c_int64, vp]
         so.dla_slab_stage.restype = ctypes.c_int
@@ -443,8 +448,9 @@ def wsum_multi_table_bytes(n_tensors: int, n_peers: int) -> int:
 
 
 def wsum_multi_table_ptrs(dtype_code: int, peer_ptrs, out_ptrs, numels, weights: Sequence[float], table_host: int,
-                          table_dev: int, stream_ptr: int) -> None:
-    """dla_wsum_multi_table: peer_ptrs is [n_tensors * n_peers] (tensor-major); sequences or ctypes arrays."""
+                          table_dev: int, stream_ptr: int, acc_in: bool = False) -> None:
+    """dla_wsum_multi_table (acc_in: dla_wsum_multi_table_acc, folding into the running sum the outputs
+    hold): peer_ptrs is [n_tensors * n_peers] (tensor-major); sequences or ctypes arrays."""
     L = lib()
     n = len(weights)
     if not isinstance(out_ptrs, ctypes.Array):
@@ -456,8 +462,12 @@ def wsum_multi_table_ptrs(dtype_code: int, peer_ptrs, out_ptrs, numels, weights:
         raise ValueError("peer_ptrs must hold n_tensors * n_peers pointers")
     if not isinstance(numels, ctypes.Array):
         numels = (ctypes.c_int64 * t)(*[int(x) for x in numels])
-    rc = L.so.dla_wsum_multi_table(dtype_code, t, peer_ptrs, out_ptrs, numels, _dbl_array(weights), n, table_host,
-                                   table_dev, stream_ptr)
+    if acc_in:
+        rc = L.so.dla_wsum_multi_table_acc(dtype_code, t, peer_ptrs, out_ptrs, numels, _dbl_array(weights), n, 1,
+                                           table_host, table_dev, stream_ptr)
+    else:
+        rc = L.so.dla_wsum_multi_table(dtype_code, t, peer_ptrs, out_ptrs, numels, _dbl_array(weights), n,
+                                       table_host, table_dev, stream_ptr)
     if rc != 0:
         L.check(rc, "dla_wsum_multi_table")
 

@@ -198,16 +198,16 @@ _rings_lock = threading.Lock()
 
 
 def wsum_multi_ptrs(dtype: torch.dtype, ptrs, out_ptrs, numels, weights: Sequence[float], device: torch.device,
-                    stream: Optional[torch.cuda.Stream] = None) -> None:
+                    stream: Optional[torch.cuda.Stream] = None, acc_in: bool = False) -> None:
     """wsum_multi on raw pointers the caller has validated (device-resident, contiguous, one dtype,
     numels[i] elements each; ptrs tensor-major [n_tensors * n_peers]).  Rounds of more than
     MULTI_TABLE_MIN_PEERS - 1 peers go through dla_wsum_multi_table (one launch per 128-peer pass)."""
     code = dtype_code(dtype)
     n = len(weights)
     s = stream if stream is not None else torch.cuda.current_stream(device)
-    table = n >= MULTI_TABLE_MIN_PEERS or (
+    table = acc_in or n >= MULTI_TABLE_MIN_PEERS or (
         n > 8 and (n + 1) * sum(numels) * torch.empty((), dtype=dtype).element_size() >= MULTI_TABLE_MIN_BYTES)
-    if table and dtype != torch.float64:
+    if table and (dtype != torch.float64 or acc_in):  # fp64 folds per tensor inside the table call
         with _rings_lock:
             ring = _rings.get(device)
             if ring is None:
@@ -215,7 +215,7 @@ def wsum_multi_ptrs(dtype: torch.dtype, ptrs, out_ptrs, numels, weights: Sequenc
         idx, h, d = ring.take(_lib.wsum_multi_table_bytes(len(out_ptrs), n))
         try:
             _lib.wsum_multi_table_ptrs(code, ptrs, out_ptrs, numels, weights, h.data_ptr(), d.data_ptr(),
-                                       int(s.cuda_stream))
+                                       int(s.cuda_stream), acc_in=acc_in)
         finally:
             ring.done(idx, s)
         return

@@ -1666,18 +1666,20 @@ hipError_t run_pass(const void* const* peers, const double* weights, int n, int6
 
 template <int DT>
 hipError_t run(const void* const* peers, const double* weights, int n, int64_t n_elems, void* out,
-               hipStream_t s, const Launch& l) {
+               hipStream_t s, const Launch& l, bool acc_in = false) {
   // Passes of at most kMaxPeersPerPass peers; pass j > 0 folds its peers into
-  // the running sum held in `out`, so the list order is kept exactly.
+  // the running sum held in `out`, so the list order is kept exactly (acc_in: so does pass 0 —
+  // `out` already holds the fold of earlier peers).
   for (int k0 = 0; k0 < n; k0 += kMaxPeersPerPass) {
     const int m = n - k0 < kMaxPeersPerPass ? n - k0 : kMaxPeersPerPass;
+    const bool acc = acc_in || k0 > 0;
     hipError_t e;
     if (m <= 8)
-      e = run_pass<DT, 8>(peers + k0, weights + k0, m, n_elems, out, s, l, k0 > 0);
+      e = run_pass<DT, 8>(peers + k0, weights + k0, m, n_elems, out, s, l, acc);
     else if (m <= 32)
-      e = run_pass<DT, 32>(peers + k0, weights + k0, m, n_elems, out, s, l, k0 > 0);
+      e = run_pass<DT, 32>(peers + k0, weights + k0, m, n_elems, out, s, l, acc);
     else
-      e = run_pass<DT, kMaxPeersPerPass>(peers + k0, weights + k0, m, n_elems, out, s, l, k0 > 0);
+      e = run_pass<DT, kMaxPeersPerPass>(peers + k0, weights + k0, m, n_elems, out, s, l, acc);
     if (e != hipSuccess) return e;
   }
   return hipSuccess;
@@ -1773,7 +1775,8 @@ hipError_t launch_multi_vec_pass(const MultiIndex* idx, const MultiSeg* segs, in
 
 template <int DT>
 hipError_t run_multi_table(const std::vector<int>& packed, const void* const* peer_ptrs, void* const* outs,
-                           const int64_t* numels, const double* weights, int n, char* th, char* td, hipStream_t s) {
+                           const int64_t* numels, const double* weights, int n, char* th, char* td, hipStream_t s,
+                           bool acc_in) {
   constexpr int per_vec = 2 * Ops<DT>::WE;  // elements per 8-byte vector
   const int m = static_cast<int>(packed.size());
   const int64_t ptab_off = multi_table_bytes(m, n) - static_cast<int64_t>(m) * n * 8;
@@ -1815,8 +1818,9 @@ hipError_t run_multi_table(const std::vector<int>& packed, const void* const* pe
     for (const Launch1& L : launches) {
       const MultiIndex* ix = reinterpret_cast<const MultiIndex*>(td + L.off);
       const MultiSeg* segs = reinterpret_cast<const MultiSeg*>(td + L.off + sizeof(MultiIndex));
-      e = k0 > 0 ? launch_multi_vec_pass<DT, true>(ix, segs, L.mc, L.grid, k0, pm, weights, plain_ok && pm >= 32, s)
-                 : launch_multi_vec_pass<DT, false>(ix, segs, L.mc, L.grid, k0, pm, weights, plain_ok && pm >= 32, s);
+      e = k0 > 0 || acc_in
+              ? launch_multi_vec_pass<DT, true>(ix, segs, L.mc, L.grid, k0, pm, weights, plain_ok && pm >= 32, s)
+              : launch_multi_vec_pass<DT, false>(ix, segs, L.mc, L.grid, k0, pm, weights, plain_ok && pm >= 32, s);
       if (e != hipSuccess) return e;
     }
   }
@@ -1877,7 +1881,7 @@ int elem_size(int dtype) {
 }
 
 int wsum_impl(int dtype, const void* const* peers, const double* weights, int n_peers,
-              int64_t n_elems, void* out, void* stream, const dla_launch_cfg_t* cfg) {
+              int64_t n_elems, void* out, void* stream, const dla_launch_cfg_t* cfg, bool acc_in = false) {
   g_last_error.clear();
   if (elem_size(dtype) == 0) return fail(DLA_E_INVALID, "dla_wsum: unknown dtype " + std::to_string(dtype));
   if (n_peers < 1) return fail(DLA_E_INVALID, "dla_wsum: n_peers must be >= 1 (fedavg.py:20 indexes models[0])");
@@ -1887,7 +1891,10 @@ int wsum_impl(int dtype, const void* const* peers, const double* weights, int n_
   if (!out) return fail(DLA_E_INVALID, "dla_wsum: null out");
   for (int k = 0; k < n_peers; ++k)
     if (!peers[k]) return fail(DLA_E_INVALID, "dla_wsum: null peer pointer " + std::to_string(k));
-  if (n_peers > kMaxPeersPerPass) {
+  if (acc_in) {  // out carries the running sum from the start: it may alias no peer
+    for (int k = 0; k < n_peers; ++k)
+      if (peers[k] == out) return fail(DLA_E_ALIAS, "dla_wsum: out aliases peer " + std::to_string(k) + " (acc_in)");
+  } else if (n_peers > kMaxPeersPerPass) {
     // Multi-pass reduce: out carries the running sum, so it may alias only peers[0].
     for (int k = 1; k < n_peers; ++k)
       if (peers[k] == out)
@@ -1908,10 +1915,10 @@ int wsum_impl(int dtype, const void* const* peers, const double* weights, int n_
   hipStream_t s = static_cast<hipStream_t>(stream);
   hipError_t e;
   switch (dtype) {
-    case DLA_F32: e = run<DLA_F32>(peers, weights, n_peers, n_elems, out, s, l); break;
-    case DLA_BF16: e = run<DLA_BF16>(peers, weights, n_peers, n_elems, out, s, l); break;
-    case DLA_F16: e = run<DLA_F16>(peers, weights, n_peers, n_elems, out, s, l); break;
-    default: e = run<DLA_F64>(peers, weights, n_peers, n_elems, out, s, l); break;
+    case DLA_F32: e = run<DLA_F32>(peers, weights, n_peers, n_elems, out, s, l, acc_in); break;
+    case DLA_BF16: e = run<DLA_BF16>(peers, weights, n_peers, n_elems, out, s, l, acc_in); break;
+    case DLA_F16: e = run<DLA_F16>(peers, weights, n_peers, n_elems, out, s, l, acc_in); break;
+    default: e = run<DLA_F64>(peers, weights, n_peers, n_elems, out, s, l, acc_in); break;
   }
   if (e != hipSuccess) return fail(static_cast<int>(e), std::string("dla_wsum: ") + hipGetErrorString(e));
   return DLA_OK;
@@ -2406,9 +2413,10 @@ int64_t dla_wsum_multi_table_bytes(int n_tensors, int n_peers) {
   return multi_table_bytes(n_tensors, n_peers);
 }
 
-int dla_wsum_multi_table(int dtype, int n_tensors, const void* const* peer_ptrs, void* const* outs,
-                         const int64_t* numels, const double* weights, int n_peers, void* table_host,
-                         void* table_dev, void* stream) {
+namespace {
+int multi_table_impl(int dtype, int n_tensors, const void* const* peer_ptrs, void* const* outs,
+                     const int64_t* numels, const double* weights, int n_peers, bool acc_in, void* table_host,
+                     void* table_dev, void* stream) {
   g_last_error.clear();
   if (n_tensors < 0 || (n_tensors > 0 && (!peer_ptrs || !outs || !numels)))
     return fail(DLA_E_INVALID, "dla_wsum_multi_table: bad tensor table");
@@ -2422,7 +2430,12 @@ int dla_wsum_multi_table(int dtype, int n_tensors, const void* const* peer_ptrs,
     const void* const* row = peer_ptrs + static_cast<int64_t>(t) * n_peers;
     bool ok = dtype != DLA_F64 && outs[t] && (reinterpret_cast<uintptr_t>(outs[t]) & 15u) == 0;
     for (int k = 0; ok && k < n_peers; ++k) ok = row[k] && (reinterpret_cast<uintptr_t>(row[k]) & 15u) == 0;
-    if (ok && n_peers > kMaxPeersPerPass)  // multi-pass: out carries the running sum (as dla_wsum)
+    if (ok && acc_in)  // out carries the running sum from the start (as dla_wsum with acc_in)
+      for (int k = 0; k < n_peers; ++k)
+        if (row[k] == outs[t])
+          return fail(DLA_E_ALIAS, "dla_wsum_multi_table_acc: out of tensor " + std::to_string(t) + " aliases peer " +
+                                       std::to_string(k));
+    if (ok && !acc_in && n_peers > kMaxPeersPerPass)  // multi-pass: out carries the running sum (as dla_wsum)
       for (int k = 1; ok && k < n_peers; ++k)
         if (row[k] == outs[t])
           return fail(DLA_E_ALIAS, "dla_wsum_multi_table: out of tensor " + std::to_string(t) + " aliases peer " +
@@ -2432,7 +2445,7 @@ int dla_wsum_multi_table(int dtype, int n_tensors, const void* const* peer_ptrs,
       packed.push_back(t);
       continue;
     }
-    const int rc = wsum_impl(dtype, row, weights, n_peers, numels[t], outs[t], stream, nullptr);
+    const int rc = wsum_impl(dtype, row, weights, n_peers, numels[t], outs[t], stream, nullptr, acc_in);
     if (rc != DLA_OK) return rc;
   }
   if (packed.empty()) return DLA_OK;
@@ -2447,12 +2460,27 @@ int dla_wsum_multi_table(int dtype, int n_tensors, const void* const* peer_ptrs,
   char* td = static_cast<char*>(table_dev);
   hipError_t e;
   switch (dtype) {
-    case DLA_F32: e = run_multi_table<DLA_F32>(packed, peer_ptrs, outs, numels, weights, n_peers, th, td, s); break;
-    case DLA_BF16: e = run_multi_table<DLA_BF16>(packed, peer_ptrs, outs, numels, weights, n_peers, th, td, s); break;
-    default: e = run_multi_table<DLA_F16>(packed, peer_ptrs, outs, numels, weights, n_peers, th, td, s); break;
+    case DLA_F32: e = run_multi_table<DLA_F32>(packed, peer_ptrs, outs, numels, weights, n_peers, th, td, s, acc_in); break;
+    case DLA_BF16: e = run_multi_table<DLA_BF16>(packed, peer_ptrs, outs, numels, weights, n_peers, th, td, s, acc_in); break;
+    default: e = run_multi_table<DLA_F16>(packed, peer_ptrs, outs, numels, weights, n_peers, th, td, s, acc_in); break;
   }
   if (e != hipSuccess) return fail(static_cast<int>(e), std::string("dla_wsum_multi_table: ") + hipGetErrorString(e));
   return DLA_OK;
+}
+}  // namespace
+
+int dla_wsum_multi_table(int dtype, int n_tensors, const void* const* peer_ptrs, void* const* outs,
+                         const int64_t* numels, const double* weights, int n_peers, void* table_host,
+                         void* table_dev, void* stream) {
+  return multi_table_impl(dtype, n_tensors, peer_ptrs, outs, numels, weights, n_peers, false, table_host, table_dev,
+                          stream);
+}
+
+int dla_wsum_multi_table_acc(int dtype, int n_tensors, const void* const* peer_ptrs, void* const* outs,
+                             const int64_t* numels, const double* weights, int n_peers, int acc_in, void* table_host,
+                             void* table_dev, void* stream) {
+  return multi_table_impl(dtype, n_tensors, peer_ptrs, outs, numels, weights, n_peers, acc_in != 0, table_host,
+                          table_dev, stream);
 }
 
 int dla_plan_create(dla_plan_t** plan, int dtype, const void* const* peers, const double* weights, int n_peers,

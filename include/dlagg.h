@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define DLA_ABI_VERSION 11
+#define DLA_ABI_VERSION 12
 
 /* element dtypes of the peer buffers and of the output */
 #define DLA_F32 0
@@ -169,6 +169,15 @@ int64_t dla_wsum_multi_table_bytes(int n_tensors, int n_peers);
 int dla_wsum_multi_table(int dtype, int n_tensors, const void* const* peer_ptrs, void* const* outs,
                          const int64_t* numels, const double* weights, int n_peers, void* table_host,
                          void* table_dev, void* stream);
+
+/* dla_wsum_multi_table continuing a fold: with acc_in != 0, outs[t] already holds the fold of earlier
+ * peers (fedavg.py:23-25 run over them in list order, in the tensor's dtype) and the n_peers given are
+ * folded into it, so a round of many device-resident models can be launched group by group while the
+ * caller still walks the later models' parameters — the result is the same bits as one call over all
+ * of them.  outs[t] may alias no peer when acc_in != 0.  acc_in == 0 is dla_wsum_multi_table.  ABI v12. */
+int dla_wsum_multi_table_acc(int dtype, int n_tensors, const void* const* peer_ptrs, void* const* outs,
+                             const int64_t* numels, const double* weights, int n_peers, int acc_in, void* table_host,
+                             void* table_dev, void* stream);
 
 /* Replaces scripts/distill.py:124-129 (teacher-logit aggregation,
  * torch.mean(torch.stack(preds), dim=0)) for a whole batch of logits at once:

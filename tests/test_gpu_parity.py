@@ -396,7 +396,8 @@ def test_multi_table_refuses_alias_of_a_later_peer():
 
 
 @pytest.mark.parametrize("name,n,dtype", [("cifar10_resnet8", 64, "f32"), ("cifar10_resnet8", 130, "f32"),
-                                          ("google_speech_resnet34", 40, "bf16")])
+                                          ("google_speech_resnet34", 40, "bf16"),
+                                          ("google_speech_resnet34", 70, "bf16")])
 def test_device_modules_of_real_layouts_through_fedavg(name, n, dtype):
     """FedAvg.aggregate on device-resident modules of the reference layouts (tests/golden/layouts.json)
     with many peers: one pointer table, one launch per 128-peer pass (_device_round); every parameter
@@ -445,6 +446,67 @@ def test_device_modules_of_real_layouts_through_fedavg(name, n, dtype):
     assert same_bits(got, want, dtype)
     assert all(p.is_cuda and p.requires_grad for p in out.parameters())
     assert torch.equal(out.steps, models[0].steps)
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16", "f64"])
+def test_multi_table_accumulate_continues_the_fold(dtype):
+    """dla_wsum_multi_table_acc (ABI v12): the peers folded in two calls — the second continuing from
+    the running sum the outputs hold — give the same bits as one call over all of them (fp64 tensors
+    take the per-tensor fold, an unaligned tensor too); acc_in refuses an output aliasing a peer."""
+    from accdfl_amd import _lib
+    from accdfl_amd.core import wsum
+
+    numels = [1_000_003, 17, 64 * 64 * 3 * 3, 5]
+    g = torch.Generator().manual_seed(73)
+    n = 45
+    peers = [[(torch.randn(m, generator=g) * 0.05).to(TDT[dtype]).cuda() for m in numels] for _ in range(n)]
+    w = [float(x) for x in np.random.default_rng(45).dirichlet(np.ones(n))]
+
+    def ptrs(pl):
+        return [pl[k][t].data_ptr() for t in range(len(numels)) for k in range(len(pl))]
+
+    one = [torch.empty(m, dtype=TDT[dtype], device="cuda") for m in numels]
+    wsum.wsum_multi_ptrs(TDT[dtype], ptrs(peers), [o.data_ptr() for o in one], numels, w, torch.device("cuda", 0))
+    two = [torch.empty(m, dtype=TDT[dtype], device="cuda") for m in numels]
+    wsum.wsum_multi_ptrs(TDT[dtype], ptrs(peers[:32]), [o.data_ptr() for o in two], numels, w[:32],
+                         torch.device("cuda", 0))
+    wsum.wsum_multi_ptrs(TDT[dtype], ptrs(peers[32:]), [o.data_ptr() for o in two], numels, w[32:],
+                         torch.device("cuda", 0), acc_in=True)
+    torch.cuda.synchronize()
+    for t in range(len(numels)):
+        want = fedavg_bits([_bits(peers[k][t].cpu(), dtype) for k in range(n)], w, dtype)
+        assert same_bits(_bits(one[t], dtype), want, dtype), t
+        assert same_bits(_bits(two[t], dtype), want, dtype), t
+    with pytest.raises(_lib.DlaggError):
+        wsum.wsum_multi_ptrs(TDT[dtype], ptrs(peers[:3]), [peers[1][t].data_ptr() for t in range(len(numels))],
+                             numels, w[:3], torch.device("cuda", 0), acc_in=True)
+
+
+def test_device_round_groups_refuse_a_later_layout_mismatch():
+    """A many-model device round walked group by group (_device_round_grouped) whose later group holds a
+    model of another shape falls back to the general path, which refuses it as the reference's add_ would
+    (fedavg.py:25); a matching round of the same size is bit-exact against the oracle."""
+    from torch import nn
+
+    from accdfl_amd.core.gradient_aggregation import fedavg as fa
+
+    def make(k, bad=False):
+        g = torch.Generator().manual_seed(k)
+        m = nn.Module()
+        m.a = nn.Parameter((torch.randn(300, 7, generator=g) * 0.05).cuda())
+        m.b = nn.Parameter((torch.randn(7, 300 if bad else 301, generator=g) * 0.05).cuda())
+        return m
+
+    n = 2 * fa._DEVICE_GROUP + 5
+    w = [float(x) for x in np.random.default_rng(n).dirichlet(np.ones(n))]
+    models = [make(k) for k in range(n)]
+    out = fa.FedAvg.aggregate(models, w)
+    for name in ("a", "b"):
+        want = fedavg_bits([getattr(m, name).detach().reshape(-1).cpu().numpy() for m in models], w, "f32")
+        assert same_bits(getattr(out, name).detach().reshape(-1).cpu().numpy(), want, "f32"), name
+    models[fa._DEVICE_GROUP + 3] = make(999, bad=True)
+    with pytest.raises(RuntimeError):
+        fa.FedAvg.aggregate(models, w)
 
 
 def test_multi_tensor_bf16_gnlenet_shapes_one_launch():
