@@ -474,9 +474,9 @@ def test_multi_table_accumulate_continues_the_fold(dtype):
                          torch.device("cuda", 0), acc_in=True)
     torch.cuda.synchronize()
     for t in range(len(numels)):
-        want = fedavg_bits([_bits(peers[k][t].cpu(), dtype) for k in range(n)], w, dtype)
-        assert same_bits(_bits(one[t], dtype), want, dtype), t
-        assert same_bits(_bits(two[t], dtype), want, dtype), t
+        want = fedavg_bits([gc.as_float(_bits(peers[k][t].cpu(), dtype), dtype) for k in range(n)], w, dtype)
+        assert same_bits(gc.as_float(_bits(one[t], dtype), dtype), want, dtype), t
+        assert same_bits(gc.as_float(_bits(two[t], dtype), dtype), want, dtype), t
     with pytest.raises(_lib.DlaggError):
         wsum.wsum_multi_ptrs(TDT[dtype], ptrs(peers[:3]), [peers[1][t].data_ptr() for t in range(len(numels))],
                              numels, w[:3], torch.device("cuda", 0), acc_in=True)
