@@ -205,7 +205,7 @@ py::list param_views(const at::Tensor& flat, py::list params, const std::vector<
 
 // deepcopy of models[0]'s device buffers (fedavg.py:20 copies them, it does not average them) in one
 // gather per (device, dtype): for each entry of `buffers`, a copy that is a view of one fresh allocation
-// per group (at::cat of the group, then views), or None for an entry that is not a plain dense CPU or
+// per group (views made first, then one fused multi-tensor copy into them), or None for an entry that is not a plain dense CPU or
 // CUDA tensor without grad (the caller deep-copies those) or is alone in its group.  An object listed twice
 // gets one copy (deepcopy's memo); buffers that share a storage are left to deepcopy.  Replaces a Python pass over every buffer (108 BN buffers of a
 // google_speech ResNet-34: ~0.15 ms per round).
@@ -251,16 +251,25 @@ py::list buffer_copies(py::list buffers) {
   for (py::ssize_t i = 0; i < n; ++i) PyList_SET_ITEM(out.ptr(), i, py::none().release().ptr());
   for (const auto& mem : members) {
     if (mem.size() < 2) continue;
-    std::vector<at::Tensor> flat_in;
-    flat_in.reserve(mem.size());
-    for (py::ssize_t i : mem) flat_in.push_back(THPVariable_Unpack(PyList_GET_ITEM(buffers.ptr(), i)).reshape({-1}));
-    const at::Tensor flat = at::cat(flat_in);
-    int64_t off = 0;
+    // one allocation, a contiguous view of it per buffer, then ONE fused multi-tensor copy
+    std::vector<at::Tensor> srcs, dsts;
+    srcs.reserve(mem.size());
+    dsts.reserve(mem.size());
+    int64_t total = 0;
     for (py::ssize_t i : mem) {
-      const at::Tensor& t = THPVariable_Unpack(PyList_GET_ITEM(buffers.ptr(), i));
-      at::Tensor c = flat.narrow(0, off, t.numel()).view(t.sizes());
+      srcs.push_back(THPVariable_Unpack(PyList_GET_ITEM(buffers.ptr(), i)));
+      total += srcs.back().numel();
+    }
+    const at::Tensor flat = at::empty({total}, srcs[0].options());
+    int64_t off = 0;
+    for (const at::Tensor& t : srcs) {
+      dsts.push_back(flat.as_strided(t.sizes(), t.strides(), off));  // contiguous source: contiguous strides
       off += t.numel();
-      PyObject* w = THPVariable_Wrap(c);
+    }
+    at::_foreach_copy_(dsts, srcs);
+    for (size_t j = 0; j < mem.size(); ++j) {
+      const py::ssize_t i = mem[j];
+      PyObject* w = THPVariable_Wrap(dsts[j]);
       if (!w) throw py::error_already_set();
       PyObject* old = PyList_GET_ITEM(out.ptr(), i);
       PyList_SET_ITEM(out.ptr(), i, w);
