@@ -433,28 +433,47 @@ def _device_round(models: List[nn.Module], weights, layout) -> "nn.Module | None
     # while the reduce runs: the result's parameters over `flat` (nn.Parameter views made natively: what
     # torch.Tensor._make_subclass(nn.Parameter, flat.as_strided(...), requires_grad) makes), models[0]'s
     # buffers, the module tree
-    memo = dict(zip(map(id, p0), mod.param_views(flat, p0, offs)))
+    memo = {}
+    mod.param_views(flat, p0, offs, memo)
     _seed_buffers(b0, memo)
     return _clone_value(models[0], memo)
 
 
-# Device rounds of at least 2 x this many models are walked and launched group by group
-# (_device_round_grouped): the walk sees every parameter object once (~35 ns each: 0.49 ms for 128
-# google_speech ResNet-34 models, more than half the 0.87 ms reduce), so one launch after the whole
-# walk leaves the GPU idle that long; 32-model groups let it fold group k while group k+1 is walked.
-_DEVICE_GROUP = 32
+# Device rounds of at least _GROUP_MIN models are walked and launched group by group
+# (_device_round_grouped): the walk sees every parameter object once (~20 ns each: ~0.25 ms for 128
+# google_speech ResNet-34 models), so one launch after the whole walk leaves the GPU idle that long.  The
+# first group is small, so the GPU starts early; each later group is _DEVICE_GROUP_GROWTH times the one
+# before it (a model takes ~2 us to walk and ~7 us to fold, so the next group is walked while the GPU
+# folds the current one), and a tail smaller than the group due joins the last group.  Few groups keep
+# the extra pass over the running sum each later group makes (dla_wsum_multi_table_acc) cheap.
+_DEVICE_GROUP_FIRST = 16
+_DEVICE_GROUP_GROWTH = 3
+_GROUP_MIN_DEFAULT = _GROUP_MIN = 64
+
+
+def _group_bounds(n: int) -> List[tuple]:
+    """[(begin, end)] of the groups a device round of n models is launched in: _DEVICE_GROUP_FIRST
+    models, then _DEVICE_GROUP_GROWTH times as many each group, the last group taking a tail shorter
+    than its due size."""
+    out, a, g = [], 0, _DEVICE_GROUP_FIRST
+    while a < n:
+        b = n if n - a - g < g else a + g
+        out.append((a, b))
+        a, g = b, g * _DEVICE_GROUP_GROWTH
+    return out
 
 
 def _device_round_grouped(models: List[nn.Module], weights) -> "nn.Module | None":
-    """_device_round for a round of many device-resident models, launched group by group: each group of
-    _DEVICE_GROUP models is walked (its own pointer table) and its fold launched at once, the groups
-    after the first continuing the fold in the result (dla_wsum_multi_table_acc) — list order and the
-    rounding of every step unchanged, so the same bits as one launch over all models (fedavg.py:23-25).
-    None when the walk extension is absent or any group does not share models[0]'s layout (dtype,
-    device, shapes); the general path then handles the round."""
+    """_device_round for a round of many device-resident models, launched group by group
+    (_group_bounds): each group is walked (its own pointer table) and its fold launched at once, the
+    groups after the first continuing the fold in the result (dla_wsum_multi_table_acc) — list order
+    and the rounding of every step unchanged, so the same bits as one launch over all models
+    (fedavg.py:23-25).  None when the walk extension is absent or any group does not share
+    models[0]'s layout (dtype, device, shapes); the general path then handles the round."""
     mod = _lib.walk_module()
-    g = _DEVICE_GROUP
-    first = _device_layout(models[:g]) if mod is not None else None
+    bounds = _group_bounds(len(models))
+    a0, b0_ = bounds[0]
+    first = _device_layout(models[a0:b0_]) if mod is not None else None
     if first is None:
         return None
     dtype, device, numels, table = first
@@ -466,17 +485,19 @@ def _device_round_grouped(models: List[nn.Module], weights) -> "nn.Module | None
     offs, total, byte_offs, nums = _flat_plan(dtype, numels)
     flat = torch.empty(total, dtype=dtype, device=device)
     outs = (ctypes.c_void_p * len(numels)).from_buffer(byte_offs + flat.data_ptr())
-    _wsum.wsum_multi_ptrs(dtype, (ctypes.c_void_p * table.size).from_buffer(table), outs, nums, weights[:g], device)
-    for a in range(g, len(models), g):
-        lay = _device_layout(models[a:a + g])
+    _wsum.wsum_multi_ptrs(dtype, (ctypes.c_void_p * table.size).from_buffer(table), outs, nums,
+                          weights[a0:b0_], device)
+    for a, b in bounds[1:]:
+        lay = _device_layout(models[a:b])
         if lay is None or lay[0] is not dtype or lay[1] != device or lay[2] != numels:
             return None
         head = mod.tensors(models[a], _PLAIN_SET)
         if head is None or [p.shape for p in head[0]] != shapes:
             return None
         _wsum.wsum_multi_ptrs(dtype, (ctypes.c_void_p * lay[3].size).from_buffer(lay[3]), outs, nums,
-                              weights[a:a + g], device, acc_in=True)
-    memo = dict(zip(map(id, p0), mod.param_views(flat, p0, offs)))
+                              weights[a:b], device, acc_in=True)
+    memo = {}
+    mod.param_views(flat, p0, offs, memo)
     _seed_buffers(b0, memo)
     return _clone_value(models[0], memo)
 
@@ -488,10 +509,7 @@ def _seed_buffers(buffers, memo: dict) -> None:
     deepcopy.  The walk extension does it in one native call (walk.cpp buffer_copies)."""
     mod = _lib.walk_module()
     if mod is not None:
-        buffers = [b for b in buffers if id(b) not in memo]
-        for b, c in zip(buffers, mod.buffer_copies(buffers)):
-            if c is not None:
-                memo[id(b)] = c
+        mod.buffer_copies(buffers, memo)
         return
     groups: Dict[tuple, list] = {}
     uses: Dict[int, int] = {}
@@ -973,6 +991,9 @@ def reduce_parameters(center_params: List[torch.Tensor], peer_params: List[List[
 # memo, so identity (tied weights, shared submodules) is preserved exactly as deepcopy does.
 _ATOMIC = frozenset({type(None), bool, int, float, complex, str, bytes, torch.dtype, torch.device})
 _plain_module_cls: Dict[type, bool] = {}
+# dicts and OrderedDicts of the tree cloned by the walk extension (walk.cpp clone_dict: the same order
+# and memo, no Python call per seeded entry)
+_NATIVE_DICT_CLONE = True
 
 
 def _plain_module(cls: type) -> bool:
@@ -994,6 +1015,9 @@ def _clone_value(v, memo: dict):
     if y is not memo:
         return y
     if t is dict or t is OrderedDict:
+        mod = _lib.walk_module() if _NATIVE_DICT_CLONE else None
+        if mod is not None:
+            return mod.clone_dict(v, memo, _ATOMIC, _clone_value, OrderedDict)
         y = t()
         memo[id(v)] = y
         get = memo.get
@@ -1008,7 +1032,11 @@ def _clone_value(v, memo: dict):
     if _plain_module(t):
         y = t.__new__(t)
         memo[id(v)] = y
-        state = {k: _clone_value(x, memo) for k, x in v.__dict__.items() if k != "_compiled_call_impl"}
+        mod = _lib.walk_module() if _NATIVE_DICT_CLONE else None
+        if mod is not None:
+            state = mod.clone_dict(v.__dict__, memo, _ATOMIC, _clone_value, OrderedDict, "_compiled_call_impl")
+        else:
+            state = {k: _clone_value(x, memo) for k, x in v.__dict__.items() if k != "_compiled_call_impl"}
         y.__setstate__(state)
         return y
     return copy.deepcopy(v, memo)
@@ -1075,7 +1103,7 @@ class FedAvg(GradientAggregation):
                     if done is not None:
                         return done
                 else:
-                    if len(models) >= 2 * _DEVICE_GROUP and p_first is not None and p_first.is_cuda:
+                    if len(models) >= _GROUP_MIN and p_first is not None and p_first.is_cuda:
                         done = _device_round_grouped(models, list(weights))
                         if done is not None:
                             return done

@@ -24,6 +24,7 @@
 #include <torch/csrc/autograd/python_variable.h>
 #include <pybind11/numpy.h>
 
+#include <algorithm>
 #include <cstdint>
 #include <stdexcept>
 #include <string>
@@ -40,17 +41,62 @@ namespace {
 // Embedded as plain bytes too, so the build's id can be read from the file without loading it.
 __attribute__((used)) const char kWalkIdTag[] = "dlagg-walk-build-id:" DLA_WALK_BUILD_ID;
 
+// The objects one walk has met (modules, parameters): open addressing with linear probing over a
+// power-of-two table of (address, stamp) slots, emptied in O(1) by moving to the next stamp.  A
+// node-based std::unordered_set allocates on every insert, which was most of the walk's cost per parameter.
+class PtrSet {
+ public:
+  PtrSet() : slots_(256) {}
+  void clear() {
+    size_ = 0;
+    if (++stamp_ == 0) {  // stamps wrapped: forget every slot for real
+      std::fill(slots_.begin(), slots_.end(), Slot{});
+      stamp_ = 1;
+    }
+  }
+  // true if `p` was not in the set (and is now)
+  bool insert(PyObject* p) {
+    if (2 * (size_ + 1) > slots_.size()) grow();
+    Slot& s = find(p);
+    if (s.stamp == stamp_) return false;
+    s = Slot{p, stamp_};
+    ++size_;
+    return true;
+  }
+
+ private:
+  struct Slot {
+    PyObject* p = nullptr;
+    uint32_t stamp = 0;
+  };
+  Slot& find(PyObject* p) {
+    const size_t mask = slots_.size() - 1;
+    size_t i = (reinterpret_cast<uintptr_t>(p) >> 4) * 0x9E3779B97F4A7C15ull >> 20 & mask;
+    while (slots_[i].stamp == stamp_ && slots_[i].p != p) i = (i + 1) & mask;
+    return slots_[i];
+  }
+  void grow() {
+    std::vector<Slot> old;
+    old.swap(slots_);
+    slots_.assign(old.size() * 2, Slot{});
+    for (const Slot& s : old)
+      if (s.stamp == stamp_) find(s.p) = s;
+  }
+  std::vector<Slot> slots_;
+  size_t size_ = 0;
+  uint32_t stamp_ = 1;
+};
+
 // One model's parameters in nn.Module.parameters() order (`which` = "_parameters"; "_buffers": its
 // buffers in nn.Module.buffers() order); false if a class is not plain.
-bool walk(PyObject* mod, PyObject* plain, std::unordered_set<PyObject*>& seen_m,
-          std::unordered_set<PyObject*>& seen_p, std::vector<PyObject*>& out, const char* which = "_parameters") {
-  if (seen_m.count(mod)) return true;
+bool walk(PyObject* mod, PyObject* plain, PtrSet& seen_m, PtrSet& seen_p, std::vector<PyObject*>& out,
+          const char* which = "_parameters") {
+  if (!seen_m.insert(mod)) return true;
   const int ok = PySet_Contains(plain, reinterpret_cast<PyObject*>(Py_TYPE(mod)));
   if (ok != 1) {
     if (ok < 0) PyErr_Clear();
     return false;
   }
-  seen_m.insert(mod);
   PyObject* d = PyObject_GenericGetDict(mod, nullptr);  // the instance __dict__ (new reference)
   if (!d) {
     PyErr_Clear();
@@ -63,8 +109,7 @@ bool walk(PyObject* mod, PyObject* plain, std::unordered_set<PyObject*>& seen_m,
     Py_ssize_t pos = 0;
     PyObject *k, *v;
     while (PyDict_Next(params, &pos, &k, &v)) {
-      if (v == Py_None || seen_p.count(v)) continue;
-      seen_p.insert(v);
+      if (v == Py_None || !seen_p.insert(v)) continue;
       out.push_back(v);
     }
     pos = 0;
@@ -94,9 +139,7 @@ py::object layout(py::list models, int device, py::object plain, bool tensor_maj
   std::vector<at::Tensor> p0;  // models[0]'s parameters (the reference layout)
   std::vector<uint64_t> ptrs;
   at::ScalarType dt = at::kFloat;
-  std::unordered_set<PyObject*> seen_m, seen_p;  // per model, cleared (buckets kept) between models
-  seen_m.reserve(512);
-  seen_p.reserve(512);
+  PtrSet seen_m, seen_p;  // per model, cleared (table kept) between models
   for (Py_ssize_t m = 0; m < n; ++m) {
     ps.clear();
     seen_m.clear();
@@ -141,7 +184,7 @@ py::object layout(py::list models, int device, py::object plain, bool tensor_maj
 // Python walk of models[0] (fedavg._device_round).
 py::object tensors(py::object model, py::object plain) {
   if (!PySet_Check(plain.ptr())) return py::none();
-  std::unordered_set<PyObject*> seen_m, seen_p;
+  PtrSet seen_m, seen_p;
   std::vector<PyObject*> ps, bs;
   if (!walk(model.ptr(), plain.ptr(), seen_m, seen_p, ps)) return py::none();
   seen_m.clear();
@@ -179,62 +222,70 @@ py::tuple block_table(py::list blocks) {
   return py::make_tuple(addrs, lens);
 }
 
+// A tensor over `flat`'s storage with the given sizes, strides and element offset: what
+// flat.as_strided(...).detach() returns (same storage, dtype, device and dispatch keys, no view or
+// autograd history, metadata changeable), made as one TensorImpl without the two dispatched ops.
+at::Tensor alias_of(const at::Tensor& flat, at::IntArrayRef sizes, at::IntArrayRef strides, int64_t offset) {
+  auto impl = c10::make_intrusive<c10::TensorImpl>(c10::Storage(flat.storage()), flat.key_set(), flat.dtype());
+  impl->set_sizes_and_strides(sizes, strides, flat.storage_offset() + offset);
+  impl->set_allow_tensor_metadata_change(true);
+  return at::Tensor(std::move(impl));
+}
+
 // The result module's fresh parameters of a device round (fedavg._device_round: deepcopy(models[0]) of
 // fedavg.py:20 with every parameter a view of ONE allocation the reduce writes): for each of models[0]'s
 // parameters p and its element offset in `flat`, an nn.Parameter over flat.as_strided(p's sizes, p's
 // strides, offset) with p's requires_grad — what torch.Tensor._make_subclass(nn.Parameter, view, rg)
 // builds (a detached alias whose metadata may change, wrapped as the Parameter class), without its ~8 us
-// of Python per parameter (110 parameters of a google_speech ResNet-34: ~0.4 ms per round).
-py::list param_views(const at::Tensor& flat, py::list params, const std::vector<int64_t>& offsets) {
+// of Python per parameter (110 parameters of a google_speech ResNet-34: ~0.4 ms per round) — stored
+// straight into the deepcopy memo as memo[id(p)].
+void param_views(const at::Tensor& flat, py::list params, const std::vector<int64_t>& offsets, py::dict memo) {
   const py::ssize_t n = PyList_GET_SIZE(params.ptr());
   if (static_cast<size_t>(n) != offsets.size()) throw std::invalid_argument("param_views: one offset per parameter");
-  py::list out(n);
   for (py::ssize_t i = 0; i < n; ++i) {
     PyObject* o = PyList_GET_ITEM(params.ptr(), i);
     if (!THPVariable_Check(o)) throw std::invalid_argument("param_views: not a tensor");
     const at::Tensor& p = THPVariable_Unpack(o);
-    at::Tensor v = flat.as_strided(p.sizes(), p.strides(), offsets[i]).detach();
-    v.unsafeGetTensorImpl()->set_allow_tensor_metadata_change(true);
+    at::Tensor v = alias_of(flat, p.sizes(), p.strides(), offsets[i]);
     v.set_requires_grad(p.requires_grad());
-    PyObject* w = THPVariable_Wrap(v, reinterpret_cast<PyTypeObject*>(ParameterClass));
+    py::object w = py::reinterpret_steal<py::object>(THPVariable_Wrap(v, reinterpret_cast<PyTypeObject*>(ParameterClass)));
     if (!w) throw py::error_already_set();
-    PyList_SET_ITEM(out.ptr(), i, w);  // steals the reference
+    py::object id = py::reinterpret_steal<py::object>(PyLong_FromVoidPtr(o));
+    if (!id || PyDict_SetItem(memo.ptr(), id.ptr(), w.ptr()) < 0) throw py::error_already_set();
   }
-  return out;
 }
 
 // deepcopy of models[0]'s device buffers (fedavg.py:20 copies them, it does not average them) in one
-// gather per (device, dtype): for each entry of `buffers`, a copy that is a view of one fresh allocation
-// per group (views made first, then one fused multi-tensor copy into them), or None for an entry that is not a plain dense CPU or
-// CUDA tensor without grad (the caller deep-copies those) or is alone in its group.  An object listed twice
-// gets one copy (deepcopy's memo); buffers that share a storage are left to deepcopy.  Replaces a Python pass over every buffer (108 BN buffers of a
-// google_speech ResNet-34: ~0.15 ms per round).
-py::list buffer_copies(py::list buffers) {
+// gather per (device, dtype), stored into the deepcopy memo: for each entry of `buffers` not already in
+// `memo`, memo[id(buffer)] = a copy that is a view of one fresh allocation per group (views made first,
+// then one fused multi-tensor copy into them).  Entries that are not plain dense CPU or CUDA tensors
+// without grad, alone in their group, or sharing a storage with another buffer get no entry (the caller's
+// deepcopy copies them, keeping the sharing).  Replaces a Python pass over every buffer (108 BN buffers
+// of a google_speech ResNet-34: ~0.15 ms per round).
+void buffer_copies(py::list buffers, py::dict memo) {
   const py::ssize_t n = PyList_GET_SIZE(buffers.ptr());
-  std::vector<int> group(n, -1);
   std::vector<std::pair<int, int>> keys;  // (device index, scalar type) of each group
   std::vector<std::vector<py::ssize_t>> members;
-  std::unordered_map<PyObject*, py::ssize_t> first_of;
-  std::vector<py::ssize_t> alias(n, -1);
+  std::vector<py::object> ids(n);
+  std::unordered_set<PyObject*> seen;
+  std::vector<char> take(n, 0);
   // tensors sharing a storage keep the stock deepcopy, which keeps them sharing one
   std::unordered_map<const void*, int> storage_uses;
   for (py::ssize_t i = 0; i < n; ++i) {
     PyObject* o = PyList_GET_ITEM(buffers.ptr(), i);
-    if (Py_TYPE(o) != reinterpret_cast<PyTypeObject*>(THPVariableClass)) continue;
+    if (Py_TYPE(o) != reinterpret_cast<PyTypeObject*>(THPVariableClass) || !seen.insert(o).second) continue;
+    ids[i] = py::reinterpret_steal<py::object>(PyLong_FromVoidPtr(o));
+    if (!ids[i]) throw py::error_already_set();
+    const int in_memo = PyDict_Contains(memo.ptr(), ids[i].ptr());
+    if (in_memo < 0) throw py::error_already_set();
+    if (in_memo) continue;
+    take[i] = 1;
     const at::Tensor& t = THPVariable_Unpack(o);
-    if (t.has_storage() && first_of.emplace(o, i).second) ++storage_uses[t.storage().unsafeGetStorageImpl()];
+    if (t.has_storage()) ++storage_uses[t.storage().unsafeGetStorageImpl()];
   }
-  first_of.clear();
   for (py::ssize_t i = 0; i < n; ++i) {
-    PyObject* o = PyList_GET_ITEM(buffers.ptr(), i);
-    if (Py_TYPE(o) != reinterpret_cast<PyTypeObject*>(THPVariableClass)) continue;
-    auto it = first_of.find(o);
-    if (it != first_of.end()) {
-      alias[i] = it->second;
-      continue;
-    }
-    first_of.emplace(o, i);
-    const at::Tensor& t = THPVariable_Unpack(o);
+    if (!take[i]) continue;
+    const at::Tensor& t = THPVariable_Unpack(PyList_GET_ITEM(buffers.ptr(), i));
     if (t.requires_grad() || !t.is_contiguous() || !t.has_storage() || !(t.is_cuda() || t.is_cpu())) continue;
     if (storage_uses[t.storage().unsafeGetStorageImpl()] > 1) continue;
     const std::pair<int, int> key{t.get_device(), static_cast<int>(t.scalar_type())};
@@ -244,11 +295,8 @@ py::list buffer_copies(py::list buffers) {
       keys.push_back(key);
       members.emplace_back();
     }
-    group[i] = static_cast<int>(g);
     members[g].push_back(i);
   }
-  py::list out(n);
-  for (py::ssize_t i = 0; i < n; ++i) PyList_SET_ITEM(out.ptr(), i, py::none().release().ptr());
   for (const auto& mem : members) {
     if (mem.size() < 2) continue;
     // one allocation, a contiguous view of it per buffer, then ONE fused multi-tensor copy
@@ -263,28 +311,205 @@ py::list buffer_copies(py::list buffers) {
     const at::Tensor flat = at::empty({total}, srcs[0].options());
     int64_t off = 0;
     for (const at::Tensor& t : srcs) {
-      dsts.push_back(flat.as_strided(t.sizes(), t.strides(), off));  // contiguous source: contiguous strides
+      dsts.push_back(alias_of(flat, t.sizes(), t.strides(), off));  // contiguous source: contiguous strides
       off += t.numel();
     }
     at::_foreach_copy_(dsts, srcs);
     for (size_t j = 0; j < mem.size(); ++j) {
-      const py::ssize_t i = mem[j];
-      PyObject* w = THPVariable_Wrap(dsts[j]);
-      if (!w) throw py::error_already_set();
-      PyObject* old = PyList_GET_ITEM(out.ptr(), i);
-      PyList_SET_ITEM(out.ptr(), i, w);
-      Py_DECREF(old);
+      py::object w = py::reinterpret_steal<py::object>(THPVariable_Wrap(dsts[j]));
+      if (!w || PyDict_SetItem(memo.ptr(), ids[mem[j]].ptr(), w.ptr()) < 0) throw py::error_already_set();
     }
   }
-  for (py::ssize_t i = 0; i < n; ++i)
-    if (alias[i] >= 0) {
-      PyObject* c = PyList_GET_ITEM(out.ptr(), alias[i]);
-      Py_INCREF(c);
-      PyObject* old = PyList_GET_ITEM(out.ptr(), i);
-      PyList_SET_ITEM(out.ptr(), i, c);
-      Py_DECREF(old);
+}
+
+// One value of the module-tree clone (fedavg._clone_value's order): the memo's copy if it holds one
+// (seeded parameters and buffers, objects met before), the value itself if its type is atomic, a new
+// dict / OrderedDict through clone_mapping, else fallback(value, memo) — the Python restatement of
+// deepcopy's protocol.  New reference, or nullptr with the Python error set.
+PyObject* clone_mapping(PyObject* v, PyObject* memo, PyObject* atomic, PyObject* fallback, PyObject* odict,
+                        PyObject* skip = nullptr);
+
+PyObject* clone_sequence(PyObject* x, PyObject* memo, PyObject* atomic, PyObject* fallback, PyObject* odict);
+
+PyObject* clone_one(PyObject* x, PyObject* memo, PyObject* atomic, PyObject* fallback, PyObject* odict) {
+  PyObject* key = PyLong_FromVoidPtr(x);
+  if (!key) return nullptr;
+  PyObject* hit = PyDict_GetItemWithError(memo, key);  // borrowed
+  Py_DECREF(key);
+  if (hit) return Py_NewRef(hit);
+  if (PyErr_Occurred()) return nullptr;
+  const int at = PySet_Contains(atomic, reinterpret_cast<PyObject*>(Py_TYPE(x)));
+  if (at < 0) return nullptr;
+  if (at) return Py_NewRef(x);
+  if (PyDict_CheckExact(x) || Py_TYPE(x) == reinterpret_cast<PyTypeObject*>(odict))
+    return clone_mapping(x, memo, atomic, fallback, odict);
+  if (PyTuple_CheckExact(x) || PyList_CheckExact(x)) return clone_sequence(x, memo, atomic, fallback, odict);
+  if (PySet_CheckExact(x) && PySet_GET_SIZE(x) == 0) {  // _non_persistent_buffers_set: a new empty set
+    PyObject* y = PySet_New(nullptr);
+    PyObject* id = y ? PyLong_FromVoidPtr(x) : nullptr;
+    const int rc = id ? PyDict_SetItem(memo, id, y) : -1;
+    Py_XDECREF(id);
+    if (rc < 0) {
+      Py_XDECREF(y);
+      return nullptr;
     }
-  return out;
+    return y;
+  }
+  return PyObject_CallFunctionObjArgs(fallback, x, memo, nullptr);
+}
+
+// A tuple or list (a conv's kernel_size / stride / padding, _reversed_padding_repeated_twice), as
+// copy.deepcopy copies them: a list is a new list registered in the memo before its items; a tuple is
+// itself when every item clones to itself (tuples of numbers), else a new tuple registered in the memo.
+PyObject* clone_sequence(PyObject* x, PyObject* memo, PyObject* atomic, PyObject* fallback, PyObject* odict) {
+  PyObject* id = PyLong_FromVoidPtr(x);
+  if (!id) return nullptr;
+  if (PyList_CheckExact(x)) {
+    PyObject* y = PyList_New(0);
+    if (!y || PyDict_SetItem(memo, id, y) < 0) {
+      Py_XDECREF(y);
+      Py_DECREF(id);
+      return nullptr;
+    }
+    Py_DECREF(id);
+    for (Py_ssize_t i = 0; i < PyList_GET_SIZE(x); ++i) {
+      PyObject* item = Py_NewRef(PyList_GET_ITEM(x, i));
+      PyObject* c = clone_one(item, memo, atomic, fallback, odict);
+      Py_DECREF(item);
+      if (!c || PyList_Append(y, c) < 0) {
+        Py_XDECREF(c);
+        Py_DECREF(y);
+        return nullptr;
+      }
+      Py_DECREF(c);
+    }
+    return y;
+  }
+  const Py_ssize_t n = PyTuple_GET_SIZE(x);
+  PyObject* y = PyTuple_New(n);
+  if (!y) {
+    Py_DECREF(id);
+    return nullptr;
+  }
+  bool same = true;
+  for (Py_ssize_t i = 0; i < n; ++i) {
+    PyObject* c = clone_one(PyTuple_GET_ITEM(x, i), memo, atomic, fallback, odict);
+    if (!c) {
+      Py_DECREF(y);
+      Py_DECREF(id);
+      return nullptr;
+    }
+    same = same && c == PyTuple_GET_ITEM(x, i);
+    PyTuple_SET_ITEM(y, i, c);
+  }
+  if (same) {
+    Py_DECREF(y);
+    Py_DECREF(id);
+    return Py_NewRef(x);
+  }
+  // an item's copy may have copied this tuple already (a cycle through a mutable item): use that one
+  PyObject* prev = PyDict_GetItemWithError(memo, id);
+  if (prev || PyErr_Occurred()) {
+    Py_DECREF(y);
+    Py_DECREF(id);
+    return prev ? Py_NewRef(prev) : nullptr;
+  }
+  const int rc = PyDict_SetItem(memo, id, y);
+  Py_DECREF(id);
+  if (rc < 0) {
+    Py_DECREF(y);
+    return nullptr;
+  }
+  return y;
+}
+
+// A dict or OrderedDict of the module tree (a module's _parameters, _buffers, _modules, hook
+// dicts): a new mapping of the same type registered in the memo first (deepcopy's order, so a cycle
+// finds it), then every entry in iteration order with its value cloned by clone_one and a non-atomic
+// key through fallback; a str key equal to `skip` (when given) is left out.
+PyObject* clone_mapping(PyObject* v, PyObject* memo, PyObject* atomic, PyObject* fallback, PyObject* odict,
+                        PyObject* skip) {
+  // an empty OrderedDict (a module's hook dicts) iterates like a dict: no items() view needed
+  const bool exact = PyDict_CheckExact(v);
+  const bool plain_iter = exact || PyDict_GET_SIZE(v) == 0;
+  PyObject* y = exact ? PyDict_New() : PyObject_CallNoArgs(reinterpret_cast<PyObject*>(Py_TYPE(v)));
+  if (!y) return nullptr;
+  PyObject* id = PyLong_FromVoidPtr(v);
+  if (!id || PyDict_SetItem(memo, id, y) < 0) {
+    Py_XDECREF(id);
+    Py_DECREF(y);
+    return nullptr;
+  }
+  Py_DECREF(id);
+  auto put = [&](PyObject* k, PyObject* x) -> bool {
+    if (skip && PyUnicode_Check(k) && PyUnicode_Compare(k, skip) == 0) return true;
+    const int at = PySet_Contains(atomic, reinterpret_cast<PyObject*>(Py_TYPE(k)));
+    if (at < 0) return false;
+    PyObject* kc = at ? Py_NewRef(k) : PyObject_CallFunctionObjArgs(fallback, k, memo, nullptr);
+    if (!kc) return false;
+    PyObject* c = clone_one(x, memo, atomic, fallback, odict);
+    const int rc = c ? (exact ? PyDict_SetItem(y, kc, c) : PyObject_SetItem(y, kc, c)) : -1;
+    Py_DECREF(kc);
+    Py_XDECREF(c);
+    return rc == 0;
+  };
+  bool ok = true;
+  if (plain_iter) {
+    // entries are cloned into another dict, so `v` is not resized by the loop; a fallback that
+    // mutated it would be caught by the size check
+    const Py_ssize_t size = PyDict_GET_SIZE(v);
+    Py_ssize_t pos = 0;
+    PyObject *k, *x;
+    while (ok && PyDict_Next(v, &pos, &k, &x)) {
+      Py_INCREF(k);
+      Py_INCREF(x);
+      ok = put(k, x);
+      Py_DECREF(k);
+      Py_DECREF(x);
+      if (ok && PyDict_GET_SIZE(v) != size) {
+        PyErr_SetString(PyExc_RuntimeError, "dictionary changed size during iteration");
+        ok = false;
+      }
+    }
+  } else {
+    static PyObject* const items_name = PyUnicode_InternFromString("items");
+    PyObject* items = PyObject_CallMethodNoArgs(v, items_name);
+    PyObject* it = items ? PyObject_GetIter(items) : nullptr;
+    Py_XDECREF(items);
+    ok = it != nullptr;
+    while (ok) {
+      PyObject* kv = PyIter_Next(it);
+      if (!kv) {
+        ok = !PyErr_Occurred();
+        break;
+      }
+      ok = PyTuple_Check(kv) && PyTuple_GET_SIZE(kv) == 2 && put(PyTuple_GET_ITEM(kv, 0), PyTuple_GET_ITEM(kv, 1));
+      Py_DECREF(kv);
+    }
+    Py_XDECREF(it);
+  }
+  if (!ok) {
+    Py_DECREF(y);
+    return nullptr;
+  }
+  return y;
+}
+
+// fedavg._clone_value for a dict / OrderedDict (`v`) of the result module's tree, in native code: the
+// mapping's entries are looked up in the deepcopy memo without a Python call each (a google_speech
+// ResNet-34's _parameters and _buffers hold 218 seeded entries).  `atomic`: the set of types copied as
+// themselves; `fallback(obj, memo)`: _clone_value, for every value neither seeded nor atomic nor a
+// mapping, and for non-atomic keys (hashable: _clone_value copies them as deepcopy does); `odict`:
+// collections.OrderedDict; `skip`: a key left out (a module __dict__'s _compiled_call_impl), or None.
+py::object clone_dict(py::object v, py::dict memo, py::object atomic, py::object fallback, py::object odict,
+                      py::object skip) {
+  if (!PyAnySet_Check(atomic.ptr()) || !(PyDict_CheckExact(v.ptr()) || Py_TYPE(v.ptr()) == reinterpret_cast<PyTypeObject*>(odict.ptr())))
+    throw std::invalid_argument("clone_dict: a dict or OrderedDict and a set of atomic types");
+  if (!skip.is_none() && !PyUnicode_Check(skip.ptr())) throw std::invalid_argument("clone_dict: skip is a str or None");
+  PyObject* y = clone_mapping(v.ptr(), memo.ptr(), atomic.ptr(), fallback.ptr(), odict.ptr(),
+                              skip.is_none() ? nullptr : skip.ptr());
+  if (!y) throw py::error_already_set();
+  return py::reinterpret_steal<py::object>(y);
 }
 
 }  // namespace
@@ -294,7 +519,9 @@ PYBIND11_MODULE(_dla_walk, m) {
   m.def("layout", &layout, py::arg("models"), py::arg("device"), py::arg("plain"), py::arg("tensor_major"));
   m.def("tensors", &tensors, py::arg("model"), py::arg("plain"));
   m.def("block_table", &block_table, py::arg("blocks"));
-  m.def("param_views", &param_views, py::arg("flat"), py::arg("params"), py::arg("offsets"));
-  m.def("buffer_copies", &buffer_copies, py::arg("buffers"));
+  m.def("param_views", &param_views, py::arg("flat"), py::arg("params"), py::arg("offsets"), py::arg("memo"));
+  m.def("buffer_copies", &buffer_copies, py::arg("buffers"), py::arg("memo"));
+  m.def("clone_dict", &clone_dict, py::arg("v"), py::arg("memo"), py::arg("atomic"), py::arg("fallback"),
+        py::arg("odict"), py::arg("skip") = py::none());
   m.attr("build_id") = py::str(kWalkIdTag + sizeof("dlagg-walk-build-id:") - 1);
 }

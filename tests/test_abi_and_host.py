@@ -5,6 +5,7 @@ import ctypes
 import os
 import re
 import time
+from collections import OrderedDict
 
 import pytest
 import torch
@@ -244,6 +245,18 @@ class _OddModule(nn.Module):
         self.register_buffer("steps", torch.tensor(5))
         self.register_buffer("np", torch.zeros(2), persistent=False)
         self.fh = self.register_forward_hook(lambda m, i, o: None)
+        # containers the native clone (walk.cpp clone_dict) copies itself: a tuple holding a mutable
+        # item (a new tuple), a list holding itself, an OrderedDict out of insertion order, a tuple
+        # key, a shared tuple of numbers, an empty set
+        self.mixed = (1, [2, 3], "s")
+        self.loop = [4]
+        self.loop.append(self.loop)
+        self.od = OrderedDict([("x", 1), ("y", [5]), ("z", 3)])
+        self.od.move_to_end("x")
+        self.tk = {(1, 2): "a", "b": self.mixed}
+        self.nums = (7, 8)
+        self.nums2 = self.nums
+        self.empty = set()
 
 
 def _same_structure(x, y, seen):
@@ -272,20 +285,33 @@ def _same_structure(x, y, seen):
         assert x == y
 
 
-def test_center_copy_is_a_deepcopy():
+@pytest.mark.parametrize("native", [True, False], ids=["native_clone", "python_clone"])
+def test_center_copy_is_a_deepcopy(native, monkeypatch):
     """The result module (fedavg.py:20 copy.deepcopy(models[0])) built by _center_copy's module
     clone matches copy.deepcopy attribute for attribute: same types and key order, fresh
     objects, buffers equal, identity preserved (tied weights, a dict shared by two attributes),
-    parameters fresh with the same requires_grad, and the copy runs."""
+    parameters fresh with the same requires_grad, and the copy runs — with the tree's dicts,
+    tuples and lists cloned by the walk extension (walk.cpp clone_dict) and in Python."""
     import copy
 
+    from accdfl_amd import _lib
+    from accdfl_amd.core.gradient_aggregation import fedavg as fa
     from accdfl_amd.core.gradient_aggregation.fedavg import _center_copy
 
+    if native and _lib.walk_module() is None:
+        pytest.skip("walk extension not built")
+    monkeypatch.setattr(fa, "_NATIVE_DICT_CLONE", native)
     m = _OddModule()
     want = copy.deepcopy(m)
     got = _center_copy(m, large=False)
     _same_structure(want, got, set())
     assert got.tied is got.enc and got.lst[0] is got.cfg and got.cfg is not m.cfg
+    assert got.mixed is not m.mixed and got.mixed[1] is not m.mixed[1] and got.mixed == m.mixed
+    assert got.tk["b"] is got.mixed and list(got.tk) == [(1, 2), "b"]
+    assert got.loop is not m.loop and got.loop[1] is got.loop and got.loop[0] == 4
+    assert type(got.od) is OrderedDict and list(got.od) == ["y", "z", "x"] and got.od["y"] is not m.od["y"]
+    assert got.nums is m.nums and got.nums2 is got.nums  # deepcopy keeps tuples of numbers
+    assert got.empty == set() and got.empty is not m.empty
     assert len(got._forward_hooks) == 1 and got._forward_hooks is not m._forward_hooks
     assert [p.requires_grad for p in got.parameters()] == [p.requires_grad for p in m.parameters()]
     assert all(p is not q for p, q in zip(got.parameters(), m.parameters()))
@@ -663,3 +689,67 @@ def test_native_walk_matches_the_python_walk():
     assert [id(p) for p in ps] == [id(p) for p in m0.parameters()]
     assert [id(b) for b in bs] == [id(b) for b in m0.buffers()]
     assert _lib.walk_module().tensors(m0, set()) is None  # a class outside the plain set
+
+
+def test_device_round_group_schedule():
+    """_group_bounds (fedavg._device_round_grouped): contiguous groups covering every model in list
+    order, the first _DEVICE_GROUP_FIRST models, each later group _DEVICE_GROUP_GROWTH times the
+    previous one except the last, which takes a tail shorter than its due size."""
+    from accdfl_amd.core.gradient_aggregation import fedavg as fa
+
+    f, k = fa._DEVICE_GROUP_FIRST, fa._DEVICE_GROUP_GROWTH
+    if (f, k) == (16, 3):
+        assert fa._group_bounds(128) == [(0, 16), (16, 64), (64, 128)]
+        assert fa._group_bounds(64) == [(0, 16), (16, 64)]
+    for n in range(1, 3000):
+        b = fa._group_bounds(n)
+        assert b[0][0] == 0 and b[-1][1] == n
+        assert all(x[1] == y[0] for x, y in zip(b, b[1:]))
+        sizes = [e - a for a, e in b]
+        assert all(s > 0 for s in sizes)
+        assert all(s == f * k ** i for i, s in enumerate(sizes[:-1]))
+        due = f * k ** (len(sizes) - 1)
+        assert sizes[-1] < 2 * due
+
+
+def test_walk_memo_seeding_on_cpu():
+    """walk.cpp param_views / buffer_copies store their copies straight into the deepcopy memo:
+    parameters as nn.Parameter views of one allocation (offsets, strides, requires_grad kept);
+    buffers copied per (device, dtype) group, skipping entries already in the memo, objects listed
+    twice (one copy), storage-sharing, grad-requiring, non-contiguous and lone-in-group buffers."""
+    from accdfl_amd import _lib
+
+    mod = _lib.walk_module()
+    if mod is None:
+        pytest.skip("walk extension not built")
+    p = [nn.Parameter(torch.randn(3, 4)), nn.Parameter(torch.randn(5), requires_grad=False)]
+    flat = torch.arange(40, dtype=torch.float32)
+    memo = {}
+    mod.param_views(flat, p, [0, 16], memo)
+    assert set(memo) == {id(x) for x in p}
+    v0, v1 = memo[id(p[0])], memo[id(p[1])]
+    assert type(v0) is nn.Parameter and v0.shape == (3, 4) and v0.requires_grad and not v1.requires_grad
+    assert torch.equal(v0.detach().reshape(-1), flat[:12]) and torch.equal(v1.detach(), flat[16:21])
+    assert v0.data_ptr() == flat.data_ptr() and v1.data_ptr() == flat.data_ptr() + 64
+    a, b, c = torch.randn(4), torch.randn(6), torch.arange(3)
+    d = torch.arange(2)
+    shared = torch.randn(8)
+    view = shared[2:5]
+    grad = torch.randn(3, requires_grad=True)
+    strided = torch.randn(4, 4)[:, 1]
+    seeded = torch.randn(2)
+    bufs = [a, b, a, c, d, shared, view, grad, strided, seeded]
+    memo = {id(seeded): "kept"}
+    mod.buffer_copies(bufs, memo)
+    assert memo[id(seeded)] == "kept"
+    for x in (a, b, c, d):
+        y = memo[id(x)]
+        assert torch.equal(x, y) and y.dtype == x.dtype and y.data_ptr() != x.data_ptr()
+    assert memo[id(a)].untyped_storage().data_ptr() == memo[id(b)].untyped_storage().data_ptr()
+    assert memo[id(c)].untyped_storage().data_ptr() == memo[id(d)].untyped_storage().data_ptr()
+    for x in (shared, view, grad, strided):
+        assert id(x) not in memo
+    lone = torch.randn(2, dtype=torch.float64)
+    memo = {}
+    mod.buffer_copies([lone, a], memo)
+    assert memo == {}  # each alone in its (device, dtype) group: left to deepcopy

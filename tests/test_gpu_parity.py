@@ -497,14 +497,18 @@ def test_device_round_groups_refuse_a_later_layout_mismatch():
         m.b = nn.Parameter((torch.randn(7, 300 if bad else 301, generator=g) * 0.05).cuda())
         return m
 
-    n = 2 * fa._DEVICE_GROUP + 5
+    n = fa._GROUP_MIN  # the smallest grouped round with the first launch and two continuing the fold
+    while len(fa._group_bounds(n)) < 3:
+        n += 1
+    n += 5
+    bounds = fa._group_bounds(n)
     w = [float(x) for x in np.random.default_rng(n).dirichlet(np.ones(n))]
     models = [make(k) for k in range(n)]
     out = fa.FedAvg.aggregate(models, w)
     for name in ("a", "b"):
         want = fedavg_bits([getattr(m, name).detach().reshape(-1).cpu().numpy() for m in models], w, "f32")
         assert same_bits(getattr(out, name).detach().reshape(-1).cpu().numpy(), want, "f32"), name
-    models[fa._DEVICE_GROUP + 3] = make(999, bad=True)
+    models[bounds[-1][0] + 3] = make(999, bad=True)
     with pytest.raises(RuntimeError):
         fa.FedAvg.aggregate(models, w)
 
