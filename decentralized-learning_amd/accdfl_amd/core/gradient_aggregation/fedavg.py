@@ -272,7 +272,7 @@ def _plain_walk(cls: type) -> bool:
 
 def _native_layout(models: List[nn.Module], device: int, tensor_major: bool):
     """The walk extension's one-pass layout (csrc/walk.cpp; ~10x faster per parameter than the Python
-    walk): (dtype, numels, pointer table bytes, device index), or None when the extension is not
+    walk): (dtype, numels, pointer table bytearray, device index), or None when the extension is not
     loaded or the round does not qualify.  Classes it has not seen are classified (models[0]'s tree)
     and the walk retried once."""
     mod = _lib.walk_module()
@@ -323,7 +323,7 @@ def _host_layout(models: List[nn.Module]):
     nat = _native_layout(models, -1, tensor_major=False)
     if nat is not None:
         dtype, numels, table, _ = nat
-        return dtype, numels, (ctypes.c_void_p * (len(table) // 8)).from_buffer_copy(table)
+        return dtype, numels, (ctypes.c_void_p * (len(table) // 8)).from_buffer(table)
     p0 = _parameters(models[0])
     if not p0:
         return None
@@ -356,7 +356,7 @@ def _device_layout(models: List[nn.Module]):
     if nat is not None:
         dtype, numels, table, dev = nat
         return (dtype, torch.device("cuda", dev), numels,
-                np.frombuffer(table, dtype=np.uint64).reshape(len(numels), len(models)).copy())
+                np.frombuffer(table, dtype=np.uint64).reshape(len(numels), len(models)))
     p0 = _parameters(models[0])
     if not p0 or not p0[0].is_cuda:
         return None
@@ -421,15 +421,19 @@ def _device_round(models: List[nn.Module], weights, layout) -> "nn.Module | None
     module tree is cloned while the kernel runs."""
     dtype, device, numels, table = layout
     mod = _lib.walk_module()
-    objs = mod.tensors(models[0], _PLAIN_SET) if mod is not None else None
-    if objs is None or len(objs[0]) != len(numels) or any(type(p) is not nn.Parameter for p in objs[0]):
+    if mod is None:
         return _device_round_per_tensor(models, weights, layout)
-    p0, b0 = objs
     offs, total, byte_offs, nums = _flat_plan(dtype, numels)
     flat = torch.empty(total, dtype=dtype, device=device)
     ptrs = (ctypes.c_void_p * table.size).from_buffer(table)
     outs = (ctypes.c_void_p * len(numels)).from_buffer(byte_offs + flat.data_ptr())
     _wsum.wsum_multi_ptrs(dtype, ptrs, outs, nums, weights, device)
+    # models[0]'s own objects, checked after the launch (the GPU starts sooner; a tree the result cannot be
+    # built over leaves `flat` unused, and the per-tensor path launches into its own tensors)
+    objs = mod.tensors(models[0], _PLAIN_SET)
+    if objs is None or len(objs[0]) != len(numels) or any(type(p) is not nn.Parameter for p in objs[0]):
+        return _device_round_per_tensor(models, weights, layout)
+    p0, b0 = objs
     # while the reduce runs: the result's parameters over `flat` (nn.Parameter views made natively: what
     # torch.Tensor._make_subclass(nn.Parameter, flat.as_strided(...), requires_grad) makes), models[0]'s
     # buffers, the module tree
@@ -477,16 +481,17 @@ def _device_round_grouped(models: List[nn.Module], weights) -> "nn.Module | None
     if first is None:
         return None
     dtype, device, numels, table = first
-    objs = mod.tensors(models[0], _PLAIN_SET)
-    if objs is None or len(objs[0]) != len(numels) or any(type(p) is not nn.Parameter for p in objs[0]):
-        return None
-    p0, b0 = objs
-    shapes = [p.shape for p in p0]
     offs, total, byte_offs, nums = _flat_plan(dtype, numels)
     flat = torch.empty(total, dtype=dtype, device=device)
     outs = (ctypes.c_void_p * len(numels)).from_buffer(byte_offs + flat.data_ptr())
     _wsum.wsum_multi_ptrs(dtype, (ctypes.c_void_p * table.size).from_buffer(table), outs, nums,
                           weights[a0:b0_], device)
+    # checked after the first launch, so the GPU starts sooner (a failed check leaves `flat` unused)
+    objs = mod.tensors(models[0], _PLAIN_SET)
+    if objs is None or len(objs[0]) != len(numels) or any(type(p) is not nn.Parameter for p in objs[0]):
+        return None
+    p0, b0 = objs
+    shapes = [p.shape for p in p0]
     for a, b in bounds[1:]:
         lay = _device_layout(models[a:b])
         if lay is None or lay[0] is not dtype or lay[1] != device or lay[2] != numels:

@@ -13,7 +13,7 @@
 // before skipped — for module classes in `plain` (classes that keep nn.Module's own walk; the caller
 // decides and caches that).  It returns None when a model's tree holds another class or the round
 // does not qualify (then the caller's general path handles it), else
-//     (dtype name, [numel of each of models[0]'s parameters], pointer table bytes, device index)
+//     (dtype name, [numel of each of models[0]'s parameters], pointer table bytearray, device index)
 // with the table tensor-major ([n_tensors][n_models] uint64) or peer-major ([n_models][n_tensors]).
 // `device`: -1 for CPU parameters, a HIP device index every parameter must be on, or -2 for the HIP
 // device of models[0]'s first parameter (the returned device index; -1 for CPU).
@@ -175,7 +175,8 @@ py::object layout(py::list models, int device, py::object plain, bool tensor_maj
   }
   py::list numels;
   for (const at::Tensor& x : p0) numels.append(x.numel());
-  py::bytes table(reinterpret_cast<const char*>(ptrs.data()), ptrs.size() * sizeof(uint64_t));
+  // writable, so the caller's ctypes / numpy views of it need no copy
+  py::bytearray table(reinterpret_cast<const char*>(ptrs.data()), ptrs.size() * sizeof(uint64_t));
   return py::make_tuple(py::str(dtype_name(dt)), numels, table, device);
 }
 
