@@ -270,7 +270,7 @@ def _plain_walk(cls: type) -> bool:
     return ok
 
 
-def _native_layout(models: List[nn.Module], device: int, tensor_major: bool):
+def _native_layout(models: List[nn.Module], device: int, tensor_major: bool, ref: "nn.Module | None" = None):
     """The walk extension's one-pass layout (csrc/walk.cpp; ~10x faster per parameter than the Python
     walk): (dtype, numels, pointer table bytearray, device index), or None when the extension is not
     loaded or the round does not qualify.  Classes it has not seen are classified (models[0]'s tree)
@@ -278,11 +278,11 @@ def _native_layout(models: List[nn.Module], device: int, tensor_major: bool):
     mod = _lib.walk_module()
     if mod is None:
         return None
-    r = mod.layout(models, device, _PLAIN_SET, tensor_major)
+    r = mod.layout(models, device, _PLAIN_SET, tensor_major, ref)
     if r is None:
-        fresh = [type(sub) for sub in models[0].modules() if type(sub) not in _plain_walk_cls]
+        fresh = [type(sub) for sub in (models[0] if ref is None else ref).modules() if type(sub) not in _plain_walk_cls]
         if any([_plain_walk(cls) for cls in fresh]):
-            r = mod.layout(models, device, _PLAIN_SET, tensor_major)
+            r = mod.layout(models, device, _PLAIN_SET, tensor_major, ref)
     if r is None:
         return None
     name, numels, table, dev = r
@@ -345,18 +345,21 @@ def _host_layout(models: List[nn.Module]):
     return dtype, [p.numel() for p in p0], (ctypes.c_void_p * len(ptrs))(*ptrs)
 
 
-def _device_layout(models: List[nn.Module]):
+def _device_layout(models: List[nn.Module], ref: "nn.Module | None" = None):
     """(dtype, device, numels, tensor-major pointer table) of a round whose models all have models[0]'s
-    parameter shapes, one supported dtype and contiguous storage on ONE HIP device (models trained on
-    the GPU, the simulator's device-resident averages), gathered in one pass; None otherwise (the
-    general path handles it).  The table is [n_tensors x n_peers] uint64, as dla_wsum_multi takes it."""
+    (or `ref`'s, when given: a model outside the list) parameter shapes, one supported dtype and
+    contiguous storage on ONE HIP device (models trained on the GPU, the simulator's device-resident
+    averages), gathered in one pass; None otherwise (the general path handles it).  The table is
+    [n_tensors x n_peers] uint64 over the listed models, as dla_wsum_multi takes it."""
     import numpy as np
 
-    nat = _native_layout(models, -2, tensor_major=True)
+    nat = _native_layout(models, -2, tensor_major=True, ref=ref)
     if nat is not None:
         dtype, numels, table, dev = nat
         return (dtype, torch.device("cuda", dev), numels,
                 np.frombuffer(table, dtype=np.uint64).reshape(len(numels), len(models)))
+    if ref is not None:
+        models = [ref] + list(models)
     p0 = _parameters(models[0])
     if not p0 or not p0[0].is_cuda:
         return None
@@ -378,6 +381,8 @@ def _device_layout(models: List[nn.Module]):
                 return None
             add(p.data_ptr())
         rows.append(row)
+    if ref is not None:
+        rows = rows[1:]
     table = np.ascontiguousarray(np.array(rows, dtype=np.uint64).T)
     return dtype, torch.device("cuda", dev), [p.numel() for p in p0], table
 
@@ -486,21 +491,19 @@ def _device_round_grouped(models: List[nn.Module], weights) -> "nn.Module | None
     outs = (ctypes.c_void_p * len(numels)).from_buffer(byte_offs + flat.data_ptr())
     _wsum.wsum_multi_ptrs(dtype, (ctypes.c_void_p * table.size).from_buffer(table), outs, nums,
                           weights[a0:b0_], device)
-    # checked after the first launch, so the GPU starts sooner (a failed check leaves `flat` unused)
+    for a, b in bounds[1:]:
+        # each later group checked against models[0]'s layout (shapes, dtype, device) in its own walk
+        lay = _device_layout(models[a:b], ref=models[0])
+        if lay is None or lay[0] is not dtype or lay[1] != device or lay[2] != numels:
+            return None
+        _wsum.wsum_multi_ptrs(dtype, (ctypes.c_void_p * lay[3].size).from_buffer(lay[3]), outs, nums,
+                              weights[a:b], device, acc_in=True)
+    # models[0]'s own objects, listed after the launches (the GPU starts sooner; a tree the result cannot
+    # be built over leaves `flat` unused and the general path handles the round)
     objs = mod.tensors(models[0], _PLAIN_SET)
     if objs is None or len(objs[0]) != len(numels) or any(type(p) is not nn.Parameter for p in objs[0]):
         return None
     p0, b0 = objs
-    shapes = [p.shape for p in p0]
-    for a, b in bounds[1:]:
-        lay = _device_layout(models[a:b])
-        if lay is None or lay[0] is not dtype or lay[1] != device or lay[2] != numels:
-            return None
-        head = mod.tensors(models[a], _PLAIN_SET)
-        if head is None or [p.shape for p in head[0]] != shapes:
-            return None
-        _wsum.wsum_multi_ptrs(dtype, (ctypes.c_void_p * lay[3].size).from_buffer(lay[3]), outs, nums,
-                              weights[a:b], device, acc_in=True)
     memo = {}
     mod.param_views(flat, p0, offs, memo)
     _seed_buffers(b0, memo)

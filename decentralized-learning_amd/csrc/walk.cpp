@@ -16,7 +16,10 @@
 //     (dtype name, [numel of each of models[0]'s parameters], pointer table bytearray, device index)
 // with the table tensor-major ([n_tensors][n_models] uint64) or peer-major ([n_models][n_tensors]).
 // `device`: -1 for CPU parameters, a HIP device index every parameter must be on, or -2 for the HIP
-// device of models[0]'s first parameter (the returned device index; -1 for CPU).
+// device of models[0]'s first parameter (the returned device index; -1 for CPU).  `ref`, when given, is a
+// model outside the list whose parameters set the layout (shapes, dtype, device) every listed model must
+// match — a round laid out group by group checks each group against its first model this way — and is
+// not part of the table.
 //
 // This is host plumbing of the Python binding, not part of the C ABI (include/dlagg.h): it takes
 // Python objects and is built against torch's headers.
@@ -132,30 +135,33 @@ const char* dtype_name(at::ScalarType t) {
   }
 }
 
-py::object layout(py::list models, int device, py::object plain, bool tensor_major) {
+py::object layout(py::list models, int device, py::object plain, bool tensor_major, py::object ref) {
   const Py_ssize_t n = static_cast<Py_ssize_t>(py::len(models));
   if (n < 1 || !PySet_Check(plain.ptr())) return py::none();
   std::vector<PyObject*> ps;
-  std::vector<at::Tensor> p0;  // models[0]'s parameters (the reference layout)
+  std::vector<at::Tensor> p0;  // the reference layout: `ref`'s parameters, else models[0]'s
   std::vector<uint64_t> ptrs;
   at::ScalarType dt = at::kFloat;
   PtrSet seen_m, seen_p;  // per model, cleared (table kept) between models
-  for (Py_ssize_t m = 0; m < n; ++m) {
+  // m = -1: `ref` (a model of the round outside this list — the first model of a round laid out group
+  // by group), walked for the layout only
+  for (Py_ssize_t m = ref.is_none() ? 0 : -1; m < n; ++m) {
     ps.clear();
     seen_m.clear();
     seen_p.clear();
-    if (!walk(PyList_GET_ITEM(models.ptr(), m), plain.ptr(), seen_m, seen_p, ps)) return py::none();
-    if (m == 0) {
+    if (!walk(m < 0 ? ref.ptr() : PyList_GET_ITEM(models.ptr(), m), plain.ptr(), seen_m, seen_p, ps)) return py::none();
+    if (p0.empty()) {
       if (ps.empty()) return py::none();
       ptrs.resize(static_cast<size_t>(n) * ps.size());
     } else if (ps.size() != p0.size()) {
       return py::none();
     }
     const size_t nt = ps.size();
+    const bool first = p0.empty();
     for (size_t t = 0; t < nt; ++t) {
       if (!THPVariable_Check(ps[t])) return py::none();
       const at::Tensor& x = THPVariable_Unpack(ps[t]);
-      if (m == 0) {
+      if (first) {
         if (t == 0) {
           dt = x.scalar_type();
           if (!dtype_name(dt)) return py::none();
@@ -170,7 +176,7 @@ py::object layout(py::list models, int device, py::object plain, bool tensor_maj
       }
       if (x.scalar_type() != dt || !x.is_contiguous() || !x.has_storage()) return py::none();
       if (device < 0 ? !x.is_cpu() : !(x.is_cuda() && x.get_device() == device)) return py::none();
-      ptrs[tensor_major ? t * n + m : m * nt + t] = reinterpret_cast<uint64_t>(x.data_ptr());
+      if (m >= 0) ptrs[tensor_major ? t * n + m : m * nt + t] = reinterpret_cast<uint64_t>(x.data_ptr());
     }
   }
   py::list numels;
@@ -517,7 +523,8 @@ py::object clone_dict(py::object v, py::dict memo, py::object atomic, py::object
 
 PYBIND11_MODULE(_dla_walk, m) {
   m.doc() = "accdfl_amd host plumbing: the per-round walk over every parameter of every model";
-  m.def("layout", &layout, py::arg("models"), py::arg("device"), py::arg("plain"), py::arg("tensor_major"));
+  m.def("layout", &layout, py::arg("models"), py::arg("device"), py::arg("plain"), py::arg("tensor_major"),
+        py::arg("ref") = py::none());
   m.def("tensors", &tensors, py::arg("model"), py::arg("plain"));
   m.def("block_table", &block_table, py::arg("blocks"));
   m.def("param_views", &param_views, py::arg("flat"), py::arg("params"), py::arg("offsets"), py::arg("memo"));

@@ -680,6 +680,13 @@ def test_native_walk_matches_the_python_walk():
     strided[0][0].weight = nn.Parameter(torch.zeros(4, 2, 3, 6)[..., ::2])  # not dense
     assert fa._native_layout(strided, -1, tensor_major=False) is None
     assert fa._native_layout(models, 0, tensor_major=False) is None  # CPU models asked for device 0
+    # `ref`: a model outside the list sets the layout every listed model must match (a group of a round laid
+    # out group by group, checked against the round's first model); its pointers are not in the table
+    _, numels_r, table_r, _ = fa._native_layout(models[2:], -1, tensor_major=False, ref=models[0])
+    assert numels_r == numels and np.frombuffer(table_r, dtype=np.uint64).tolist() == [x for r in want[2:] for x in r]
+    assert fa._native_layout(models[1:2], -1, tensor_major=False, ref=bad[1]) is None  # shape differs from ref
+    assert fa._native_layout(models[1:2], -1, tensor_major=False, ref=half[0]) is None  # dtype differs from ref
+    assert fa._native_layout(bad[1:], -1, tensor_major=False, ref=bad[1]) is not None
     # tensors(): models[0]'s parameter and buffer objects in parameters() / buffers() order (the device
     # round builds the result's fresh tensors from them)
     m0 = models[0]
