@@ -999,8 +999,9 @@ def reduce_parameters(center_params: List[torch.Tensor], peer_params: List[List[
 # memo, so identity (tied weights, shared submodules) is preserved exactly as deepcopy does.
 _ATOMIC = frozenset({type(None), bool, int, float, complex, str, bytes, torch.dtype, torch.device})
 _plain_module_cls: Dict[type, bool] = {}
-# dicts and OrderedDicts of the tree cloned by the walk extension (walk.cpp clone_dict: the same order
-# and memo, no Python call per seeded entry)
+_PLAIN_MODULE_SET: set = set()  # the classes _plain_module accepts, as the walk extension takes them
+# the tree cloned by the walk extension (walk.cpp clone_value: the same order and memo, no Python call
+# per seeded entry, dict, container or plain module)
 _NATIVE_DICT_CLONE = True
 
 
@@ -1012,10 +1013,23 @@ def _plain_module(cls: type) -> bool:
               and getattr(cls, "__deepcopy__", None) is None and cls not in copyreg.dispatch_table
               and not any("__slots__" in c.__dict__ for c in cls.__mro__))
         _plain_module_cls[cls] = ok
+        if ok:
+            _PLAIN_MODULE_SET.add(cls)
     return ok
 
 
+def _clone_fallback(v, memo: dict):
+    """The walk extension's fallback for an object its clone does not take itself: a module class not
+    yet classified (classified now, then cloned natively), else copy.deepcopy with the same memo."""
+    if _plain_module(type(v)):
+        return _lib.walk_module().clone_value(v, memo, _ATOMIC, _PLAIN_MODULE_SET, _clone_fallback, OrderedDict)
+    return copy.deepcopy(v, memo)
+
+
 def _clone_value(v, memo: dict):
+    mod = _lib.walk_module() if _NATIVE_DICT_CLONE else None
+    if mod is not None:
+        return mod.clone_value(v, memo, _ATOMIC, _PLAIN_MODULE_SET, _clone_fallback, OrderedDict)
     t = type(v)
     if t in _ATOMIC:
         return v
@@ -1023,9 +1037,6 @@ def _clone_value(v, memo: dict):
     if y is not memo:
         return y
     if t is dict or t is OrderedDict:
-        mod = _lib.walk_module() if _NATIVE_DICT_CLONE else None
-        if mod is not None:
-            return mod.clone_dict(v, memo, _ATOMIC, _clone_value, OrderedDict)
         y = t()
         memo[id(v)] = y
         get = memo.get
@@ -1040,11 +1051,7 @@ def _clone_value(v, memo: dict):
     if _plain_module(t):
         y = t.__new__(t)
         memo[id(v)] = y
-        mod = _lib.walk_module() if _NATIVE_DICT_CLONE else None
-        if mod is not None:
-            state = mod.clone_dict(v.__dict__, memo, _ATOMIC, _clone_value, OrderedDict, "_compiled_call_impl")
-        else:
-            state = {k: _clone_value(x, memo) for k, x in v.__dict__.items() if k != "_compiled_call_impl"}
+        state = {k: _clone_value(x, memo) for k, x in v.__dict__.items() if k != "_compiled_call_impl"}
         y.__setstate__(state)
         return y
     return copy.deepcopy(v, memo)
@@ -1063,12 +1070,34 @@ def _center_copy(model0: nn.Module, large: bool = True) -> nn.Module:
     tree through _clone_value, deepcopy's protocol without its per-object dispatch: the GL
     merge of two GNLeNet models builds this copy every round); the buffers of each (device, dtype) are
     copied by one gather into one fresh allocation (_seed_buffers) instead of a deepcopy each."""
-    memo = _fresh_params(model0, large)
     mod = _lib.walk_module()
     objs = mod.tensors(model0, _PLAIN_SET) if mod is not None else None
+    memo = _flat_params(mod, objs[0], large) if objs is not None else None
+    if memo is None:
+        memo = _fresh_params(model0, large)
     if objs is not None and len(objs[1]) > 1:
         _seed_buffers(objs[1], memo)
     return _clone_value(model0, memo)
+
+
+def _flat_params(mod, params: list, large: bool) -> "dict | None":
+    """_fresh_params for contiguous CPU nn.Parameters of one dtype, in one allocation: the deepcopy memo
+    id(parameter) -> an nn.Parameter over its own 256-byte-aligned part of one fresh tensor (each with a
+    storage of its own, walk.cpp alias_of: pickles like a deepcopied tensor), made natively — a GL merge
+    builds this copy every round.  The allocation is pooled pre-faulted memory when large (as
+    _fresh_params gives each large parameter).  None when the parameters do not qualify."""
+    if not params:
+        return None
+    dtype = params[0].dtype
+    for p in params:
+        if type(p) is not nn.Parameter or p.dtype is not dtype or not p.is_cpu or not p.is_contiguous():
+            return None
+    offs, total, _, _ = _flat_plan(dtype, [p.numel() for p in params])
+    flat = (_host_memory.result_tensor((total,), dtype) if large
+            else torch.empty(total, dtype=dtype))
+    memo = {}
+    mod.param_views(flat, params, offs, memo)
+    return memo
 
 
 def _fresh_params(model0: nn.Module, large: bool = True) -> dict:

@@ -229,21 +229,42 @@ py::tuple block_table(py::list blocks) {
   return py::make_tuple(addrs, lens);
 }
 
-// A tensor over `flat`'s storage with the given sizes, strides and element offset: what
-// flat.as_strided(...).detach() returns (same storage, dtype, device and dispatch keys, no view or
-// autograd history, metadata changeable), made as one TensorImpl without the two dispatched ops.
+// A tensor over part of `flat`'s allocation with the given sizes, strides and element offset, holding a
+// storage of its OWN (its bytes only) whose data pointer keeps `flat`'s storage alive: what deepcopy
+// gives each tensor (a storage per tensor, so pickle.dumps(state_dict()) — the reference's
+// serialize_model — writes each tensor's bytes once, not the whole allocation per tensor), while the
+// reduce and the buffer gather still write ONE allocation.  Same dtype, device and dispatch keys as
+// `flat`, no view or autograd history, metadata changeable; resizable through `flat`'s allocator (a
+// resize reallocates and lets go of `flat`).  One TensorImpl, no dispatched op.
 at::Tensor alias_of(const at::Tensor& flat, at::IntArrayRef sizes, at::IntArrayRef strides, int64_t offset) {
-  auto impl = c10::make_intrusive<c10::TensorImpl>(c10::Storage(flat.storage()), flat.key_set(), flat.dtype());
-  impl->set_sizes_and_strides(sizes, strides, flat.storage_offset() + offset);
+  const int64_t es = static_cast<int64_t>(flat.element_size());
+  int64_t extent = 1;  // elements the tensor spans
+  for (size_t d = 0; d < sizes.size(); ++d) {
+    if (sizes[d] == 0) {
+      extent = 0;
+      break;
+    }
+    extent += (sizes[d] - 1) * strides[d];
+  }
+  char* base = static_cast<char*>(flat.data_ptr()) + offset * es;
+  if (offset < 0 || (offset + extent) * es > static_cast<int64_t>(flat.nbytes()))
+    throw std::invalid_argument("alias_of: outside the allocation");
+  auto* keep = new c10::Storage(flat.storage());  // released by the DataPtr's deleter
+  c10::DataPtr dp(base, keep, [](void* ctx) { delete static_cast<c10::Storage*>(ctx); }, flat.device());
+  at::Allocator* alloc = flat.storage().allocator();
+  c10::Storage st(c10::Storage::use_byte_size_t(), static_cast<size_t>(extent * es), std::move(dp), alloc,
+                  /*resizable=*/alloc != nullptr);
+  auto impl = c10::make_intrusive<c10::TensorImpl>(std::move(st), flat.key_set(), flat.dtype());
+  impl->set_sizes_and_strides(sizes, strides, 0);
   impl->set_allow_tensor_metadata_change(true);
   return at::Tensor(std::move(impl));
 }
 
 // The result module's fresh parameters of a device round (fedavg._device_round: deepcopy(models[0]) of
-// fedavg.py:20 with every parameter a view of ONE allocation the reduce writes): for each of models[0]'s
-// parameters p and its element offset in `flat`, an nn.Parameter over flat.as_strided(p's sizes, p's
-// strides, offset) with p's requires_grad — what torch.Tensor._make_subclass(nn.Parameter, view, rg)
-// builds (a detached alias whose metadata may change, wrapped as the Parameter class), without its ~8 us
+// fedavg.py:20 with every parameter over part of ONE allocation the reduce writes): for each of
+// models[0]'s parameters p and its element offset in `flat`, an nn.Parameter over alias_of(flat, p's
+// sizes, p's strides, offset) with p's requires_grad — what torch.Tensor._make_subclass(nn.Parameter,
+// data, rg) builds (a detached tensor whose metadata may change, wrapped as the Parameter class), without its ~8 us
 // of Python per parameter (110 parameters of a google_speech ResNet-34: ~0.4 ms per round) — stored
 // straight into the deepcopy memo as memo[id(p)].
 void param_views(const at::Tensor& flat, py::list params, const std::vector<int64_t>& offsets, py::dict memo) {
@@ -329,135 +350,164 @@ void buffer_copies(py::list buffers, py::dict memo) {
   }
 }
 
-// One value of the module-tree clone (fedavg._clone_value's order): the memo's copy if it holds one
-// (seeded parameters and buffers, objects met before), the value itself if its type is atomic, a new
-// dict / OrderedDict through clone_mapping, else fallback(value, memo) — the Python restatement of
-// deepcopy's protocol.  New reference, or nullptr with the Python error set.
-PyObject* clone_mapping(PyObject* v, PyObject* memo, PyObject* atomic, PyObject* fallback, PyObject* odict,
-                        PyObject* skip = nullptr);
+// The module-tree clone (fedavg._clone_value, deepcopy's protocol restated) in native code.  Ctx: the
+// deepcopy memo (id -> copy), the set of types copied as themselves, the set of module classes cloned
+// here (fedavg._plain_module: torch's __getstate__, no other copy hook), `fallback(obj, memo)` (the
+// Python _clone_value, for every other object), collections.OrderedDict, and "_compiled_call_impl" (the
+// __dict__ entry a module clone leaves out).
+struct CloneCtx {
+  PyObject* memo;
+  PyObject* atomic;
+  PyObject* modules;
+  PyObject* fallback;
+  PyObject* odict;
+  PyObject* skip;
+};
 
-PyObject* clone_sequence(PyObject* x, PyObject* memo, PyObject* atomic, PyObject* fallback, PyObject* odict);
+PyObject* clone_mapping(PyObject* v, const CloneCtx& c, bool module_state = false);
+PyObject* clone_sequence(PyObject* x, const CloneCtx& c);
 
-PyObject* clone_one(PyObject* x, PyObject* memo, PyObject* atomic, PyObject* fallback, PyObject* odict) {
+bool memo_put(PyObject* memo, PyObject* x, PyObject* y) {
+  PyObject* id = PyLong_FromVoidPtr(x);
+  const int rc = id ? PyDict_SetItem(memo, id, y) : -1;
+  Py_XDECREF(id);
+  return rc == 0;
+}
+
+// A module of a class in ctx.modules, as copy._reconstruct does it: y = cls.__new__(cls), registered in
+// the memo, state = a clone of x.__dict__ without _compiled_call_impl, y.__setstate__(state).
+PyObject* clone_module(PyObject* x, const CloneCtx& c) {
+  PyTypeObject* tp = Py_TYPE(x);
+  static PyObject* const no_args = PyTuple_New(0);
+  static PyObject* const setstate = PyUnicode_InternFromString("__setstate__");
+  PyObject* y = tp->tp_new(tp, no_args, nullptr);
+  if (!y) return nullptr;
+  if (!memo_put(c.memo, x, y)) {
+    Py_DECREF(y);
+    return nullptr;
+  }
+  PyObject* d = PyObject_GenericGetDict(x, nullptr);
+  PyObject* state = d ? clone_mapping(d, c, /*module_state=*/true) : nullptr;
+  Py_XDECREF(d);
+  PyObject* r = state ? PyObject_CallMethodOneArg(y, setstate, state) : nullptr;
+  Py_XDECREF(state);
+  if (!r) {
+    Py_DECREF(y);
+    return nullptr;
+  }
+  Py_DECREF(r);
+  return y;
+}
+
+// One value, in fedavg._clone_value's order: the memo's copy if it holds one (seeded parameters and
+// buffers, objects met before), the value itself if its type is atomic, a clone of a dict /
+// OrderedDict / tuple / list / empty set / plain module made here, else fallback(value, memo).  New
+// reference, or nullptr with the Python error set.
+PyObject* clone_one(PyObject* x, const CloneCtx& c) {
   PyObject* key = PyLong_FromVoidPtr(x);
   if (!key) return nullptr;
-  PyObject* hit = PyDict_GetItemWithError(memo, key);  // borrowed
+  PyObject* hit = PyDict_GetItemWithError(c.memo, key);  // borrowed
   Py_DECREF(key);
   if (hit) return Py_NewRef(hit);
   if (PyErr_Occurred()) return nullptr;
-  const int at = PySet_Contains(atomic, reinterpret_cast<PyObject*>(Py_TYPE(x)));
+  const int at = PySet_Contains(c.atomic, reinterpret_cast<PyObject*>(Py_TYPE(x)));
   if (at < 0) return nullptr;
   if (at) return Py_NewRef(x);
-  if (PyDict_CheckExact(x) || Py_TYPE(x) == reinterpret_cast<PyTypeObject*>(odict))
-    return clone_mapping(x, memo, atomic, fallback, odict);
-  if (PyTuple_CheckExact(x) || PyList_CheckExact(x)) return clone_sequence(x, memo, atomic, fallback, odict);
+  if (PyDict_CheckExact(x) || Py_TYPE(x) == reinterpret_cast<PyTypeObject*>(c.odict)) return clone_mapping(x, c);
+  if (PyTuple_CheckExact(x) || PyList_CheckExact(x)) return clone_sequence(x, c);
   if (PySet_CheckExact(x) && PySet_GET_SIZE(x) == 0) {  // _non_persistent_buffers_set: a new empty set
     PyObject* y = PySet_New(nullptr);
-    PyObject* id = y ? PyLong_FromVoidPtr(x) : nullptr;
-    const int rc = id ? PyDict_SetItem(memo, id, y) : -1;
-    Py_XDECREF(id);
-    if (rc < 0) {
+    if (!y || !memo_put(c.memo, x, y)) {
       Py_XDECREF(y);
       return nullptr;
     }
     return y;
   }
-  return PyObject_CallFunctionObjArgs(fallback, x, memo, nullptr);
+  const int mod = PySet_Contains(c.modules, reinterpret_cast<PyObject*>(Py_TYPE(x)));
+  if (mod < 0) return nullptr;
+  if (mod) return clone_module(x, c);
+  return PyObject_CallFunctionObjArgs(c.fallback, x, c.memo, nullptr);
 }
 
 // A tuple or list (a conv's kernel_size / stride / padding, _reversed_padding_repeated_twice), as
 // copy.deepcopy copies them: a list is a new list registered in the memo before its items; a tuple is
 // itself when every item clones to itself (tuples of numbers), else a new tuple registered in the memo.
-PyObject* clone_sequence(PyObject* x, PyObject* memo, PyObject* atomic, PyObject* fallback, PyObject* odict) {
-  PyObject* id = PyLong_FromVoidPtr(x);
-  if (!id) return nullptr;
+PyObject* clone_sequence(PyObject* x, const CloneCtx& c) {
   if (PyList_CheckExact(x)) {
     PyObject* y = PyList_New(0);
-    if (!y || PyDict_SetItem(memo, id, y) < 0) {
+    if (!y || !memo_put(c.memo, x, y)) {
       Py_XDECREF(y);
-      Py_DECREF(id);
       return nullptr;
     }
-    Py_DECREF(id);
     for (Py_ssize_t i = 0; i < PyList_GET_SIZE(x); ++i) {
       PyObject* item = Py_NewRef(PyList_GET_ITEM(x, i));
-      PyObject* c = clone_one(item, memo, atomic, fallback, odict);
+      PyObject* ci = clone_one(item, c);
       Py_DECREF(item);
-      if (!c || PyList_Append(y, c) < 0) {
-        Py_XDECREF(c);
+      if (!ci || PyList_Append(y, ci) < 0) {
+        Py_XDECREF(ci);
         Py_DECREF(y);
         return nullptr;
       }
-      Py_DECREF(c);
+      Py_DECREF(ci);
     }
     return y;
   }
   const Py_ssize_t n = PyTuple_GET_SIZE(x);
   PyObject* y = PyTuple_New(n);
-  if (!y) {
-    Py_DECREF(id);
-    return nullptr;
-  }
+  if (!y) return nullptr;
   bool same = true;
   for (Py_ssize_t i = 0; i < n; ++i) {
-    PyObject* c = clone_one(PyTuple_GET_ITEM(x, i), memo, atomic, fallback, odict);
-    if (!c) {
+    PyObject* ci = clone_one(PyTuple_GET_ITEM(x, i), c);
+    if (!ci) {
       Py_DECREF(y);
-      Py_DECREF(id);
       return nullptr;
     }
-    same = same && c == PyTuple_GET_ITEM(x, i);
-    PyTuple_SET_ITEM(y, i, c);
+    same = same && ci == PyTuple_GET_ITEM(x, i);
+    PyTuple_SET_ITEM(y, i, ci);
   }
   if (same) {
     Py_DECREF(y);
-    Py_DECREF(id);
     return Py_NewRef(x);
   }
   // an item's copy may have copied this tuple already (a cycle through a mutable item): use that one
-  PyObject* prev = PyDict_GetItemWithError(memo, id);
+  PyObject* id = PyLong_FromVoidPtr(x);
+  PyObject* prev = id ? PyDict_GetItemWithError(c.memo, id) : nullptr;
+  Py_XDECREF(id);
   if (prev || PyErr_Occurred()) {
     Py_DECREF(y);
-    Py_DECREF(id);
     return prev ? Py_NewRef(prev) : nullptr;
   }
-  const int rc = PyDict_SetItem(memo, id, y);
-  Py_DECREF(id);
-  if (rc < 0) {
+  if (!memo_put(c.memo, x, y)) {
     Py_DECREF(y);
     return nullptr;
   }
   return y;
 }
 
-// A dict or OrderedDict of the module tree (a module's _parameters, _buffers, _modules, hook
-// dicts): a new mapping of the same type registered in the memo first (deepcopy's order, so a cycle
-// finds it), then every entry in iteration order with its value cloned by clone_one and a non-atomic
-// key through fallback; a str key equal to `skip` (when given) is left out.
-PyObject* clone_mapping(PyObject* v, PyObject* memo, PyObject* atomic, PyObject* fallback, PyObject* odict,
-                        PyObject* skip) {
+// A dict or OrderedDict of the module tree (a module's _parameters, _buffers, _modules, hook dicts), or
+// a module's __dict__ as the state its clone is set from (module_state: "_compiled_call_impl" left out):
+// a new mapping of the same type registered in the memo first (deepcopy's order, so a cycle finds it),
+// then every entry in iteration order with its value cloned by clone_one and a non-atomic key through
+// the fallback.
+PyObject* clone_mapping(PyObject* v, const CloneCtx& c, bool module_state) {
   // an empty OrderedDict (a module's hook dicts) iterates like a dict: no items() view needed
   const bool exact = PyDict_CheckExact(v);
   const bool plain_iter = exact || PyDict_GET_SIZE(v) == 0;
   PyObject* y = exact ? PyDict_New() : PyObject_CallNoArgs(reinterpret_cast<PyObject*>(Py_TYPE(v)));
-  if (!y) return nullptr;
-  PyObject* id = PyLong_FromVoidPtr(v);
-  if (!id || PyDict_SetItem(memo, id, y) < 0) {
-    Py_XDECREF(id);
-    Py_DECREF(y);
+  if (!y || !memo_put(c.memo, v, y)) {
+    Py_XDECREF(y);
     return nullptr;
   }
-  Py_DECREF(id);
   auto put = [&](PyObject* k, PyObject* x) -> bool {
-    if (skip && PyUnicode_Check(k) && PyUnicode_Compare(k, skip) == 0) return true;
-    const int at = PySet_Contains(atomic, reinterpret_cast<PyObject*>(Py_TYPE(k)));
+    if (module_state && PyUnicode_Check(k) && PyUnicode_Compare(k, c.skip) == 0) return true;
+    const int at = PySet_Contains(c.atomic, reinterpret_cast<PyObject*>(Py_TYPE(k)));
     if (at < 0) return false;
-    PyObject* kc = at ? Py_NewRef(k) : PyObject_CallFunctionObjArgs(fallback, k, memo, nullptr);
+    PyObject* kc = at ? Py_NewRef(k) : PyObject_CallFunctionObjArgs(c.fallback, k, c.memo, nullptr);
     if (!kc) return false;
-    PyObject* c = clone_one(x, memo, atomic, fallback, odict);
-    const int rc = c ? (exact ? PyDict_SetItem(y, kc, c) : PyObject_SetItem(y, kc, c)) : -1;
+    PyObject* ci = clone_one(x, c);
+    const int rc = ci ? (exact ? PyDict_SetItem(y, kc, ci) : PyObject_SetItem(y, kc, ci)) : -1;
     Py_DECREF(kc);
-    Py_XDECREF(c);
+    Py_XDECREF(ci);
     return rc == 0;
   };
   bool ok = true;
@@ -502,19 +552,19 @@ PyObject* clone_mapping(PyObject* v, PyObject* memo, PyObject* atomic, PyObject*
   return y;
 }
 
-// fedavg._clone_value for a dict / OrderedDict (`v`) of the result module's tree, in native code: the
-// mapping's entries are looked up in the deepcopy memo without a Python call each (a google_speech
-// ResNet-34's _parameters and _buffers hold 218 seeded entries).  `atomic`: the set of types copied as
-// themselves; `fallback(obj, memo)`: _clone_value, for every value neither seeded nor atomic nor a
-// mapping, and for non-atomic keys (hashable: _clone_value copies them as deepcopy does); `odict`:
-// collections.OrderedDict; `skip`: a key left out (a module __dict__'s _compiled_call_impl), or None.
-py::object clone_dict(py::object v, py::dict memo, py::object atomic, py::object fallback, py::object odict,
-                      py::object skip) {
-  if (!PyAnySet_Check(atomic.ptr()) || !(PyDict_CheckExact(v.ptr()) || Py_TYPE(v.ptr()) == reinterpret_cast<PyTypeObject*>(odict.ptr())))
-    throw std::invalid_argument("clone_dict: a dict or OrderedDict and a set of atomic types");
-  if (!skip.is_none() && !PyUnicode_Check(skip.ptr())) throw std::invalid_argument("clone_dict: skip is a str or None");
-  PyObject* y = clone_mapping(v.ptr(), memo.ptr(), atomic.ptr(), fallback.ptr(), odict.ptr(),
-                              skip.is_none() ? nullptr : skip.ptr());
+// fedavg._clone_value in native code, for a value of the result module's tree: the memo's entries are
+// looked up without a Python call each (a google_speech ResNet-34's _parameters and _buffers hold 218
+// seeded entries), and the tree's dicts, containers and plain modules are cloned here.  `atomic`: the set
+// of types copied as themselves; `modules`: the set of module classes cloned here; `fallback(obj, memo)`:
+// _clone_value, for every other object and for non-atomic keys (hashable: _clone_value copies them as
+// deepcopy does); `odict`: collections.OrderedDict.
+py::object clone_value(py::object v, py::dict memo, py::object atomic, py::object modules, py::object fallback,
+                       py::object odict) {
+  if (!PyAnySet_Check(atomic.ptr()) || !PyAnySet_Check(modules.ptr()))
+    throw std::invalid_argument("clone_value: sets of atomic types and module classes");
+  static PyObject* const skip = PyUnicode_InternFromString("_compiled_call_impl");
+  const CloneCtx c{memo.ptr(), atomic.ptr(), modules.ptr(), fallback.ptr(), odict.ptr(), skip};
+  PyObject* y = clone_one(v.ptr(), c);
   if (!y) throw py::error_already_set();
   return py::reinterpret_steal<py::object>(y);
 }
@@ -529,7 +579,7 @@ PYBIND11_MODULE(_dla_walk, m) {
   m.def("block_table", &block_table, py::arg("blocks"));
   m.def("param_views", &param_views, py::arg("flat"), py::arg("params"), py::arg("offsets"), py::arg("memo"));
   m.def("buffer_copies", &buffer_copies, py::arg("buffers"), py::arg("memo"));
-  m.def("clone_dict", &clone_dict, py::arg("v"), py::arg("memo"), py::arg("atomic"), py::arg("fallback"),
-        py::arg("odict"), py::arg("skip") = py::none());
+  m.def("clone_value", &clone_value, py::arg("v"), py::arg("memo"), py::arg("atomic"), py::arg("modules"),
+        py::arg("fallback"), py::arg("odict"));
   m.attr("build_id") = py::str(kWalkIdTag + sizeof("dlagg-walk-build-id:") - 1);
 }

@@ -738,6 +738,17 @@ def test_walk_memo_seeding_on_cpu():
     assert type(v0) is nn.Parameter and v0.shape == (3, 4) and v0.requires_grad and not v1.requires_grad
     assert torch.equal(v0.detach().reshape(-1), flat[:12]) and torch.equal(v1.detach(), flat[16:21])
     assert v0.data_ptr() == flat.data_ptr() and v1.data_ptr() == flat.data_ptr() + 64
+    # each has a storage of its own bytes (as deepcopy gives), so the reference's serialize_model
+    # (pickle.dumps(state_dict())) writes each once, not the whole allocation per tensor; the
+    # allocation stays alive while either does
+    assert v0.untyped_storage().nbytes() == 48 and v1.untyped_storage().nbytes() == 20
+    assert v0.storage_offset() == 0 and v1.storage_offset() == 0
+    import pickle
+
+    alone = pickle.dumps({"a": v0.detach().clone(), "b": v1.detach().clone()})
+    assert abs(len(pickle.dumps({"a": v0.detach(), "b": v1.detach()})) - len(alone)) < 64
+    del flat
+    assert torch.equal(v1.detach(), torch.arange(16, 21, dtype=torch.float32))
     a, b, c = torch.randn(4), torch.randn(6), torch.arange(3)
     d = torch.arange(2)
     shared = torch.randn(8)
@@ -752,8 +763,12 @@ def test_walk_memo_seeding_on_cpu():
     for x in (a, b, c, d):
         y = memo[id(x)]
         assert torch.equal(x, y) and y.dtype == x.dtype and y.data_ptr() != x.data_ptr()
-    assert memo[id(a)].untyped_storage().data_ptr() == memo[id(b)].untyped_storage().data_ptr()
-    assert memo[id(c)].untyped_storage().data_ptr() == memo[id(d)].untyped_storage().data_ptr()
+    # one allocation per (device, dtype) group, a storage of its own per copy
+    assert memo[id(b)].data_ptr() == memo[id(a)].data_ptr() + 16 and memo[id(d)].data_ptr() == memo[id(c)].data_ptr() + 24
+    assert [memo[id(x)].untyped_storage().nbytes() for x in (a, b, c, d)] == [16, 24, 24, 16]
+    grown = memo[id(b)]
+    grown.resize_(10)  # resizable like a deepcopied tensor: it moves to an allocation of its own
+    assert grown.shape == (10,) and torch.equal(grown[:6], b) and torch.equal(memo[id(a)], a)
     for x in (shared, view, grad, strided):
         assert id(x) not in memo
     lone = torch.randn(2, dtype=torch.float64)

@@ -448,6 +448,39 @@ def test_device_modules_of_real_layouts_through_fedavg(name, n, dtype):
     assert torch.equal(out.steps, models[0].steps)
 
 
+def test_device_round_result_pickles_like_a_deepcopy():
+    """The device round's result (parameters and buffer copies over one allocation each, walk.cpp
+    alias_of) has a storage per tensor, as deepcopy(models[0]) does: the reference's serialize_model
+    (pickle.dumps(state_dict()), accdfl/core/models/__init__.py:9-10) writes each tensor's bytes once,
+    not the whole allocation per tensor, and the payload decodes to the result's values."""
+    import copy
+    import pickle
+
+    from accdfl_amd.core.gradient_aggregation.fedavg import FedAvg
+
+    shapes = [(32, 3, 5, 5), (32,), (32,), (32,), (32, 32, 5, 5), (32,), (32,), (32,), (64, 32, 5, 5), (64,),
+              (64,), (64,), (10, 576), (10,)]
+    g = torch.Generator().manual_seed(11)
+    models = []
+    for k in range(6):
+        m = torch.nn.Module()
+        m.ps = torch.nn.ParameterList([torch.nn.Parameter((torch.randn(s, generator=g) * 0.05).cuda()) for s in shapes])
+        for j in range(4):
+            m.register_buffer("rm%d" % j, torch.randn(32, generator=g).cuda())
+        models.append(m)
+    out = FedAvg.aggregate(models, [1 / 6] * 6)
+    torch.cuda.synchronize()
+    want = len(pickle.dumps(copy.deepcopy(models[0]).state_dict()))
+    payload = pickle.dumps(out.state_dict())
+    assert abs(len(payload) - want) < 0.01 * want, (len(payload), want)
+    back = pickle.loads(payload)  # bytes this test just wrote
+    for k, v in out.state_dict().items():
+        assert torch.equal(back[k], v), k
+    ptrs = [p.data_ptr() for p in out.parameters()]
+    assert len({p.untyped_storage().data_ptr() for p in out.parameters()}) == len(ptrs)  # a storage each
+    assert all(b - a > 0 for a, b in zip(ptrs, ptrs[1:]))  # over one allocation, in order
+
+
 @pytest.mark.parametrize("dtype", ["f32", "bf16", "f64"])
 def test_multi_table_accumulate_continues_the_fold(dtype):
     """dla_wsum_multi_table_acc (ABI v12): the peers folded in two calls — the second continuing from
