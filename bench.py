@@ -904,11 +904,34 @@ GNLENET = [(32, 3, 5, 5), (32,), (32,), (32,), (32, 32, 5, 5), (32,), (32,), (32
            (64,), (64,), (10, 576), (10,)]  # accdfl/core/models/cifar10.py GNLeNet parameters
 
 
-def _gnlenet_models(n):
+def _gnlenet_models(n, layers=False):
+    """n GNLeNet-layout CPU models: one ParameterList of the 14 tensors, or (layers) the module tree of
+    layers the reference's model class builds (conv / pool / GroupNorm / linear submodules,
+    accdfl/core/models/cifar10.py) with the same parameters in the same order — the result's deepcopy
+    then clones nine modules with their hook dicts and attributes, as at the reference's call sites."""
     from torch import nn
 
     g = torch.Generator().manual_seed(n)
-    return [nn.ParameterList([nn.Parameter(torch.randn(s, generator=g) * 0.05) for s in GNLENET]) for _ in range(n)]
+    if not layers:
+        return [nn.ParameterList([nn.Parameter(torch.randn(s, generator=g) * 0.05) for s in GNLENET])
+                for _ in range(n)]
+    out = []
+    for _ in range(n):
+        m = nn.Module()
+        m.conv1 = nn.Conv2d(3, 32, 5, padding="same")
+        m.pool = nn.MaxPool2d(2, 2)
+        m.gn1 = nn.GroupNorm(2, 32)
+        m.conv2 = nn.Conv2d(32, 32, 5, padding="same")
+        m.gn2 = nn.GroupNorm(2, 32)
+        m.conv3 = nn.Conv2d(32, 64, 5, padding="same")
+        m.gn3 = nn.GroupNorm(2, 64)
+        m.fc1 = nn.Linear(576, 10)
+        with torch.no_grad():
+            for p, s in zip(m.parameters(), GNLENET):
+                assert tuple(p.shape) == s
+                p.copy_(torch.randn(s, generator=g) * 0.05)
+        out.append(m)
+    return out
 
 
 def _median_ms(fn, reps):
@@ -1131,10 +1154,12 @@ def host_inclusive_small(reps=50):
     from accdfl_amd.core.gradient_aggregation.fedavg import FedAvg
 
     out = {}
-    for n in (2, 8):
-        models = _gnlenet_models(n)
-        w = [float(1.0 / n)] * n
-        out["gnlenet_n%d" % n] = {"ours_ms": _median_ms(lambda: FedAvg.aggregate(models, w), reps)}
+    for layers in (False, True):
+        for n in (2, 8):
+            models = _gnlenet_models(n, layers)
+            w = [float(1.0 / n)] * n
+            out["gnlenet%s_n%d" % ("_layers" if layers else "", n)] = {
+                "ours_ms": _median_ms(lambda: FedAvg.aggregate(models, w), reps)}
     return out
 
 
@@ -1450,10 +1475,12 @@ def cpu_gnlenet_small(reps=50):
     from oracle.fedavg_oracle import fedavg_modules_torch  # timed CPU baseline (kind "port")
 
     out = {}
-    for n in (2, 8):
-        models = _gnlenet_models(n)
-        w = [float(1.0 / n)] * n
-        out["gnlenet_n%d" % n] = {"cpu_port_ms": _median_ms(lambda: fedavg_modules_torch(models, w), reps)}
+    for layers in (False, True):
+        for n in (2, 8):
+            models = _gnlenet_models(n, layers)
+            w = [float(1.0 / n)] * n
+            out["gnlenet%s_n%d" % ("_layers" if layers else "", n)] = {
+                "cpu_port_ms": _median_ms(lambda: fedavg_modules_torch(models, w), reps)}
     return out
 
 
