@@ -1,6 +1,7 @@
 """r04: egress of an averaged 25 M fp32 row from HBM into serialize_model bytes (wire.dumps_state_dict over a
 DeviceSource: chunked D2H through two page-locked bounce buffers, each chunk copied out by the threaded
-memcpy while the next one's D2H runs) at the chunk size ACCDFL_AMD_EGRESS_CHUNK_MB of this process.
+memcpy while the next one's D2H runs) at the chunk size ACCDFL_AMD_EGRESS_CHUNK_MB of this process,
+bound to the GPU's NUMA node (EGRESS_NO_BIND=1: not bound).
 Prints one JSON line: the median ms of 15 encodes and the bytes' check against the row.
 Usage on the GPU box: ACCDFL_AMD_EGRESS_CHUNK_MB=8 python profiles/r04_egress_probe.py"""
 import json
@@ -15,9 +16,11 @@ sys.path.insert(0, os.path.join(ROOT, "decentralized-learning_amd"))
 import torch  # noqa: E402
 
 from accdfl_amd.core import wire  # noqa: E402
+from accdfl_amd.core.host_memory import bind_to_gpu_node  # noqa: E402
 
 
 def main():
+    node = bind_to_gpu_node() if os.environ.get("EGRESS_NO_BIND") != "1" else None
     flat = torch.randn(25_000_000, generator=torch.Generator().manual_seed(5)).cuda()
     src = wire.DeviceSource(flat, 0, (25_000_000,))
     ts = []
@@ -27,7 +30,7 @@ def main():
         data = wire.dumps_state_dict({"w": src})
         ts.append(time.perf_counter() - t0)
     ok = data == wire.dumps_state_dict({"w": flat.cpu()})
-    print(json.dumps({"chunk_MB": wire._EGRESS_CHUNK >> 20, "egress_ms": round(statistics.median(ts[1:]) * 1e3, 3),
+    print(json.dumps({"numa_node_bound": node, "chunk_MB": wire._EGRESS_CHUNK >> 20, "egress_ms": round(statistics.median(ts[1:]) * 1e3, 3),
                       "min_ms": round(min(ts[1:]) * 1e3, 3), "bytes_equal": ok}), flush=True)
 
 

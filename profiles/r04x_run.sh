@@ -1,6 +1,7 @@
 #!/bin/bash
 # r04x: the egress copy-out's chunk size (wire._EGRESS_CHUNK): 100 MB from HBM into serialize_model bytes at
-# 4, 8, 16 and 32 MiB chunks, three interleaved rounds of fresh processes (profiles/r04_egress_probe.py).
+# 4, 8, 16 and 32 MiB chunks bound to the GPU's NUMA node and 32 MiB unbound, three interleaved rounds of fresh
+# processes (profiles/r04_egress_probe.py).
 set -o pipefail
 export TMPDIR=/tmp
 out=gpurun_out/r04x
@@ -18,4 +19,5 @@ for i in 1 2 3; do
   for mb in 4 8 16 32; do
     run 120 env ACCDFL_AMD_EGRESS_CHUNK_MB=$mb python -u profiles/r04_egress_probe.py >> $out/egress.jsonl 2>> $out/egress.err
   done
+  run 120 env EGRESS_NO_BIND=1 python -u profiles/r04_egress_probe.py >> $out/egress.jsonl 2>> $out/egress.err
 done
