@@ -234,8 +234,8 @@ py::tuple block_table(py::list blocks) {
 // gives each tensor (a storage per tensor, so pickle.dumps(state_dict()) — the reference's
 // serialize_model — writes each tensor's bytes once, not the whole allocation per tensor), while the
 // reduce and the buffer gather still write ONE allocation.  Same dtype, device and dispatch keys as
-// `flat`, no view or autograd history, metadata changeable; resizable through `flat`'s allocator (a
-// resize reallocates and lets go of `flat`).  One TensorImpl, no dispatched op.
+// `flat`, no view or autograd history, metadata changeable; resizable through `flat`'s allocator, or the
+// device's default one (a resize reallocates and lets go of `flat`).  One TensorImpl, no dispatched op.
 at::Tensor alias_of(const at::Tensor& flat, at::IntArrayRef sizes, at::IntArrayRef strides, int64_t offset) {
   const int64_t es = static_cast<int64_t>(flat.element_size());
   int64_t extent = 1;  // elements the tensor spans
@@ -251,7 +251,8 @@ at::Tensor alias_of(const at::Tensor& flat, at::IntArrayRef sizes, at::IntArrayR
     throw std::invalid_argument("alias_of: outside the allocation");
   auto* keep = new c10::Storage(flat.storage());  // released by the DataPtr's deleter
   c10::DataPtr dp(base, keep, [](void* ctx) { delete static_cast<c10::Storage*>(ctx); }, flat.device());
-  at::Allocator* alloc = flat.storage().allocator();
+  at::Allocator* alloc = flat.storage().allocator();  // none for memory torch did not allocate (a pool's)
+  if (!alloc) alloc = c10::GetAllocator(flat.device().type());
   c10::Storage st(c10::Storage::use_byte_size_t(), static_cast<size_t>(extent * es), std::move(dp), alloc,
                   /*resizable=*/alloc != nullptr);
   auto impl = c10::make_intrusive<c10::TensorImpl>(std::move(st), flat.key_set(), flat.dtype());

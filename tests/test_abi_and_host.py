@@ -766,6 +766,14 @@ def test_walk_memo_seeding_on_cpu():
     # one allocation per (device, dtype) group, a storage of its own per copy
     assert memo[id(b)].data_ptr() == memo[id(a)].data_ptr() + 16 and memo[id(d)].data_ptr() == memo[id(c)].data_ptr() + 24
     assert [memo[id(x)].untyped_storage().nbytes() for x in (a, b, c, d)] == [16, 24, 24, 16]
+    import numpy as np
+
+    pooled = torch.from_numpy(np.arange(8, dtype=np.float32))  # memory torch did not allocate
+    pv = {}
+    mod.param_views(pooled, [nn.Parameter(torch.zeros(3), requires_grad=False)], [2], pv)
+    (pq,) = pv.values()
+    assert torch.equal(pq, torch.tensor([2.0, 3.0, 4.0]))
+    pq.data.resize_(5)  # resizable through the CPU allocator
     grown = memo[id(b)]
     grown.resize_(10)  # resizable like a deepcopied tensor: it moves to an allocation of its own
     assert grown.shape == (10,) and torch.equal(grown[:6], b) and torch.equal(memo[id(a)], a)
