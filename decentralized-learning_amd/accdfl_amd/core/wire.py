@@ -695,7 +695,6 @@ def _join_pieces(pieces) -> bytes:
 # 8 MiB gets only 4) and the store kind of the copy-out (A/B knobs).
 _EGRESS_CHUNK = int(float(os.environ.get("ACCDFL_AMD_EGRESS_CHUNK_MB", "32")) * (1 << 20))
 _EGRESS_NT = os.environ.get("ACCDFL_AMD_EGRESS_NT", "0") == "1"
-_EGRESS_RAMP = os.environ.get("ACCDFL_AMD_EGRESS_RAMP", "1") == "1"
 _egress_bounce = {}
 _egress_lock = threading.Lock()
 
@@ -718,25 +717,6 @@ def _copy_from_device(dst: int, src: "DeviceSource", nbytes: int) -> None:
         _copy_chunks(dst, src, nbytes, bufs, stream, evs)
 
 
-def _egress_chunks(nbytes: int) -> List[tuple]:
-    """(offset, length) of the egress chunks: _EGRESS_CHUNK each, or (_EGRESS_RAMP) ramped at both
-    ends — the first chunk's D2H and the last chunk's copy-out overlap nothing, so the first is
-    _EGRESS_CHUNK / 8 and grows 4x per chunk, and a last chunk above _EGRESS_CHUNK / 4 is split
-    so the final copy-out is at most that."""
-    if not _EGRESS_RAMP:
-        return [(a, min(_EGRESS_CHUNK, nbytes - a)) for a in range(0, nbytes, _EGRESS_CHUNK)]
-    out, a, c = [], 0, max(_EGRESS_CHUNK // 8, 1)
-    while a < nbytes:
-        ln = min(c, nbytes - a)
-        out.append((a, ln))
-        a, c = a + ln, min(c * 4, _EGRESS_CHUNK)
-    tail = _EGRESS_CHUNK // 4
-    if len(out) > 1 and out[-1][1] > tail:
-        a, ln = out.pop()
-        out += [(a, ln - tail), (a + ln - tail, tail)]
-    return out
-
-
 def _copy_chunks(dst, src, nbytes, bufs, stream, evs):
     from accdfl_amd import _lib
 
@@ -744,7 +724,7 @@ def _copy_chunks(dst, src, nbytes, bufs, stream, evs):
     stream.wait_stream(torch.cuda.current_stream(dev))  # the reduce that produced src is done
     flat_u8 = src.flat.view(torch.uint8)
     base = src.offset * src.flat.element_size()
-    chunks = _egress_chunks(nbytes)
+    chunks = [(a, min(_EGRESS_CHUNK, nbytes - a)) for a in range(0, nbytes, _EGRESS_CHUNK)]
 
     def issue(c):
         a, ln = chunks[c]

@@ -1,6 +1,7 @@
 """r04: egress of an averaged 25 M fp32 row from HBM into serialize_model bytes (wire.dumps_state_dict over a
 DeviceSource: chunked D2H through two page-locked bounce buffers, each chunk copied out by the threaded
-memcpy while the next one's D2H runs) at the chunk size ACCDFL_AMD_EGRESS_CHUNK_MB and chunk ramp ACCDFL_AMD_EGRESS_RAMP of this process,
+memcpy while the next one's D2H runs) at the chunk size ACCDFL_AMD_EGRESS_CHUNK_MB of this process (r04y: and the chunk ramp
+ACCDFL_AMD_EGRESS_RAMP of that tree, since removed),
 bound to the GPU's NUMA node (EGRESS_NO_BIND=1: not bound).
 Prints one JSON line: the median ms of 15 encodes and the bytes' check against the row.
 Usage on the GPU box: ACCDFL_AMD_EGRESS_CHUNK_MB=8 python profiles/r04_egress_probe.py"""
@@ -34,7 +35,7 @@ def main():
         data = wire.dumps_state_dict({"w": src})
         ts.append(time.perf_counter() - t0)
     ok = data == wire.dumps_state_dict({"w": flat.cpu()})
-    print(json.dumps({"numa_node_bound": node, "chunk_MB": wire._EGRESS_CHUNK >> 20, "ramp": wire._EGRESS_RAMP, "egress_ms": round(statistics.median(ts[1:]) * 1e3, 3),
+    print(json.dumps({"numa_node_bound": node, "chunk_MB": wire._EGRESS_CHUNK >> 20, "ramp": getattr(wire, "_EGRESS_RAMP", None), "egress_ms": round(statistics.median(ts[1:]) * 1e3, 3),
                       "min_ms": round(min(ts[1:]) * 1e3, 3), "free_ms": round(statistics.median(frees[2:]) * 1e3, 3),
                       "bytes_equal": ok}), flush=True)
 
