@@ -1002,7 +1002,7 @@ _plain_module_cls: Dict[type, bool] = {}
 _PLAIN_MODULE_SET: set = set()  # the classes _plain_module accepts, as the walk extension takes them
 # the tree cloned by the walk extension (walk.cpp clone_value: the same order and memo, no Python call
 # per seeded entry, dict, container or plain module)
-_NATIVE_DICT_CLONE = True
+_NATIVE_CLONE = True
 
 
 def _plain_module(cls: type) -> bool:
@@ -1027,7 +1027,7 @@ def _clone_fallback(v, memo: dict):
 
 
 def _clone_value(v, memo: dict):
-    mod = _lib.walk_module() if _NATIVE_DICT_CLONE else None
+    mod = _lib.walk_module() if _NATIVE_CLONE else None
     if mod is not None:
         return mod.clone_value(v, memo, _ATOMIC, _PLAIN_MODULE_SET, _clone_fallback, OrderedDict)
     t = type(v)

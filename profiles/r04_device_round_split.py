@@ -108,7 +108,7 @@ def split(models, w):
     memo = dict(pm)
     fa._seed_buffers(b0, memo)
     for native in (False, True):
-        fa._NATIVE_DICT_CLONE = native
+        fa._NATIVE_CLONE = native
         row["clone_tree_" + ("native" if native else "python")] = host_us(lambda: fa._clone_value(models[0], dict(memo)))
     row["memo_copy"] = host_us(lambda: dict(memo))
     row["device_round"] = host_us(lambda: fa._device_round(models, w, (dtype, device, numels, table)))

@@ -245,7 +245,7 @@ class _OddModule(nn.Module):
         self.register_buffer("steps", torch.tensor(5))
         self.register_buffer("np", torch.zeros(2), persistent=False)
         self.fh = self.register_forward_hook(lambda m, i, o: None)
-        # containers the native clone (walk.cpp clone_dict) copies itself: a tuple holding a mutable
+        # containers the native clone (walk.cpp clone_value) copies itself: a tuple holding a mutable
         # item (a new tuple), a list holding itself, an OrderedDict out of insertion order, a tuple
         # key, a shared tuple of numbers, an empty set
         self.mixed = (1, [2, 3], "s")
@@ -291,7 +291,7 @@ def test_center_copy_is_a_deepcopy(native, monkeypatch):
     clone matches copy.deepcopy attribute for attribute: same types and key order, fresh
     objects, buffers equal, identity preserved (tied weights, a dict shared by two attributes),
     parameters fresh with the same requires_grad, and the copy runs — with the tree's dicts,
-    tuples and lists cloned by the walk extension (walk.cpp clone_dict) and in Python."""
+    tuples and lists cloned by the walk extension (walk.cpp clone_value) and in Python."""
     import copy
 
     from accdfl_amd import _lib
@@ -300,7 +300,7 @@ def test_center_copy_is_a_deepcopy(native, monkeypatch):
 
     if native and _lib.walk_module() is None:
         pytest.skip("walk extension not built")
-    monkeypatch.setattr(fa, "_NATIVE_DICT_CLONE", native)
+    monkeypatch.setattr(fa, "_NATIVE_CLONE", native)
     m = _OddModule()
     want = copy.deepcopy(m)
     got = _center_copy(m, large=False)
