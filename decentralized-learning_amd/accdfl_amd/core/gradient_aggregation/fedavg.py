@@ -26,7 +26,7 @@ Where the arithmetic runs: always on the HIP device (libdlagg.so).  Models alrea
 on the device are reduced in place of their parameters with no copies; models on several
 GPUs are bucket-sharded over those GPUs (dla_wsum_sharded).  CPU models (every reference
 call site): small rounds (_is_small: rows of at most _SMALL_ROW_BYTES = 64 MiB and under
-_SMALL_ROUND_BYTES = 96 MB of input in all, e.g. the GL merge of two models of any BASELINE
+_SMALL_ROUND_BYTES = 48 MiB of input in all, e.g. the GL merge of two models of any BASELINE
 layout) are packed into page-locked rows that the kernel reads across PCIe
 (dla_host_round_start / _finish) while the result module is built; larger rounds stream element
 chunks through the GPU in one
@@ -185,15 +185,19 @@ def _flat_slices(tensors: List[torch.Tensor], numels: List[int], start: int, end
 
 # Small rounds go through dla_host_round_* (one native call packs every peer into page-locked rows
 # and enqueues the reduce, which reads them across PCIe; one call waits and unpacks) instead of the
-# chunked dla_host_reduce: below ~96 MB of input the kernel's own PCIe reads beat the chunked DMAs
-# (no pack-before-DMA fill, no per-chunk round trips).  Measured on the reference layouts, us
+# chunked dla_host_reduce: below ~48 MB of input the one-shot round is as fast or faster (no per-chunk
+# round trips); above it the chunked round's pack / PCIe overlap wins.  Round 4, both paths reading
+# page-locked rows with the kernel, ms small / chunked (profiles/r04s2/small_large_ab.jsonl, pageable
+# peers): GNLeNet 8 peers 0.160 / 0.154, 64 peers (21.9 MB) 0.653 / 0.689; FEMNIST 2 peers 0.540 /
+# 0.555, 4 peers (27 MB) 0.880 / 0.933, 8 peers (54 MB) 1.884 / 1.493; ResNet-8 2 peers (39.5 MB)
+# 1.586 / 1.620, 4 peers (79 MB) 2.913 / 2.362.  Round 2 (staging DMAs then), us
 # small / dla_host_reduce (profiles/r02zo_layout_paths.log): FEMNIST 2 peers 619 / 828, 4 peers
 # 943 / 1343, 8 peers (54 MB) 1644-1882 / 1759-1979, 32 peers (216 MB) 6152 / 4704; ResNet-8 2 peers
 # 1393-2496 / 2290-2780, 3 peers 1895 / 2587, 4 peers (79 MB) 2497 / 2966, 8 peers (158 MB)
 # 4951 / 4213; GNLeNet 8 peers 257 / 367, 64 peers 1084 / 1528.  (Round 2 first bounded it at
 # 2 MiB per row against the per-tensor pipelined path, profiles/r02s_small_round_crossover.log.)
 _SMALL_ROW_BYTES = 64 << 20
-_SMALL_ROUND_BYTES = 96 << 20
+_SMALL_ROUND_BYTES = 48 << 20
 
 
 def _is_small(n: int, row_bytes: int) -> bool:

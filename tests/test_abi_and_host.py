@@ -567,7 +567,9 @@ def test_host_round_routing_and_chunks():
     mb = 1 << 20
     assert fa._is_small(2, 341_416)                       # GL merge of two GNLeNet models
     assert fa._is_small(2, 19_729_376)                    # GL merge of two ResNet-8 models (19.7 MB rows)
-    assert fa._is_small(4, 19_729_376)                    # 79 MB
+    assert fa._is_small(4, 6_760_184)                     # four FEMNIST models, 27 MB
+    assert not fa._is_small(4, 19_729_376)                # 79 MB: dla_host_reduce (profiles/r04s2)
+    assert not fa._is_small(8, 6_760_184)                 # 54 MB: dla_host_reduce
     assert not fa._is_small(8, 19_729_376)                # 158 MB: dla_host_reduce
     assert not fa._is_small(32, 6_760_184)                # configs[2], 216 MB
     assert not fa._is_small(1, 65 * mb) and not fa._is_small(2, 0)

@@ -242,8 +242,8 @@ def test_resnet34_layout_through_fedavg_aggregate(placement):
 def test_config_layouts_through_fedavg_aggregate(name, n, dtype):
     """configs[3'] ResNet-8 (64 peers, 32 tensors, 4.93 M params) and configs[2] FEMNIST CNN
     (32 peers, 8 tensors, 1.69 M params) through FedAvg.aggregate on CPU modules (dla_host_reduce),
-    and the GL-merge-sized rounds of the same layouts (2-8 peers, < 96 MB: the small-round path
-    with 19.7 MB rows), every element against the oracle."""
+    and the GL-merge-sized rounds of the same layouts (2-8 peers: the small-round path below 48 MiB,
+    with 19.7 MB rows, dla_host_reduce above), every element against the oracle."""
     from accdfl_amd.core.gradient_aggregation.fedavg import FedAvg
 
     lay = LAYOUTS[name]
