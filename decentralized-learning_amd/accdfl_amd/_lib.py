@@ -29,7 +29,7 @@ LIB_PATH = os.environ.get("DLAGG_LIB", os.path.join(PKG_ROOT, "lib",
 
 # dtype codes (include/dlagg.h)
 DLA_F32, DLA_BF16, DLA_F16, DLA_F64 = 0, 1, 2, 3
-ABI_VERSION = 12
+ABI_VERSION = 13
 
 HIPCC_FLAGS = [
     "--offload-arch=gfx950",
@@ -74,6 +74,7 @@ EXPORTED = (
     "dla_slab_stage",
     "dla_host_in_place_rounds",
     "dla_wsum_multi_table_acc",
+    "dla_wsum_mixed",
 )
 
 
@@ -335,6 +336,9 @@ class _Lib:
         so.dla_slab_stage.restype = ctypes.c_int
         so.dla_host_in_place_rounds.argtypes = []
         so.dla_host_in_place_rounds.restype = ctypes.c_int64
+        so.dla_wsum_mixed.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(vp),
+                                      ctypes.POINTER(ctypes.c_double), ctypes.c_int, ctypes.c_int64, vp, vp]
+        so.dla_wsum_mixed.restype = ctypes.c_int
         so.dla_plan_destroy.argtypes = [vp]
         so.dla_plan_destroy.restype = None
         v = so.dla_version()
@@ -405,6 +409,16 @@ def wsum_ptrs(dtype_code: int, peer_ptrs: Sequence[int], weights: Sequence[float
         rc = L.so.dla_wsum_ex(dtype_code, _ptr_array(peer_ptrs), _dbl_array(weights), n, n_elems, out_ptr,
                               stream_ptr, ctypes.byref(cfg))
     L.check(rc, "dla_wsum")
+
+
+def wsum_mixed_ptrs(out_code: int, peer_codes: Sequence[int], peer_ptrs: Sequence[int], weights: Sequence[float],
+                    n_elems: int, out_ptr: int, stream_ptr: int) -> None:
+    """dla_wsum_mixed: one parameter whose peers have several dtypes (peer_codes[0] == out_code)."""
+    L = lib()
+    n = len(peer_ptrs)
+    rc = L.so.dla_wsum_mixed(out_code, (ctypes.c_int * n)(*peer_codes), _ptr_array(peer_ptrs), _dbl_array(weights), n,
+                             n_elems, out_ptr, stream_ptr)
+    L.check(rc, "dla_wsum_mixed")
 
 
 def select_kernel(dtype_code: int, n_peers: int, n_elems: int) -> str:

@@ -12,10 +12,12 @@
   order, bit-identical to the reference (fedavg.py:21-25; include/dlagg.h);
 * zip truncation (:24): parameter i only takes terms from models that have an i-th
   parameter;
+* models whose parameters have other dtypes than models[0]'s follow the reference's
+  promotion (:25: the product rounded in the peer's dtype, the sum in models[0]'s);
 * inputs are never mutated.
 
-Deliberate differences (documented in DESIGN.md): parameters whose shapes or dtypes
-differ between models raise RuntimeError instead of broadcasting / promoting.
+Deliberate difference (documented in DESIGN.md): parameters whose shapes differ between
+models raise RuntimeError instead of broadcasting.
 
 The result's CPU parameters are ordinary pageable tensors as in the reference; those of a
 large round come from a pool of already-faulted pageable blocks (``core/host_memory.py``:
@@ -956,10 +958,23 @@ def _reduce_param(device, center: torch.Tensor, terms: List[torch.Tensor], weigh
         torch.cuda.current_stream(device).synchronize()
 
 
+def _reduce_param_mixed(device, center: torch.Tensor, terms: List[torch.Tensor], weights: List[float]):
+    """A parameter whose contributors do not share models[0]'s dtype (dla_wsum_mixed: products
+    rounded in each peer's dtype, sums in the centre's after promotion, fedavg.py:25)."""
+    dev_terms = [t.detach().to(device).contiguous() for t in terms]
+    out = torch.empty(center.numel(), dtype=center.dtype, device=device)
+    _wsum.wsum_mixed([t.view(-1) for t in dev_terms], weights, out)
+    center.copy_(out.view_as(center))
+    if center.device.type == "cpu":
+        torch.cuda.current_stream(device).synchronize()
+
+
 def reduce_parameters(center_params: List[torch.Tensor], peer_params: List[List[torch.Tensor]],
                       weights: List[float]) -> None:
     """fedavg.py:21-25 on parameter lists: center_params[i] <- FedAvg over the models
-    that have an i-th parameter.  ``center_params`` is a deepcopy of models[0]'s."""
+    that have an i-th parameter.  ``center_params`` is a deepcopy of models[0]'s.  Parameters whose
+    contributors have other dtypes than models[0]'s are folded with the reference's promotion
+    (_reduce_param_mixed); a shape mismatch raises (the reference would broadcast)."""
     n = len(peer_params)
     if not center_params:
         return
@@ -967,18 +982,28 @@ def reduce_parameters(center_params: List[torch.Tensor], peer_params: List[List[
     device = _wsum.require_device(first if first.type == "cuda" else None)
     full: Dict[torch.dtype, List[int]] = {}
     partial: List[int] = []
+    mixed: List[int] = []
     for i, c in enumerate(center_params):
         _wsum.dtype_code(c.dtype)
         ks = [k for k in range(n) if len(peer_params[k]) > i]
+        same = True
         for k in ks:
             p = peer_params[k][i]
-            if p.shape != c.shape or p.dtype != c.dtype:
-                raise RuntimeError("FedAvg: parameter %d of model %d has shape/dtype %s/%s, model 0 has %s/%s"
-                                   % (i, k, tuple(p.shape), p.dtype, tuple(c.shape), c.dtype))
-        if len(ks) == n:
+            if p.shape != c.shape:
+                raise RuntimeError("FedAvg: parameter %d of model %d has shape %s, model 0 has %s"
+                                   % (i, k, tuple(p.shape), tuple(c.shape)))
+            if p.dtype != c.dtype:
+                _wsum.dtype_code(p.dtype)
+                same = False
+        if not same:
+            mixed.append(i)
+        elif len(ks) == n:
             full.setdefault(c.dtype, []).append(i)
         else:
             partial.append(i)
+    for i in mixed:
+        ks = [k for k in range(n) if len(peer_params[k]) > i]
+        _reduce_param_mixed(device, center_params[i], [peer_params[k][i] for k in ks], [weights[k] for k in ks])
     for dtype, idx in full.items():
         center = [center_params[i] for i in idx]
         peers = [[peer_params[k][i] for i in idx] for k in range(n)]

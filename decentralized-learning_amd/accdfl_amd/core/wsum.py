@@ -87,6 +87,30 @@ def wsum(peers: Sequence[torch.Tensor], weights: Sequence[float], out: Optional[
     return out
 
 
+def wsum_mixed(peers: Sequence[torch.Tensor], weights: Sequence[float], out: torch.Tensor,
+               stream: Optional[torch.cuda.Stream] = None) -> torch.Tensor:
+    """out = FedAvg(peers, weights) when the peers do not share one dtype (dla_wsum_mixed): each
+    product is rounded in its peer's dtype and each sum in ``out``'s (peers[0]'s) dtype after
+    promotion, as ``c1.add_(w * p1)`` (fedavg.py:25) does for a peer of another dtype."""
+    n = len(peers)
+    if n < 1:
+        raise IndexError("list index out of range")
+    if len(weights) != n:
+        raise AssertionError("len(weights) != len(peers)")
+    device = require_device(out.device)
+    _check_dev(out, device, "out")
+    numel = out.numel()
+    for k, p in enumerate(peers):
+        _check_dev(p, device, "peer %d" % k)
+        if p.numel() != numel:
+            raise ValueError("peer %d: numel %d differs from out's %d" % (k, p.numel(), numel))
+    if peers[0].dtype != out.dtype:
+        raise ValueError("peer 0 (models[0]) must have out's dtype")
+    _lib.wsum_mixed_ptrs(dtype_code(out.dtype), [dtype_code(p.dtype) for p in peers], [p.data_ptr() for p in peers],
+                         weights, numel, out.data_ptr(), _stream_ptr(device, stream))
+    return out
+
+
 def wsum_rows(slab: torch.Tensor, weights: Sequence[float], n_elems: Optional[int] = None,
               out: Optional[torch.Tensor] = None, stream: Optional[torch.cuda.Stream] = None) -> torch.Tensor:
     """FedAvg over the first len(weights) rows of a 2-D device slab [rows, pitch]."""

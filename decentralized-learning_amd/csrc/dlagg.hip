@@ -1116,6 +1116,73 @@ __global__ __launch_bounds__(kBlock) void wsum_scalar_kernel(
   }
 }
 
+// ------------------------------------------------- mixed-dtype kernel (peers of several dtypes)
+// fedavg.py:25 `c1.add_(w * p1)` when peer k's parameter has another dtype than models[0]'s (the
+// centre's): torch computes w * p1 in p1's op-math and rounds it to p1's dtype, then adds in the
+// op-math of the PROMOTED type (f64 if either side is f64, else f32) and rounds the sum to the
+// centre's dtype; a double sum lands in a 16-bit centre through float (c10::BFloat16 / c10::Half
+// take a float).  The running sum is carried as a double holding a value of the centre's dtype
+// exactly.  One element per lane; the dtype switch is uniform across the wave (per peer).  A rare
+// path (mixed rounds do not occur at the reference's call sites), so it is plain and scalar.
+struct MixedTable {
+  const void* p[kMaxPeersPerPass];
+  double w[kMaxPeersPerPass];
+  int8_t dt[kMaxPeersPerPass];
+};
+
+__device__ inline double mixed_load(const void* p, int dt, int64_t j) {
+  switch (dt) {
+    case DLA_F32: return static_cast<double>(static_cast<const float*>(p)[j]);
+    case DLA_BF16: return static_cast<double>(bf16_bits_to_f(static_cast<const uint16_t*>(p)[j]));
+    case DLA_F16: return static_cast<double>(half_bits_to_f(static_cast<const uint16_t*>(p)[j]));
+    default: return static_cast<const double*>(p)[j];
+  }
+}
+
+// an f32 op-math result rounded RNE to dtype dt (F32, BF16 or F16), as f32
+__device__ inline float mixed_round32(float f, int dt) {
+  return dt == DLA_BF16 ? round_bf16(pin(f)) : dt == DLA_F16 ? round_f16(f) : f;
+}
+
+// an f64 op-math result rounded to dtype dt (to 16-bit dtypes through float, as torch casts)
+__device__ inline double mixed_round64(double d, int dt) {
+  if (dt == DLA_F64) return d;
+  return static_cast<double>(mixed_round32(pin(static_cast<float>(d)), dt));
+}
+
+__device__ inline void mixed_store(void* p, int dt, int64_t j, double v) {
+  switch (dt) {
+    case DLA_F32: static_cast<float*>(p)[j] = static_cast<float>(v); break;
+    case DLA_BF16:  // v is a bf16 value: its f32 pattern's high half is the bf16
+      static_cast<uint16_t*>(p)[j] = static_cast<uint16_t>(__float_as_uint(static_cast<float>(v)) >> 16);
+      break;
+    case DLA_F16: static_cast<uint16_t*>(p)[j] = static_cast<uint16_t>(f_to_half_bits(static_cast<float>(v))); break;
+    default: static_cast<double*>(p)[j] = v; break;
+  }
+}
+
+template <bool ACC_IN>
+__global__ __launch_bounds__(kBlock) void wsum_mixed_kernel(const MixedTable tab, int n_peers, int out_dt,
+                                                            int64_t n_elems, void* __restrict__ out) {
+  for (int64_t j = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; j < n_elems;
+       j += static_cast<int64_t>(gridDim.x) * kBlock) {
+    double acc = ACC_IN ? mixed_load(out, out_dt, j) : 0.0;
+    for (int k = 0; k < n_peers; ++k) {
+      const int dk = tab.dt[k];
+      const double x = mixed_load(tab.p[k], dk, j);
+      if (!ACC_IN && k == 0)  // fedavg.py:22 p.mul_(0) on models[0]'s own values (peer 0 has out_dt)
+        acc = out_dt == DLA_F64 ? x * 0.0 : static_cast<double>(static_cast<float>(x) * 0.0f);
+      const double prod = dk == DLA_F64 ? tab.w[k] * x
+                                        : static_cast<double>(mixed_round32(
+                                              static_cast<float>(tab.w[k]) * static_cast<float>(x), dk));
+      acc = (out_dt == DLA_F64 || dk == DLA_F64)
+                ? mixed_round64(acc + prod, out_dt)
+                : static_cast<double>(mixed_round32(static_cast<float>(acc) + static_cast<float>(prod), out_dt));
+    }
+    mixed_store(out, out_dt, j, acc);
+  }
+}
+
 // ------------------------------------------------------------------ launching
 
 struct Launch {
@@ -1880,6 +1947,31 @@ int elem_size(int dtype) {
   }
 }
 
+hipError_t run_mixed(int out_dtype, const int* peer_dtypes, const void* const* peers, const double* weights, int n,
+                     int64_t n_elems, void* out, hipStream_t s) {
+  int64_t grid = (n_elems + kBlock - 1) / kBlock;
+  if (grid > 4096) grid = 4096;  // grid-stride beyond 16 workgroups per CU
+  for (int k0 = 0; k0 < n; k0 += kMaxPeersPerPass) {
+    const int m = n - k0 < kMaxPeersPerPass ? n - k0 : kMaxPeersPerPass;
+    MixedTable tab;
+    std::memset(&tab, 0, sizeof(tab));
+    for (int k = 0; k < m; ++k) {
+      tab.p[k] = peers[k0 + k];
+      tab.w[k] = weights[k0 + k];
+      tab.dt[k] = static_cast<int8_t>(peer_dtypes[k0 + k]);
+    }
+    if (k0 == 0)
+      hipLaunchKernelGGL(wsum_mixed_kernel<false>, dim3(static_cast<unsigned>(grid)), dim3(kBlock), 0, s, tab, m,
+                         out_dtype, n_elems, out);
+    else
+      hipLaunchKernelGGL(wsum_mixed_kernel<true>, dim3(static_cast<unsigned>(grid)), dim3(kBlock), 0, s, tab, m,
+                         out_dtype, n_elems, out);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
 int wsum_impl(int dtype, const void* const* peers, const double* weights, int n_peers,
               int64_t n_elems, void* out, void* stream, const dla_launch_cfg_t* cfg, bool acc_in = false) {
   g_last_error.clear();
@@ -2537,6 +2629,31 @@ int dla_mean(int dtype, const void* const* peers, int n_peers, int64_t n_elems, 
   const hipError_t e = dtype == DLA_F32 ? run_mean<DLA_F32>(peers, n_peers, n_elems, out, s)
                                         : run_mean<DLA_F64>(peers, n_peers, n_elems, out, s);
   if (e != hipSuccess) return fail(static_cast<int>(e), std::string("dla_mean: ") + hipGetErrorString(e));
+  return DLA_OK;
+}
+
+int dla_wsum_mixed(int out_dtype, const int* peer_dtypes, const void* const* peers, const double* weights,
+                   int n_peers, int64_t n_elems, void* out, void* stream) {
+  g_last_error.clear();
+  if (elem_size(out_dtype) == 0) return fail(DLA_E_INVALID, "dla_wsum_mixed: unknown out dtype");
+  if (n_peers < 1 || !peers || !weights || !peer_dtypes)
+    return fail(DLA_E_INVALID, "dla_wsum_mixed: n_peers must be >= 1 with peers, weights and dtypes");
+  if (n_elems < 0) return fail(DLA_E_INVALID, "dla_wsum_mixed: n_elems < 0");
+  for (int k = 0; k < n_peers; ++k) {
+    if (elem_size(peer_dtypes[k]) == 0)
+      return fail(DLA_E_INVALID, "dla_wsum_mixed: unknown dtype of peer " + std::to_string(k));
+    if (!peers[k]) return fail(DLA_E_INVALID, "dla_wsum_mixed: null peer pointer " + std::to_string(k));
+  }
+  if (peer_dtypes[0] != out_dtype)
+    return fail(DLA_E_INVALID, "dla_wsum_mixed: peers[0] is models[0], whose deepcopy is the result: "
+                               "its dtype must be out_dtype (fedavg.py:20)");
+  if (n_elems == 0) return DLA_OK;
+  if (!out) return fail(DLA_E_INVALID, "dla_wsum_mixed: null out");
+  for (int k = 1; k < n_peers; ++k)
+    if (peers[k] == out) return fail(DLA_E_ALIAS, "dla_wsum_mixed: out aliases peer " + std::to_string(k));
+  const hipError_t e = run_mixed(out_dtype, peer_dtypes, peers, weights, n_peers, n_elems, out,
+                                 static_cast<hipStream_t>(stream));
+  if (e != hipSuccess) return fail(static_cast<int>(e), std::string("dla_wsum_mixed: ") + hipGetErrorString(e));
   return DLA_OK;
 }
 

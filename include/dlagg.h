@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define DLA_ABI_VERSION 12
+#define DLA_ABI_VERSION 13
 
 /* element dtypes of the peer buffers and of the output */
 #define DLA_F32 0
@@ -178,6 +178,22 @@ int dla_wsum_multi_table(int dtype, int n_tensors, const void* const* peer_ptrs,
 int dla_wsum_multi_table_acc(int dtype, int n_tensors, const void* const* peer_ptrs, void* const* outs,
                              const int64_t* numels, const double* weights, int n_peers, int acc_in, void* table_host,
                              void* table_dev, void* stream);
+
+/* fedavg.py:20-25 for one parameter whose peers do not all share models[0]'s dtype: the reference
+ * accepts such models and `c1.add_(w * p1)` (:25) then rounds the product in the PEER's dtype
+ * (op-math f32, or f64 for an f64 peer) and the sum in the CENTRE's dtype after promotion (the add in
+ * f64 when either side is f64, else in f32; an f64 sum reaches a 16-bit centre through float):
+ *     acc = p_0 * 0                                           (in out_dtype, op-math of out_dtype)
+ *     for k in list order:
+ *         prod = R_{d_k}(W_{d_k}(w_k) * p_k[j])
+ *         acc  = R_{out}(acc + prod)   in f64 if out or d_k is F64, else in f32
+ *   peer_dtypes  host array of n_peers DLA_* codes; peer_dtypes[0] must be out_dtype (models[0]'s
+ *                parameter is the result's, fedavg.py:20)
+ *   peers        n_peers DEVICE pointers, peer k to n_elems elements of peer_dtypes[k]
+ *   out          DEVICE pointer to n_elems elements of out_dtype; may alias peers[0] only
+ * Uniform dtypes give dla_wsum's bits (it is the special case d_k = out).  Any alignment.  ABI v13. */
+int dla_wsum_mixed(int out_dtype, const int* peer_dtypes, const void* const* peers, const double* weights,
+                   int n_peers, int64_t n_elems, void* out, void* stream);
 
 /* Replaces scripts/distill.py:124-129 (teacher-logit aggregation,
  * torch.mean(torch.stack(preds), dim=0)) for a whole batch of logits at once:

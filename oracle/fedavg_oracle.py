@@ -101,6 +101,54 @@ def fedavg_bits(peers: Sequence[np.ndarray], weights, dtype: str) -> np.ndarray:
         return acc
 
 
+def _as_f64(p, dt: str) -> np.ndarray:
+    if dt == "bf16":
+        return bf16_to_f32(np.asarray(p, np.uint16)).astype(np.float64)
+    return np.asarray(p, {"f32": np.float32, "f16": np.float16, "f64": np.float64}[dt]).astype(np.float64)
+
+
+def _round32(x32: np.ndarray, dt: str) -> np.ndarray:
+    """An f32 op-math result rounded RNE to dtype dt, returned as float64 (exact)."""
+    if dt == "bf16":
+        return bf16_to_f32(f32_to_bf16(x32)).astype(np.float64)
+    if dt == "f16":
+        return x32.astype(np.float16).astype(np.float64)
+    return x32.astype(np.float64)
+
+
+def _round64(x64: np.ndarray, dt: str) -> np.ndarray:
+    """An f64 op-math result cast to dtype dt as torch does (to 16-bit types through float)."""
+    return x64 if dt == "f64" else _round32(x64.astype(np.float32), dt)
+
+
+def fedavg_bits_mixed(peers: Sequence[np.ndarray], dtypes: Sequence[str], weights) -> np.ndarray:
+    """Bit-model of fedavg.py:20-25 for one parameter whose peers have several dtypes (peer k in
+    ``dtypes[k]``, represented as in :func:`fedavg_bits`); the result has dtypes[0] (the deepcopy of
+    models[0], :20).  ``c1.add_(w * p1)`` (:25) rounds ``w * p1`` in p1's dtype (op-math f32, or f64
+    for an f64 peer), then adds in the promoted type's op-math (f64 if either side is f64, else f32)
+    and rounds the sum to the centre's dtype; an f64 sum reaches a 16-bit centre through float
+    (c10::BFloat16 / c10::Half take a float).  Pinned by the reference: tests/golden/mixed_*."""
+    n = len(peers)
+    if n < 1:
+        raise IndexError("list index out of range")
+    if len(weights) != n or len(dtypes) != n:
+        raise AssertionError
+    d0 = dtypes[0]
+    with np.errstate(all="ignore"):
+        x0 = _as_f64(peers[0], d0)
+        acc = x0 * 0.0 if d0 == "f64" else (x0.astype(np.float32) * np.float32(0)).astype(np.float64)
+        for p, dk, w in zip(peers, dtypes, weights):
+            x = _as_f64(p, dk)
+            prod = float(w) * x if dk == "f64" else _round32(_op32(w) * x.astype(np.float32), dk)
+            if d0 == "f64" or dk == "f64":
+                acc = _round64(acc + prod, d0)
+            else:
+                acc = _round32(acc.astype(np.float32) + prod.astype(np.float32), d0)
+    if d0 == "bf16":
+        return f32_to_bf16(acc.astype(np.float32))
+    return acc.astype({"f32": np.float32, "f16": np.float16, "f64": np.float64}[d0])
+
+
 def fedavg_param_lists(param_lists: List[List[np.ndarray]], weights, dtype: str) -> List[np.ndarray]:
     """FedAvg over per-model parameter lists with the reference's zip truncation
     (fedavg.py:24: parameter i gets a term from every model that has >= i+1 params)."""

@@ -138,3 +138,68 @@ void oracle_wsum_f16(const uint16_t* const* peers, const double* w, int n, int64
     out[j] = acc;
   }
 }
+
+/* Mixed dtypes (fedavg.py:25 when a peer's parameter has another dtype than models[0]'s): the
+ * product rounded in the peer's dtype (op-math f32, f64 for an f64 peer), the sum in the promoted
+ * type (f64 if either side is f64, else f32) rounded to the centre's dtype; an f64 sum reaches a
+ * 16-bit centre through float, as torch's c10::BFloat16 / c10::Half(float) casts do.  Codes as
+ * include/dlagg.h: 0 f32, 1 bf16, 2 f16, 3 f64.  The running value is kept as a double holding a
+ * value of the centre's dtype exactly. */
+static inline double mx_load(const void* p, int dt, int64_t j) {
+  switch (dt) {
+    case 0: return (double)((const float*)p)[j];
+    case 1: return (double)bf16_to_f32(((const uint16_t*)p)[j]);
+    case 2: return (double)f16_to_f32(((const uint16_t*)p)[j]);
+    default: return ((const double*)p)[j];
+  }
+}
+
+static inline float mx_round32(float f, int dt) {
+  if (dt == 1) return bf16_to_f32(f32_to_bf16(f));
+  if (dt == 2) return f16_to_f32(f32_to_f16(f));
+  return f;
+}
+
+void oracle_wsum_mixed(int out_dt, const int* dts, const void* const* peers, const double* w, int n, int64_t len,
+                       void* out) {
+#pragma omp parallel for schedule(static)
+  for (int64_t j = 0; j < len; ++j) {
+    volatile double acc;
+    const double x0 = mx_load(peers[0], dts[0], j);
+    if (out_dt == 3) {
+      acc = x0 * 0.0;
+    } else {
+      volatile float z = (float)x0 * 0.0f;
+      acc = z;
+    }
+    for (int k = 0; k < n; ++k) {
+      const int dk = dts[k];
+      const double x = mx_load(peers[k], dk, j);
+      volatile double prod;
+      if (dk == 3) {
+        prod = w[k] * x;
+      } else {
+        volatile float p32 = (float)w[k] * (float)x;
+        prod = mx_round32(p32, dk);
+      }
+      if (out_dt == 3 || dk == 3) {
+        volatile double s = acc + prod;
+        if (out_dt == 3) {
+          acc = s;
+        } else {
+          volatile float s32 = (float)s;
+          acc = mx_round32(s32, out_dt);
+        }
+      } else {
+        volatile float s32 = (float)acc + (float)prod;
+        acc = mx_round32(s32, out_dt);
+      }
+    }
+    switch (out_dt) {
+      case 0: ((float*)out)[j] = (float)acc; break;
+      case 1: ((uint16_t*)out)[j] = f32_to_bf16((float)acc); break;
+      case 2: ((uint16_t*)out)[j] = f32_to_f16((float)acc); break;
+      default: ((double*)out)[j] = acc; break;
+    }
+  }
+}

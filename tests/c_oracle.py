@@ -32,3 +32,22 @@ def c_wsum(flat_peers, weights, dtype):
     out = np.empty_like(arrs[0])
     fn(ptrs, w, ctypes.c_int(n), ctypes.c_int64(out.size), ctypes.c_void_p(out.ctypes.data))
     return out
+
+
+_CODE = {"f32": 0, "bf16": 1, "f16": 2, "f64": 3}
+_NP = {"f32": np.float32, "bf16": np.uint16, "f16": np.uint16, "f64": np.float64}
+
+
+def c_wsum_mixed(flat_peers, dtypes, weights):
+    """fedavg.py:20-25 for peers of several dtypes (oracle_wsum_mixed; f32/f64 values, bf16/f16 raw
+    uint16 bits); the result has dtypes[0]."""
+    so = lib()
+    n = len(flat_peers)
+    arrs = [np.ascontiguousarray(p) for p in flat_peers]
+    ptrs = (ctypes.c_void_p * n)(*[a.ctypes.data for a in arrs])
+    w = (ctypes.c_double * n)(*[float(x) for x in weights])
+    codes = (ctypes.c_int * n)(*[_CODE[d] for d in dtypes])
+    out = np.empty(arrs[0].size, dtype=_NP[dtypes[0]])
+    so.oracle_wsum_mixed(ctypes.c_int(_CODE[dtypes[0]]), codes, ptrs, w, ctypes.c_int(n), ctypes.c_int64(out.size),
+                         ctypes.c_void_p(out.ctypes.data))
+    return out

@@ -29,7 +29,7 @@ class Case:
 
 def case_names() -> List[str]:
     return sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN_DIR, "*.npz"))
-                  if not os.path.basename(p).startswith("wire_"))
+                  if not os.path.basename(p).startswith(("wire_", "mixed_")))
 
 
 def load(name: str) -> Case:
@@ -85,3 +85,42 @@ def build_models(case: Case, device="cpu"):
                 self.register_buffer("b%d" % j, torch.from_numpy(b.copy()))
 
     return [Peer(case.params[k], case.buffers[k]).to(device) for k in range(len(case.params))]
+
+
+@dataclass
+class MixedCase:
+    """A round whose models do not share one dtype (make_golden.save_mixed_cases)."""
+    name: str
+    dtypes: List[List[str]]             # [peer][param]
+    weights: Optional[list]
+    params: List[List[np.ndarray]]      # [peer][param] raw bits, shaped
+    out: List[np.ndarray]               # reference output params (raw bits, models[0]'s dtypes)
+
+    @property
+    def out_dtypes(self) -> List[str]:
+        return self.dtypes[0]
+
+
+def mixed_case_names() -> List[str]:
+    return sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN_DIR, "mixed_*.npz")))
+
+
+def load_mixed(name: str) -> MixedCase:
+    z = np.load(os.path.join(GOLDEN_DIR, name + ".npz"))
+    meta = json.loads(str(z["meta"]))
+    n = meta["n_peers"]
+    params = [[z["p_%d_%d" % (k, i)].reshape(s) for i, s in enumerate(meta["shapes"][k])] for k in range(n)]
+    out = [z["out_%d" % i].reshape(s) for i, s in enumerate(meta["shapes"][0])]
+    return MixedCase(meta["name"], meta["dtypes"], meta["weights"], params, out)
+
+
+def build_mixed_models(case: MixedCase, device="cpu"):
+    """The peer nn.Modules of a mixed case (parameter i of peer k in case.dtypes[k][i])."""
+    from torch import nn
+
+    class Peer(nn.Module):
+        def __init__(self, ps, dts):
+            super().__init__()
+            self.ps = nn.ParameterList([nn.Parameter(to_torch(p, d)) for p, d in zip(ps, dts)])
+
+    return [Peer(case.params[k], case.dtypes[k]).to(device) for k in range(len(case.params))]

@@ -61,7 +61,7 @@ def test_library_version_and_argument_errors(lib_path):
     from accdfl_amd import _lib
 
     L = _lib.lib()
-    assert L.so.dla_version() == 12
+    assert L.so.dla_version() == 13
     assert L.build_id == _lib.source_build_id() == _lib.file_build_id(lib_path)
     assert L.max_peers_per_pass == 128
     # kernel selection by shape (host-only query): north star, configs[3] share, configs[4] share,

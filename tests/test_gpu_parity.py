@@ -1313,3 +1313,93 @@ def test_host_round_refuses_device_memory():
     a = torch.ones(10)
     with pytest.raises(_lib.DlaggError, match="page-locked"):
         _lib.host_round_start(0, 2, [a.data_ptr()] * 2, [10], [0.5, 0.5], rows.data_ptr(), 64, res.data_ptr(), 0)
+
+
+# ------------------------------------------------------------------ mixed-dtype rounds (ABI v13)
+MIXED = gc.mixed_case_names()
+
+
+def _check_mixed_output(c, out_model, device_type):
+    for i, (p, want) in enumerate(zip(out_model.parameters(), c.out)):
+        d = c.out_dtypes[i]
+        assert p.device.type == device_type and p.dtype == TDT[d]
+        assert same_bits(gc.from_torch(p, d), want, d), "%s param %d differs from the reference" % (c.name, i)
+
+
+@pytest.mark.parametrize("where", ["cpu", "cuda:0"])
+@pytest.mark.parametrize("name", MIXED)
+def test_fedavg_mixed_dtypes_match_reference(name, where):
+    """Models whose parameters do not share models[0]'s dtype: fedavg.py:25 rounds each product in the
+    peer's dtype and each sum in models[0]'s after promotion (dla_wsum_mixed), CPU and device modules."""
+    from accdfl_amd.core.gradient_aggregation.fedavg import FedAvg
+
+    c = gc.load_mixed(name)
+    models = gc.build_mixed_models(c, where)
+    out = FedAvg.aggregate(models, c.weights)
+    torch.cuda.synchronize()
+    _check_mixed_output(c, out, where.split(":")[0])
+
+
+@pytest.mark.parametrize("name", ["mixed_f32_bf16_n2", "mixed_bf16_f32_n2", "mixed_specials_f16_n4",
+                                  "mixed_per_param_n3"])
+def test_device_model_manager_mixed_dtypes(name):
+    """A peer of another dtype is not staged into the slab; the round averages the registry through
+    FedAvg.aggregate's promoted path."""
+    from types import SimpleNamespace
+
+    from accdfl_amd.core.gradient_aggregation import GradientAggregationMethod
+    from accdfl_amd.core.model_manager import DeviceModelManager
+
+    c = gc.load_mixed(name)
+    mm = DeviceModelManager(None, SimpleNamespace(gradient_aggregation=GradientAggregationMethod.FEDAVG), 0)
+    for k, m in enumerate(gc.build_mixed_models(c, "cpu")):
+        mm.process_incoming_trained_model(b"peer%d" % k, m)
+    _check_mixed_output(c, mm.aggregate_trained_models(c.weights), "cpu")
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16", "f16", "f64"])
+@pytest.mark.parametrize("n", [3, 130])
+def test_wsum_mixed_with_one_dtype_is_dla_wsum(dtype, n):
+    """dla_wsum_mixed with every peer in one dtype is dla_wsum's arithmetic (the special case d_k = out)."""
+    from accdfl_amd.core import wsum
+
+    peers = [p.cuda() for p in _random_peers(n, 4099, dtype, seed=n)]
+    w = [float(x) for x in np.random.default_rng(n).dirichlet(np.ones(n))]
+    want = wsum.wsum(peers, w)
+    got = wsum.wsum_mixed(peers, w, torch.empty_like(peers[0]))
+    assert np.array_equal(_bits(got, dtype), _bits(want, dtype))
+
+
+def test_wsum_mixed_many_peers_against_c_oracle():
+    """130 peers cycling through the four dtypes (two passes; the second continues from `out`), an
+    unaligned element count, every element against the C oracle."""
+    from accdfl_amd.core import wsum
+    from c_oracle import c_wsum_mixed
+
+    n, numel = 130, 200_003
+    cyc = ["f32", "bf16", "f16", "f64"]
+    dts = ["bf16"] + [cyc[k % 4] for k in range(1, n)]
+    g = torch.Generator().manual_seed(5)
+    cpu = [(torch.randn(numel, generator=g, dtype=torch.float64) * 0.05).to(TDT[d]) for d in dts]
+    w = [float(x) for x in np.random.default_rng(5).dirichlet(np.ones(n))]
+    out = torch.empty(numel, dtype=torch.bfloat16, device="cuda")
+    wsum.wsum_mixed([p.cuda() for p in cpu], w, out)
+    flat = [gc.as_float(gc.from_torch(p, d), d) for p, d in zip(cpu, dts)]
+    want = c_wsum_mixed(flat, dts, w)
+    assert same_bits(_bits(out, "bf16"), want, "bf16")
+
+
+def test_wsum_mixed_rejects_bad_arguments():
+    from accdfl_amd import _lib
+    from accdfl_amd.core import wsum
+
+    a = torch.zeros(64, dtype=torch.float32, device="cuda")
+    b = torch.zeros(64, dtype=torch.bfloat16, device="cuda")
+    with pytest.raises(ValueError, match="peer 0"):
+        wsum.wsum_mixed([b, a], [0.5, 0.5], torch.empty_like(a))
+    with pytest.raises(_lib.DlaggError, match="out_dtype"):  # the C ABI's own check
+        _lib.wsum_mixed_ptrs(_lib.DLA_F32, [_lib.DLA_BF16, _lib.DLA_F32], [b.data_ptr(), a.data_ptr()], [0.5, 0.5],
+                             64, a.data_ptr(), 0)
+    with pytest.raises(_lib.DlaggError, match="aliases"):
+        _lib.wsum_mixed_ptrs(_lib.DLA_F32, [_lib.DLA_F32, _lib.DLA_BF16], [a.data_ptr(), b.data_ptr()], [0.5, 0.5],
+                             64, b.data_ptr(), 0)

@@ -115,3 +115,61 @@ def test_timed_flat_ports_match_the_bit_model(dtype):
     want = fedavg_bits([gc.as_float(gc.from_torch(p, name), name) for p in peers], w, name)
     assert same_bits(gc.from_torch(lit, name), gc.from_torch(warm, name), name)
     assert same_bits(gc.as_float(gc.from_torch(warm, name), name), want, name)
+
+
+MIXED = gc.mixed_case_names()
+
+
+def _mixed_terms(c, i):
+    """(flat peer arrays, dtypes, weights) of parameter i of a mixed case, zip truncation applied."""
+    from oracle.fedavg_oracle import default_weights
+
+    n = len(c.params)
+    weights = default_weights(n, c.weights)
+    ks = [k for k in range(n) if len(c.params[k]) > i]
+    return ([gc.as_float(c.params[k][i], c.dtypes[k][i]).reshape(-1) for k in ks], [c.dtypes[k][i] for k in ks],
+            [weights[k] for k in ks])
+
+
+def test_mixed_golden_set_present():
+    # VERDICT r04 Missing #3: fp32 centre with a bf16 peer, bf16 centre with an fp32 peer, an f16 mix
+    for required in ("mixed_f32_bf16_n2", "mixed_bf16_f32_n2", "mixed_f16_bf16_n2", "mixed_specials_f16_n4",
+                     "mixed_many_peers_n130"):
+        assert required in MIXED
+
+
+@pytest.mark.parametrize("name", MIXED)
+def test_mixed_oracles_match_reference(name):
+    """Both restatements of the promoted arithmetic (NumPy and C) against the reference's own bits."""
+    from c_oracle import c_wsum_mixed
+    from oracle.fedavg_oracle import fedavg_bits_mixed
+
+    c = gc.load_mixed(name)
+    for i, want in enumerate(c.out):
+        peers, dts, w = _mixed_terms(c, i)
+        d0 = c.out_dtypes[i]
+        got = fedavg_bits_mixed(peers, dts, w)
+        assert same_bits(np.asarray(got).view(want.dtype), want.reshape(-1), d0), "%s param %d (numpy)" % (name, i)
+        got = c_wsum_mixed(peers, dts, w)
+        assert same_bits(got.view(want.dtype), want.reshape(-1), d0), "%s param %d (C)" % (name, i)
+
+
+@pytest.mark.parametrize("name", MIXED)
+def test_mixed_torch_port_matches_reference(name):
+    c = gc.load_mixed(name)
+    out = fedavg_modules_torch(gc.build_mixed_models(c), c.weights)
+    for i, (p, w) in enumerate(zip(out.parameters(), c.out)):
+        assert same_bits(gc.from_torch(p, c.out_dtypes[i]), w, c.out_dtypes[i]), "%s param %d" % (name, i)
+
+
+def test_mixed_oracle_reduces_to_uniform():
+    """With one dtype the promoted model is fedavg_bits itself (every uniform golden)."""
+    from oracle.fedavg_oracle import fedavg_bits_mixed
+
+    for name in ("specials_bf16_n4", "specials_f16_n4", "specials_f64_n4", "ragged_f32_n3"):
+        c = gc.load(name)
+        for i, want in enumerate(c.out):
+            peers = [gc.as_float(pl[i], c.dtype).reshape(-1) for pl in c.params]
+            from oracle.fedavg_oracle import default_weights
+            got = fedavg_bits_mixed(peers, [c.dtype] * len(peers), default_weights(len(peers), c.weights))
+            assert same_bits(np.asarray(got).view(want.dtype), want.reshape(-1), c.dtype), (name, i)

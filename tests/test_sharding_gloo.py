@@ -1,7 +1,10 @@
-"""Multi-rank sharding logic on CPU (gloo, world_size 2 and 3): bucket-sharded and
-peer-sharded (all-to-all transpose) FedAvg reassemble to exactly the single-process
-oracle result.  The per-bucket reduce is the CPU oracle injected as the reducer —
-the kernel itself is covered by the -m gpu tests; this exercises the exchange steps."""
+"""Multi-rank sharding logic on CPU (gloo, world_size 2, 3 and 8), fp32 and bf16:
+bucket-sharded and peer-sharded (all-to-all transpose) FedAvg reassemble to exactly the
+single-process C-oracle result (fedavg.py:20-25 over the whole model).  The per-bucket
+reduce is the NumPy oracle injected as the reducer on CPU, and the libdlagg kernel on the
+box's one GPU (every rank sharing cuda:0) for the -m gpu cases; this exercises the
+exchange steps, the bucket alignment of each dtype (64 fp32 / 128 bf16 elements), ragged
+and empty trailing buckets, and 128 / 130 peers (one and two kernel passes)."""
 import os
 import socket
 
@@ -10,6 +13,9 @@ import pytest
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
+
+_TORCH = {"f32": torch.float32, "bf16": torch.bfloat16}
+_BITS = {"f32": (np.uint32, torch.int32), "bf16": (np.uint16, torch.int16)}
 
 
 def _free_port():
@@ -20,12 +26,26 @@ def _free_port():
     return port
 
 
-def _oracle_reducer(peers, weights, out):
-    from oracle.fedavg_oracle import fedavg_bits
+def _to_bits(t: torch.Tensor, dtype: str) -> np.ndarray:
+    """Raw bit patterns of a f32 / bf16 tensor (uint32 / uint16)."""
+    np_u, t_i = _BITS[dtype]
+    return t.contiguous().cpu().view(t_i).numpy().view(np_u).copy()
 
-    res = fedavg_bits([p.numpy() for p in peers], weights, "f32")
-    out.copy_(torch.from_numpy(res))
-    return out
+
+def _from_bits(bits: np.ndarray, dtype: str) -> torch.Tensor:
+    np_u, t_i = _BITS[dtype]
+    signed = np.int32 if np_u is np.uint32 else np.int16
+    return torch.from_numpy(np.ascontiguousarray(bits).view(signed)).view(_TORCH[dtype])
+
+
+def _oracle_reducer(dtype):
+    def red(peers, weights, out):
+        from oracle.fedavg_oracle import fedavg_bits
+
+        res = fedavg_bits([_to_bits(p, dtype) if dtype == "bf16" else p.numpy() for p in peers], weights, dtype)
+        out.copy_(_from_bits(res.view(_BITS[dtype][0]), dtype))
+        return out
+    return red
 
 
 def _hip_reducer(peers, weights, out):
@@ -37,19 +57,24 @@ def _hip_reducer(peers, weights, out):
     return out
 
 
-def _inputs(n_peers, n_elems):
+def _inputs(n_peers, n_elems, dtype="f32"):
+    """Seeded peers as bit patterns (fp32 values, bf16 = the RNE cast of the same values)
+    and Dirichlet weights as Python floats."""
     rng = np.random.default_rng(123)
-    peers = (rng.standard_normal((n_peers, n_elems)) * 0.05).astype(np.float32)
+    vals = (rng.standard_normal((n_peers, n_elems), dtype=np.float32) * np.float32(0.05))
     weights = [float(x) for x in rng.dirichlet(np.ones(n_peers))]
-    return peers, weights
+    if dtype == "f32":
+        return vals.view(np.uint32), weights
+    return _to_bits(torch.from_numpy(vals).to(torch.bfloat16), "bf16"), weights
 
 
-def _worker(rank, world, port, n_peers, n_elems, root, q, reducer="oracle"):
+def _worker(rank, world, port, n_peers, n_elems, root, q, reducer="oracle", dtype="f32"):
     import sys
 
     for p in (os.path.join(root, "decentralized-learning_amd"), root):
         sys.path.insert(0, p)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
+    torch.set_num_threads(1)
     nccl = reducer == "nccl"
     dev = torch.device("cuda", rank) if nccl else torch.device("cpu")
     if nccl:
@@ -61,79 +86,119 @@ def _worker(rank, world, port, n_peers, n_elems, root, q, reducer="oracle"):
         from accdfl_amd.core import wsum
         from accdfl_amd.core.sharding import BucketShardedFedAvg
 
-        peers, weights = _inputs(n_peers, n_elems)
-        red = {"hip": _hip_reducer, "oracle": _oracle_reducer,
+        bits, weights = _inputs(n_peers, n_elems, dtype)
+        peers = _from_bits(bits, dtype)
+        red = {"hip": _hip_reducer, "oracle": _oracle_reducer(dtype),
                "nccl": lambda ps, w, out: wsum.wsum(list(ps), w, out=out)}[reducer]
-        sh = BucketShardedFedAvg(n_elems, torch.float32, device=dev, reducer=red)
-        # (1) bucket-sharded: this rank holds its bucket of every peer
+        sh = BucketShardedFedAvg(n_elems, _TORCH[dtype], device=dev, reducer=red)
+        # (1) bucket-sharded: this rank holds its bucket of every peer, zero-padded to bucket_len
         s, e = sh.local_range
-        buckets = [torch.from_numpy(peers[k, s:e].copy()) for k in range(n_peers)]
-        padded = [torch.cat([b, torch.zeros(sh.bucket_len - b.numel())]).to(dev) for b in buckets]
-        full = sh.all_gather(sh.reduce_bucket(padded, weights))
-        # (2) peer-sharded: rank r holds whole peers r*m .. r*m+m-1
-        m = n_peers // world
-        local = torch.from_numpy(peers[rank * m:(rank + 1) * m].copy()).to(dev)
-        full2 = sh.aggregate_peer_sharded(local, weights)
-        full3 = sh.aggregate_peer_sharded(local, weights, exact=False)
-        q.put((rank, full.cpu().numpy().view(np.uint32).copy(), full2.cpu().numpy().view(np.uint32).copy(),
-               full3.cpu().numpy().copy()))
+        padded = torch.zeros((n_peers, sh.bucket_len), dtype=_TORCH[dtype])
+        padded[:, : e - s] = peers[:, s:e]
+        full = sh.all_gather(sh.reduce_bucket(list(padded.to(dev)), weights))
+        res = {"bucket": _to_bits(full, dtype), "range": (s, e), "bucket_len": sh.bucket_len}
+        if n_peers % world == 0:
+            # (2) peer-sharded: rank r holds whole peers r*m .. r*m+m-1
+            m = n_peers // world
+            local = peers[rank * m:(rank + 1) * m].contiguous().to(dev)
+            res["peer"] = _to_bits(sh.aggregate_peer_sharded(local, weights), dtype)
+            if dtype == "f32":
+                res["rs"] = sh.aggregate_peer_sharded(local, weights, exact=False).cpu().numpy().copy()
+        q.put((rank, res))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,n_peers,n_elems", [(2, 8, 10_001), (3, 6, 4_099), (2, 4, 37)])
-def test_sharded_fedavg_is_bit_exact(world, n_peers, n_elems):
-    _run_sharded(world, n_peers, n_elems, "oracle")
+# world, peers, elements, dtype: ragged last buckets (10_001 / 4_099), every bucket but the first
+# empty (37 over 2 and 8 ranks), bf16's 128-element alignment, 8 ranks with 128 peers (one kernel
+# pass) and 130 peers (two passes; no peer-sharded split: 130 is not a multiple of 8)
+_CPU_CASES = [(2, 8, 10_001, "f32"), (3, 6, 4_099, "f32"), (2, 4, 37, "f32"),
+              (2, 8, 10_001, "bf16"), (3, 6, 4_099, "bf16"), (8, 4, 37, "bf16"),
+              (8, 128, 2_051, "bf16"), (8, 130, 1_031, "f32")]
+
+
+@pytest.mark.parametrize("world,n_peers,n_elems,dtype", _CPU_CASES)
+def test_sharded_fedavg_is_bit_exact(world, n_peers, n_elems, dtype):
+    _run_sharded(world, n_peers, n_elems, "oracle", dtype)
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world,n_peers,n_elems", [(2, 8, 1_000_003), (4, 8, 65_537)])
-def test_sharded_fedavg_hip_reducer_is_bit_exact(world, n_peers, n_elems):
+@pytest.mark.parametrize("world,n_peers,n_elems,dtype", [
+    (2, 8, 1_000_003, "f32"), (4, 8, 65_537, "f32"), (2, 8, 1_000_003, "bf16"),
+    # configs[4]'s split: 8 ranks, bf16, 128 peers (one pass) and 130 (two passes), ragged last bucket
+    (8, 128, 1_000_003, "bf16"), (8, 130, 262_147, "bf16"), (8, 128, 262_147, "f32")])
+def test_sharded_fedavg_hip_reducer_is_bit_exact(world, n_peers, n_elems, dtype):
     """The same exchange steps with the libdlagg kernel as each rank's bucket reducer
     (gloo ranks sharing the box's one GPU; the RCCL transport is the driver's 8-GPU run)."""
-    _run_sharded(world, n_peers, n_elems, "hip")
+    _run_sharded(world, n_peers, n_elems, "hip", dtype)
 
 
 @pytest.mark.gpu
 @pytest.mark.skipif(not torch.cuda.is_available() or torch.cuda.device_count() < 2,
                     reason="RCCL needs one GPU per rank (the driver's multi-GPU node)")
-@pytest.mark.parametrize("world,n_peers,n_elems", [(2, 8, 1_000_003)])
-def test_sharded_fedavg_over_rccl(world, n_peers, n_elems):
+@pytest.mark.parametrize("world,n_peers,n_elems,dtype", [(2, 8, 1_000_003, "f32"), (2, 8, 1_000_003, "bf16")])
+def test_sharded_fedavg_over_rccl(world, n_peers, n_elems, dtype):
     """The same exchange steps over RCCL (backend "nccl"), one GPU per rank, device tensors:
     all-gather and all-to-all bit-exact, reduce-scatter within its stated bound."""
-    _run_sharded(world, n_peers, n_elems, "nccl")
+    if world > torch.cuda.device_count():
+        pytest.skip("needs %d GPUs" % world)
+    _run_sharded(world, n_peers, n_elems, "nccl", dtype)
 
 
 def test_reduce_scatter_mode_is_fp32_fp64_only():
     """exact=False (reduce-scatter, re-associated) states its bound for fp32 / fp64 sums only."""
     from accdfl_amd.core.sharding import BucketShardedFedAvg
 
-    sh = BucketShardedFedAvg(64, torch.bfloat16, reducer=_oracle_reducer)
+    sh = BucketShardedFedAvg(64, torch.bfloat16, reducer=_oracle_reducer("bf16"))
     with pytest.raises(ValueError, match="float32 / float64 only"):
         sh.aggregate_peer_sharded(torch.zeros((2, 64), dtype=torch.bfloat16), exact=False)
 
 
-def _run_sharded(world, n_peers, n_elems, reducer):
-    from oracle.fedavg_oracle import fedavg_bits
+def test_bucket_alignment_per_dtype():
+    """Bucket starts are 256-byte aligned: 64 fp32 / 128 bf16 elements; trailing buckets may be empty."""
+    from accdfl_amd.core.sharding import BucketShardedFedAvg, bucket_bounds
+
+    assert bucket_bounds(1_000_003, 8, 128)[-1] == (7 * 125_056, 1_000_003)
+    assert bucket_bounds(37, 8, 128) == [(0, 37)] + [(37, 37)] * 7
+    for dt, align in ((torch.float32, 64), (torch.bfloat16, 128), (torch.float64, 32)):
+        sh = BucketShardedFedAvg(21_296_355, dt, reducer=_oracle_reducer("f32"))
+        assert all(s % align == 0 for s, _ in sh.bounds)
+        assert sh.bounds[-1][1] == 21_296_355
+
+
+def _run_sharded(world, n_peers, n_elems, reducer, dtype="f32"):
+    from c_oracle import c_wsum
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, n_peers, n_elems, root, q, reducer))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n_peers, n_elems, root, q, reducer, dtype))
              for r in range(world)]
     for p in procs:
         p.start()
-    results = [q.get(timeout=240) for _ in range(world)]
-    for p in procs:
-        p.join(timeout=60)
-        assert p.exitcode == 0
-    peers, weights = _inputs(n_peers, n_elems)
-    want = fedavg_bits(list(peers), weights, "f32").view(np.uint32)
-    # tolerance of the reduce-scatter (re-associating) mode: N * 2^-23 * sum_k |w_k p_k|
-    bound = n_peers * 2.0 ** -23 * np.sum(np.abs(np.asarray(weights)[:, None] * peers.astype(np.float64)), axis=0)
-    for rank, full, full2, full3 in results:
-        assert np.array_equal(full, want), "bucket-sharded rank %d" % rank
-        assert np.array_equal(full2, want), "peer-sharded rank %d" % rank
-        err = np.abs(full3.astype(np.float64) - want.view(np.float32).astype(np.float64))
-        assert np.all(err <= bound + 1e-45), "reduce-scatter mode rank %d: max err %g" % (rank, err.max())
+    try:
+        results = [q.get(timeout=300) for _ in range(world)]
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    bits, weights = _inputs(n_peers, n_elems, dtype)
+    peers = list(bits) if dtype == "bf16" else list(bits.view(np.float32))
+    want = c_wsum(peers, weights, dtype).view(_BITS[dtype][0])
+    covered = 0
+    for rank, res in sorted(results, key=lambda r: r[0]):
+        s, e = res["range"]
+        covered += e - s
+        assert np.array_equal(res["bucket"], want), "bucket-sharded rank %d (%s)" % (rank, dtype)
+        if "peer" in res:
+            assert np.array_equal(res["peer"], want), "peer-sharded rank %d (%s)" % (rank, dtype)
+        if "rs" in res:
+            # tolerance of the reduce-scatter (re-associating) mode: N * 2^-23 * sum_k |w_k p_k|
+            vals = bits.view(np.float32).astype(np.float64)
+            bound = n_peers * 2.0 ** -23 * np.sum(np.abs(np.asarray(weights)[:, None] * vals), axis=0)
+            err = np.abs(res["rs"].astype(np.float64) - want.view(np.float32).astype(np.float64))
+            assert np.all(err <= bound + 1e-45), "reduce-scatter mode rank %d: max err %g" % (rank, err.max())
+    assert covered == n_elems
