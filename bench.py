@@ -501,21 +501,31 @@ def cpu_baseline_cold(n, p, threads, budget_s):
             "median_ms": round(row["median_ms"], 1), "reduces": row["reduces"], "threads": threads}
 
 
-def cpu_baseline(n, p, budget_s):
+def cpu_baseline(n, p, budget_s, headline=None):
     """The reference op sequence (deepcopy -> mul_(0) -> add_(w*p)) on torch-CPU, timed on a
     bounded sample of the same workload: repeated full NS reduces until ~budget_s, at the
     process's CPU share (cpu_threads), at every affinity CPU when that differs, and on one
     thread, with the product temporary in a held buffer (fedavg_flat_torch_warm: same ops,
     same bits, no page faults — the sequence at its best).  ``value`` / ``cores`` is the
     fastest of these counts.  ``cold_fresh_process`` times the literal sequence (a fresh
-    temporary per peer) in a new process at the same thread count."""
+    temporary per peer) in a new process at the same thread count.
+
+    ``headline``: (the headline's own peers copied to host, its output copied to host).  The timed
+    reduces then run on exactly the headline's inputs, and the output of the last one is compared
+    bit for bit, every element, with the output the timed GPU headline produced
+    (``headline_oracle_parity``): the driver's bench line is checked against the reference's
+    arithmetic in the run that produced it."""
     sys.path.insert(0, ROOT)
     from oracle.fedavg_oracle import fedavg_flat_torch_warm  # timed CPU baseline (kind "port")
 
     share, how = cpu_threads()
     aff = len(os.sched_getaffinity(0))
-    gen = torch.Generator().manual_seed(1000)
-    peers = [torch.randn(p, generator=gen) * 0.05 for _ in range(n)]
+    if headline is not None:
+        peers, head_out = headline
+    else:
+        gen = torch.Generator().manual_seed(1000)
+        peers = [torch.randn(p, generator=gen) * 0.05 for _ in range(n)]
+        head_out = None
     w = [float(x) for x in np.random.default_rng(0).dirichlet(np.ones(n))]
     out = torch.empty(p)
     tmp = torch.empty(p)
@@ -542,7 +552,16 @@ def cpu_baseline(n, p, budget_s):
     torch.set_num_threads(share)
     best = min((v[0], th) for th, v in per.items())[1]
     med, cnt, tot = per[best]
-    del peers, out, tmp
+    check = None
+    if head_out is not None:
+        same = torch.equal(out.view(torch.int32), head_out.view(torch.int32))
+        bad = 0 if same else int((out.view(torch.int32) != head_out.view(torch.int32)).sum())
+        check = {"parity_ok": bool(same), "elements": p, "mismatches": bad,
+                 "check": "the timed GPU headline's output (every element, D2H after the timed region) == the "
+                          "reference op sequence (oracle port, fedavg.py:20-25) on the same %d peers, bit for bit" % n}
+        log("cpu baseline: headline vs oracle port on the same peers: %s" % ("bit-exact" if same else
+                                                                           "%d mismatches" % bad))
+    del peers, out, tmp, head_out
     log("cpu baseline: literal op sequence in a fresh process")
     cold = cpu_baseline_cold(n, p, share, min(4.0, budget_s))
     return {
@@ -563,6 +582,9 @@ def cpu_baseline(n, p, budget_s):
                    "rate. cold_fresh_process is the literal sequence, page faults included" % (p * 4 >> 20)),
         "cold_fresh_process": cold,
         "cpu": _cpu_model(),
+        "headline_oracle_parity": check,
+        "sample_inputs": "the headline's own peers (copied from HBM)" if check is not None else
+                         "seeded CPU peers (torch.Generator 1000)",
     }
 
 
@@ -1440,11 +1462,11 @@ def cpu_per_config():
     return res
 
 
-def cpu_baseline_all(args, result, n, p):
+def cpu_baseline_all(args, result, n, p, headline=None):
     """The cpu_baseline object: the reference op sequence on the host cores (the only leg that runs
     the oracle port), plus every other CPU comparison, each ratio filled into the GPU row it
-    belongs to."""
-    cb = cpu_baseline(n, p, args.cpu_seconds)
+    belongs to.  ``headline``: see cpu_baseline."""
+    cb = cpu_baseline(n, p, args.cpu_seconds, headline)
     if not args.no_small:
         cb["per_config"] = cpu_per_config()
         for name, row in cb["per_config"].items():
@@ -1961,6 +1983,14 @@ def main():
         parity["headline (all-gathered buckets vs one-GPU reduce of the whole model)"] = row.get("parity_ok")
         result["headline_parity"] = row
     head_out = inp.out[:p].clone()
+    headline_host = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.dtype == "f32" and cfg is None:
+        # the headline's peers and output on the host, for the oracle check in the cpu_baseline leg
+        # (after the timed region; the peers are regenerated exactly as SlabInput made them)
+        pitch = max(128, (p + 127) // 128 * 128)
+        rows = make_slab(n, pitch, dt, device, 1000 + 97 * rank)
+        headline_host = ([rows[k, :p].cpu() for k in range(n)], head_out.cpu())
+        del rows
     del inp
     torch.cuda.empty_cache()
     if cfg is None and args.layout == "slab":
@@ -2036,8 +2066,14 @@ def main():
                 return dfl_round(msgs, p, device)
             result["dfl_round"] = legs.run("dfl_round", dfl)
         if not args.no_cpu_baseline and args.dtype == "f32":
-            result["cpu_baseline"] = legs.run("cpu_baseline", lambda L: cpu_baseline_all(args, result, n, p),
+            result["cpu_baseline"] = legs.run("cpu_baseline",
+                                              lambda L: cpu_baseline_all(args, result, n, p, headline_host),
                                               timeout_s=max(args.leg_timeout, 600))
+            headline_host = None
+            hp = result["cpu_baseline"].get("headline_oracle_parity")
+            if hp is not None:
+                parity["headline == reference op sequence (oracle port, every element)"] = hp.get("parity_ok")
+                result["headline_oracle_parity"] = hp
     parity = {k: v for k, v in parity.items() if v is not None}
     result["parity"] = parity
     result["parity_ok"] = all(parity.values()) if parity else None

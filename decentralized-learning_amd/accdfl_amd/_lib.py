@@ -24,6 +24,15 @@ HEADER = os.path.join(INCLUDE, "dlagg.h")
 # ACCDFL_AMD_TUNING=1 loads the tuning build (lib/libdlagg_tuning.so, -DDLA_TUNING=1: the same library
 # plus the A/B environment knobs the profiles/ scripts sweep); the product build reads no environment.
 TUNING = os.environ.get("ACCDFL_AMD_TUNING", "") == "1"
+
+
+def tuning_env(name: str, default: str) -> str:
+    """An A/B knob of the host side (the profiles/ scripts sweep them): read from the environment only
+    under ACCDFL_AMD_TUNING=1, as the C library reads its knobs only in the tuning build; the product
+    runs the measured policy and reads only the documented variables (ACCDFL_AMD_DEVICES,
+    ACCDFL_AMD_RESULT_MEMORY)."""
+    return os.environ.get(name, default) if TUNING else default
+
 LIB_PATH = os.environ.get("DLAGG_LIB", os.path.join(PKG_ROOT, "lib",
                                                     "libdlagg_tuning.so" if TUNING else "libdlagg.so"))
 
@@ -331,8 +340,8 @@ class _Lib:
                                                 ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_double),
                                                 ctypes.c_int, ctypes.c_int, vp, vp, vp]
         so.dla_wsum_multi_table_acc.restype = ctypes.c_int
-        so.dla_slab_stage.argtypes = [ctypes.c_int, vp, ctypes.c_int64, ctypes.c_int64, ctypes.c_int, ctypes.c_int64,
-                                      vp, ctypes.c_int64, vp]
+        so.dla_slab_stage.argtypes = [ctypes.c_int, vp, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int,
+                                      ctypes.c_int64, vp, ctypes.c_int64, vp]
         so.dla_slab_stage.restype = ctypes.c_int
         so.dla_host_in_place_rounds.argtypes = []
         so.dla_host_in_place_rounds.restype = ctypes.c_int64
@@ -628,13 +637,13 @@ def wsum_slab_tiled_ptr(dtype_code: int, base_ptr: int, tile_elems: int, slab_ro
     L.check(rc, "dla_wsum_slab_tiled")
 
 
-def slab_stage(dtype_code: int, base_ptr: int, tile_elems: int, slab_rows: int, row: int, dst_elem: int, src_ptr: int,
-               n_elems: int, stream_ptr: int) -> None:
+def slab_stage(dtype_code: int, base_ptr: int, tile_elems: int, slab_rows: int, n_tiles: int, row: int, dst_elem: int,
+               src_ptr: int, n_elems: int, stream_ptr: int) -> None:
     """dla_slab_stage: n_elems elements at src_ptr (host or device) -> row `row` of a tile-interleaved
-    slab from flat element dst_elem on (one 2D copy for the whole tiles)."""
+    slab of n_tiles tiles from flat element dst_elem on (one 2D copy for the whole tiles)."""
     L = lib()
-    L.check(L.so.dla_slab_stage(dtype_code, base_ptr, tile_elems, slab_rows, row, dst_elem, src_ptr, n_elems,
-                                stream_ptr), "dla_slab_stage")
+    L.check(L.so.dla_slab_stage(dtype_code, base_ptr, tile_elems, slab_rows, n_tiles, row, dst_elem, src_ptr,
+                                n_elems, stream_ptr), "dla_slab_stage")
 
 
 def host_in_place_rounds() -> int:

@@ -760,7 +760,7 @@ _native_staging: Dict[Tuple[torch.device, torch.dtype, int], _NativeStaging] = {
 # Bytes of every peer's rows per chunk of dla_host_reduce (two chunks in flight): large enough that
 # one DMA per chunk runs at the PCIe rate, small enough that packing chunk c+1 overlaps the DMA of
 # chunk c from the start of the round.
-_NATIVE_CHUNK_BYTES = int(float(os.environ.get("ACCDFL_AMD_HOST_CHUNK_MB", "32")) * (1 << 20))
+_NATIVE_CHUNK_BYTES = int(float(_lib.tuning_env("ACCDFL_AMD_HOST_CHUNK_MB", "32")) * (1 << 20))
 
 
 _NATIVE_MIN_CHUNK_BYTES = 2 << 20
@@ -816,7 +816,7 @@ def _bucket_native(st: _NativeStaging, dev, flats: List[List[torch.Tensor]], num
 # * "packed": one thread packing every peer into pinned staging peer-major and issuing the DMAs.
 # Peers that are not contiguous CPU tensors take "pipelined".
 _HOST_PATHS = ("native", "pipelined", "packed")
-_HOST_PATH = os.environ.get("ACCDFL_AMD_HOST_PATH", "native")
+_HOST_PATH = _lib.tuning_env("ACCDFL_AMD_HOST_PATH", "native")
 if _HOST_PATH not in _HOST_PATHS:
     raise ValueError("ACCDFL_AMD_HOST_PATH must be one of %s" % (_HOST_PATHS,))
 

@@ -30,13 +30,15 @@ from typing import Dict, List
 import numpy as np
 import torch
 
+from accdfl_amd._lib import tuning_env as _tuning_env
+
 MODES = ("pooled", "pinned", "pageable")
 _mode = os.environ.get("ACCDFL_AMD_RESULT_MEMORY", "pooled")
 if _mode not in MODES:
     raise ValueError("ACCDFL_AMD_RESULT_MEMORY must be one of %s" % (MODES,))
 
 POOL_MIN_BYTES = 1 << 20          # smaller tensors are plain torch.empty
-POOL_FREE_BYTES = int(os.environ.get("ACCDFL_AMD_POOL_FREE_BYTES", str(2 << 30)))
+POOL_FREE_BYTES = int(_tuning_env("ACCDFL_AMD_POOL_FREE_BYTES", str(2 << 30)))
 
 
 def set_result_memory(mode: str) -> None:

@@ -126,7 +126,7 @@ class PeerSlab:
                 else:
                     for k in range(self.n):
                         flat = self._tiles_of(old, k).reshape(-1)[: self.total].contiguous()
-                        _lib.slab_stage(self.code, new.data_ptr(), self.tile, cap, k, 0, flat.data_ptr(),
+                        _lib.slab_stage(self.code, new.data_ptr(), self.tile, cap, new.shape[0], k, 0, flat.data_ptr(),
                                         self.total, int(self.copy_stream.cuda_stream))
                         flat.record_stream(self.copy_stream)
         old.record_stream(self.copy_stream)
@@ -181,8 +181,8 @@ class PeerSlab:
                 self._put_pageable(row, off, src, n)
                 return
             self._held.append(src)
-        _lib.slab_stage(self.code, self.buf.data_ptr(), self.tile, self.capacity, row, off, src.data_ptr(), n,
-                        int(self.copy_stream.cuda_stream))
+        _lib.slab_stage(self.code, self.buf.data_ptr(), self.tile, self.capacity, self.buf.shape[0], row, off,
+                        src.data_ptr(), n, int(self.copy_stream.cuda_stream))
 
     def _put_pageable(self, row: int, off: int, src: torch.Tensor, n: int):
         chunk = max(1, self.PAGEABLE_CHUNK_BYTES // self.buf.element_size())
@@ -194,8 +194,8 @@ class PeerSlab:
                 m = min(chunk, n - s0)
                 buf = self._dev_chunks[i & 1][:m]
                 buf.copy_(flat[s0:s0 + m], non_blocking=True)  # pageable: consumed before this returns
-                _lib.slab_stage(self.code, self.buf.data_ptr(), self.tile, self.capacity, row, off + s0, buf.data_ptr(),
-                                m, int(self.copy_stream.cuda_stream))
+                _lib.slab_stage(self.code, self.buf.data_ptr(), self.tile, self.capacity, self.buf.shape[0], row,
+                                off + s0, buf.data_ptr(), m, int(self.copy_stream.cuda_stream))
 
     def _release_inflight(self):
         """Drop the page-locked sources whose copies the copy stream has passed."""

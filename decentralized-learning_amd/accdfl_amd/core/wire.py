@@ -33,6 +33,8 @@ import numpy as np
 import torch
 from torch import nn
 
+from accdfl_amd._lib import tuning_env as _tuning_env
+
 
 class UnsafePayloadError(pickle.UnpicklingError):
     """The payload references something a state_dict pickle never contains."""
@@ -153,7 +155,7 @@ def _block_table(blocks: list) -> Tuple[np.ndarray, np.ndarray]:
 
 # Gathers into a page-locked ingress buffer (read next by the H2D DMA, not by the CPU) use streaming
 # stores (dla_host_copy_batch_ex, DLA_COPY_STREAMING); ACCDFL_AMD_INGRESS_NT=0 turns them off (A/B).
-_INGRESS_NT = os.environ.get("ACCDFL_AMD_INGRESS_NT", "1") != "0"
+_INGRESS_NT = _tuning_env("ACCDFL_AMD_INGRESS_NT", "1") != "0"
 
 
 # When a list, _gather appends each gather's wall time in ms (bench.py dfl_round's phase split).
@@ -693,8 +695,8 @@ def _join_pieces(pieces) -> bytes:
 
 # Bounce chunk of _copy_from_device (its copy-out runs on up to 8 threads from 16 MiB: a chunk of
 # 8 MiB gets only 4) and the store kind of the copy-out (A/B knobs).
-_EGRESS_CHUNK = int(float(os.environ.get("ACCDFL_AMD_EGRESS_CHUNK_MB", "32")) * (1 << 20))
-_EGRESS_NT = os.environ.get("ACCDFL_AMD_EGRESS_NT", "0") == "1"
+_EGRESS_CHUNK = int(float(_tuning_env("ACCDFL_AMD_EGRESS_CHUNK_MB", "32")) * (1 << 20))
+_EGRESS_NT = _tuning_env("ACCDFL_AMD_EGRESS_NT", "0") == "1"
 _egress_bounce = {}
 _egress_lock = threading.Lock()
 

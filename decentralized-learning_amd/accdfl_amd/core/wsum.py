@@ -168,7 +168,7 @@ def wsum_multi(peer_params: Sequence[Sequence[torch.Tensor]], weights: Sequence[
 # 128 x ResNet-34 bf16 865 / 1851 (813); 64 x ResNet-8 f32 219 / 310 (192); 64 x GNLeNet 14 / 48
 # (4.3); 16 x ResNet-34 bf16 (724 MB) 134 / 165 (106); but 32 x FEMNIST (223 MB) 41.3 / 35.2 (32.1)
 # and 8 x GNLeNet 13.0 / 6.3 (3.3), where the table's copy costs more than it saves.
-MULTI_TABLE_MIN_PEERS = int(os.environ.get("ACCDFL_AMD_MULTI_TABLE_MIN_PEERS", "33"))
+MULTI_TABLE_MIN_PEERS = int(_lib.tuning_env("ACCDFL_AMD_MULTI_TABLE_MIN_PEERS", "33"))
 MULTI_TABLE_MIN_BYTES = 256 << 20
 
 

@@ -3278,13 +3278,20 @@ int dla_wsum_slab_tiled(int dtype, const void* base, int64_t tile_elems, int64_t
   return DLA_OK;
 }
 
-int dla_slab_stage(int dtype, void* base, int64_t tile_elems, int64_t slab_rows, int row, int64_t dst_elem,
-                   const void* src, int64_t n_elems, void* stream) {
+int dla_slab_stage(int dtype, void* base, int64_t tile_elems, int64_t slab_rows, int64_t n_tiles, int row,
+                   int64_t dst_elem, const void* src, int64_t n_elems, void* stream) {
   g_last_error.clear();
   const int es = elem_size(dtype);
   if (es == 0) return fail(DLA_E_INVALID, "dla_slab_stage: unknown dtype");
   if (!base || tile_elems < 1 || slab_rows < 1 || row < 0 || row >= slab_rows || dst_elem < 0 || n_elems < 0)
     return fail(DLA_E_INVALID, "dla_slab_stage: need base, tile_elems >= 1 and 0 <= row < slab_rows");
+  // the range must lie inside the slab's row: a bad argument fails here instead of letting the copy
+  // engine write past the end of the HBM buffer
+  if (n_tiles < 0 || n_tiles > (INT64_MAX / tile_elems) || dst_elem > n_tiles * tile_elems ||
+      n_elems > n_tiles * tile_elems - dst_elem)
+    return fail(DLA_E_INVALID, "dla_slab_stage: elements [" + std::to_string(dst_elem) + ", " +
+                                   std::to_string(dst_elem + n_elems) + ") do not fit the row's " +
+                                   std::to_string(n_tiles) + " tiles of " + std::to_string(tile_elems));
   if (n_elems == 0) return DLA_OK;
   if (!src) return fail(DLA_E_INVALID, "dla_slab_stage: null src");
   hipStream_t s = static_cast<hipStream_t>(stream);

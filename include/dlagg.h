@@ -32,6 +32,15 @@
  * dla_last_error() returns a thread-local message.  No C++ exception crosses the ABI.
  * Threading: reentrant; work is enqueued on `stream` (a hipStream_t, NULL = the
  * default stream) and the call does not synchronise.
+ *
+ * Surface.  The drop-in for the reference path is: dla_wsum, dla_wsum_multi(_table[_acc]),
+ * dla_wsum_mixed, dla_wsum_slab(_tiled) + dla_slab_stage, dla_wsum_sharded, dla_host_round_start /
+ * _finish, dla_host_reduce / dla_host_reduce_launch / _join, dla_plan_*, dla_mean and the helpers
+ * (version, build id, last error, shard range, tile size, copy batch, shutdown).  INTERNAL entry
+ * points — exported for the library's own tests, benchmarks and diagnostics, not part of the
+ * drop-in and free to change: dla_wsum_ex (forced launch knobs), dla_select_kernel,
+ * dla_host_in_place_rounds, dla_host_reduce_deferred (dla_host_reduce_launch's body on the
+ * caller's thread).
  */
 #ifndef DLAGG_H
 #define DLAGG_H
@@ -104,7 +113,7 @@ const char* dla_last_error(void);
 int dla_wsum(int dtype, const void* const* peers, const double* weights, int n_peers,
              int64_t n_elems, void* out, void* stream);
 
-/* dla_wsum with explicit launch knobs (benchmarks / tuning). */
+/* INTERNAL: dla_wsum with explicit launch knobs (benchmarks / tuning). */
 int dla_wsum_ex(int dtype, const void* const* peers, const double* weights, int n_peers,
                 int64_t n_elems, void* out, void* stream, const dla_launch_cfg_t* cfg);
 
@@ -139,9 +148,11 @@ int64_t dla_slab_tile_elems(int dtype, int slab_rows, int64_t n_elems);
  * engine writes each tile in place) plus up to two plain copies for the partial tiles at either end,
  * enqueued on `stream`.  No contiguous device row and no scatter pass.  The usual async-copy rules
  * hold: page-locked sources must stay untouched until the stream passes the copy; pageable sources
- * are consumed before the call returns.  ABI v10. */
-int dla_slab_stage(int dtype, void* base, int64_t tile_elems, int64_t slab_rows, int row, int64_t dst_elem,
-                   const void* src, int64_t n_elems, void* stream);
+ * are consumed before the call returns.  n_tiles: the slab's tile count (its leading dimension); a
+ * range [dst_elem, dst_elem + n_elems) beyond n_tiles * tile_elems is refused with DLA_E_INVALID
+ * before any copy (ABI v13).  ABI v10. */
+int dla_slab_stage(int dtype, void* base, int64_t tile_elems, int64_t slab_rows, int64_t n_tiles, int row,
+                   int64_t dst_elem, const void* src, int64_t n_elems, void* stream);
 
 /* Replaces the per-parameter inner loop of fedavg.py:24-25 for T parameter
  * tensors at once (one model = T tensors, parameters() order).
@@ -207,7 +218,7 @@ int dla_mean(int dtype, const void* const* peers, int n_peers, int64_t n_elems, 
 /* Largest peer count one kernel pass takes (kernel-argument pointer table). */
 int dla_max_peers_per_pass(void);
 
-/* Name of the kernel family dla_wsum picks (default launch, 16-byte aligned buffers) for
+/* INTERNAL (benchmarks, profilers).  Name of the kernel family dla_wsum picks (default launch, 16-byte aligned buffers) for
  * this dtype, peer count and size: "wsum_bigtile_kernel", "wsum_vec_kernel", "wsum_wide_kernel"
  * or "wsum_stream_kernel" (static string; "" for invalid arguments).  For profilers and
  * benchmarks that must name the dominant kernel.  ABI v4. */
@@ -324,11 +335,11 @@ int dla_host_reduce(int dtype, int n_peers, int n_tensors, const void* const* te
                     const double* weights, void* const* outs, int64_t begin, int64_t end, int64_t chunk_elems,
                     void* h_stage, void* d_stage, void* h_out, void* d_out, void* stream, void* copy_stream);
 
-/* Host rounds (dla_host_reduce / _deferred / _launch calls and dla_host_round_start) whose peers the
+/* INTERNAL (diagnostics).  Host rounds (dla_host_reduce / _deferred / _launch calls and dla_host_round_start) whose peers the
  * kernel read in place from page-locked rows, since the library was loaded (diagnostics).  ABI v11. */
 int64_t dla_host_in_place_rounds(void);
 
-/* dla_host_reduce with the outputs published late: outs[] is read only once *outs_ready (written by
+/* INTERNAL (tests; the product calls dla_host_reduce_launch).  dla_host_reduce with the outputs published late: outs[] is read only once *outs_ready (written by
  * the caller, read with acquire semantics) turns non-zero — > 0: outs[] is filled; < 0: the caller
  * gives up, and the call drains its copies and returns DLA_E_INVALID.  The caller starts the call on
  * one thread, allocates the result tensors on another while the first chunks are packed, copied in

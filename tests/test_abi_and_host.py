@@ -119,13 +119,18 @@ def test_library_version_and_argument_errors(lib_path):
     with pytest.raises(_lib.DlaggError, match="aliases peer 5"):
         _lib.wsum_multi_table_ptrs(0, ptrs, [ptrs[5]], [64], [1.0] * 130, 0, 0, 0)
     # dla_slab_stage: argument errors caught before any copy (row outside the slab, null base / src)
-    rc = L.so.dla_slab_stage(0, 4096, 1024, 8, 8, 0, 8192, 100, None)
+    rc = L.so.dla_slab_stage(0, 4096, 1024, 8, 4, 8, 0, 8192, 100, None)
     assert rc == -1 and b"row" in L.so.dla_last_error()
-    rc = L.so.dla_slab_stage(0, None, 1024, 8, 0, 0, 8192, 100, None)
+    rc = L.so.dla_slab_stage(0, None, 1024, 8, 4, 0, 0, 8192, 100, None)
     assert rc == -1
-    rc = L.so.dla_slab_stage(0, 4096, 1024, 8, 0, 0, None, 100, None)
+    rc = L.so.dla_slab_stage(0, 4096, 1024, 8, 4, 0, 0, None, 100, None)
     assert rc == -1 and b"src" in L.so.dla_last_error()
-    assert L.so.dla_slab_stage(0, 4096, 1024, 8, 0, 0, None, 0, None) == 0  # nothing to copy
+    assert L.so.dla_slab_stage(0, 4096, 1024, 8, 4, 0, 0, None, 0, None) == 0  # nothing to copy
+    # a range past the slab's 4 tiles of 1024 elements is refused before any copy
+    rc = L.so.dla_slab_stage(0, 4096, 1024, 8, 4, 0, 4000, 8192, 97, None)
+    assert rc == -1 and b"do not fit" in L.so.dla_last_error()
+    rc = L.so.dla_slab_stage(0, 4096, 1024, 8, 4, 0, 4097, 8192, 0, None)
+    assert rc == -1 and b"do not fit" in L.so.dla_last_error()
     # launch knobs outside the built set are refused before any launch
     for bad in (_lib.LaunchCfg(3, 0, 0, 0), _lib.LaunchCfg(4, 3, 0, 0), _lib.LaunchCfg(4, 1, 0, 128),
                 _lib.LaunchCfg(10, 0, 0, 0), _lib.LaunchCfg(11, 0, 0, 0)):  # 16-byte vec forms: not built
