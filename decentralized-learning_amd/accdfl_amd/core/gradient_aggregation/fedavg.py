@@ -187,12 +187,14 @@ def _flat_slices(tensors: List[torch.Tensor], numels: List[int], start: int, end
 
 # Small rounds go through dla_host_round_* (one native call packs every peer into page-locked rows
 # and enqueues the reduce, which reads them across PCIe; one call waits and unpacks) instead of the
-# chunked dla_host_reduce: below ~48 MB of input the one-shot round is as fast or faster (no per-chunk
-# round trips); above it the chunked round's pack / PCIe overlap wins.  Round 4, both paths reading
-# page-locked rows with the kernel, ms small / chunked (profiles/r04s2/small_large_ab.jsonl, pageable
-# peers): GNLeNet 8 peers 0.160 / 0.154, 64 peers (21.9 MB) 0.653 / 0.689; FEMNIST 2 peers 0.540 /
-# 0.555, 4 peers (27 MB) 0.880 / 0.933, 8 peers (54 MB) 1.884 / 1.493; ResNet-8 2 peers (39.5 MB)
-# 1.586 / 1.620, 4 peers (79 MB) 2.913 / 2.362.  Round 2 (staging DMAs then), us
+# chunked dla_host_reduce: below ~40 MB of input the one-shot round is faster (no per-chunk round
+# trips); from ~50 to ~80 MB the two TIE within run-to-run noise, and the 48 MiB bound sits in that
+# tie.  Round 4, both paths reading page-locked rows with the kernel, ms small / chunked, pageable
+# peers — the re-run (profiles/r04s3/small_large_ab.jsonl): GNLeNet 8 peers 0.158 / 0.165, 64 peers
+# (21.9 MB) 0.580 / 0.680; FEMNIST 2 peers 0.506 / 0.582, 4 peers (27 MB) 0.874 / 1.001, 8 peers
+# (54 MB) 1.504 / 1.492 (tie); ResNet-8 2 peers (39.5 MB) 1.341 / 1.644, 4 peers (79 MB) 2.324 / 2.298
+# (tie).  The first run (profiles/r04s2) read FEMNIST 8 peers 1.884 / 1.493 and GNLeNet 8 peers
+# 0.160 / 0.154: single samples, not reproduced.  Round 2 (staging DMAs then), us
 # small / dla_host_reduce (profiles/r02zo_layout_paths.log): FEMNIST 2 peers 619 / 828, 4 peers
 # 943 / 1343, 8 peers (54 MB) 1644-1882 / 1759-1979, 32 peers (216 MB) 6152 / 4704; ResNet-8 2 peers
 # 1393-2496 / 2290-2780, 3 peers 1895 / 2587, 4 peers (79 MB) 2497 / 2966, 8 peers (158 MB)

@@ -173,18 +173,36 @@ MULTI_TABLE_MIN_BYTES = 256 << 20
 
 
 class _TableRing:
-    """Page-locked host + device buffers for dla_wsum_multi_table's table, a few slots per device
-    used round-robin; a slot is refilled only after the stream that last read it has passed that
-    call (its event), so back-to-back rounds never overwrite a table still being copied or read."""
+    """Page-locked host + device buffers for dla_wsum_multi_table's table, SLOTS slots per device used
+    round-robin.  A slot is refilled only after the stream that last read it has passed that call, so
+    back-to-back rounds never overwrite a table still being copied or read.  The guard is one event per
+    FENCE_EVERY calls (recorded after the last of them, on their stream), not one per call: an event
+    recorded between two kernels of a stream costs ~3 us of GPU time (profiles/r05e: 124.8 -> 127.7 us
+    per back-to-back headline reduce); a slot is reused SLOTS calls after its last use, by when the
+    event after it has been recorded (or is recorded then)."""
 
-    SLOTS = 4
+    SLOTS = 8
+    FENCE_EVERY = 4
 
     def __init__(self, device: torch.device):
         self.device = device
-        self.slots = [None] * self.SLOTS  # (host uint8, device uint8, event or None)
+        self.slots = [None] * self.SLOTS  # (host uint8, device uint8)
+        self.fence = [None] * self.SLOTS  # event recorded after the slot's last use, or None
         self.busy = [False] * self.SLOTS  # taken and not yet done (another thread's call in flight)
+        self.pending = []                 # (slot, stream) used since the last fence
         self.i = 0
         self.lock = threading.Lock()
+
+    def _fence_locked(self):
+        """Record the event covering every pending slot (one per stream they ran on)."""
+        evs = {}
+        for idx, st in self.pending:
+            ev = evs.get(st.cuda_stream)
+            if ev is None:
+                ev = evs[st.cuda_stream] = torch.cuda.Event()
+                ev.record(st)
+            self.fence[idx] = ev
+        self.pending = []
 
     def take(self, nbytes: int):
         """(slot index, host buffer, device buffer); the caller passes the index to done()."""
@@ -197,24 +215,27 @@ class _TableRing:
                 raise RuntimeError("wsum_multi_table: more than %d concurrent calls on %s" % (self.SLOTS, self.device))
             idx = self.i
             self.busy[idx] = True
-            slot = self.slots[idx]
-        if slot is not None and slot[2] is not None:
-            slot[2].synchronize()
+            if any(k == idx for k, _ in self.pending):
+                self._fence_locked()
+            ev, slot = self.fence[idx], self.slots[idx]
+        if ev is not None:
+            ev.synchronize()
         if slot is None or slot[0].numel() < nbytes:
             size = max(nbytes, 64 << 10)
             size = 1 << (size - 1).bit_length()
             slot = (torch.empty(size, dtype=torch.uint8, pin_memory=True),
-                    torch.empty(size, dtype=torch.uint8, device=self.device), None)
+                    torch.empty(size, dtype=torch.uint8, device=self.device))
             self.slots[idx] = slot
         return idx, slot[0], slot[1]
 
     def done(self, idx: int, stream: torch.cuda.Stream):
-        h, d, _ = self.slots[idx]
-        ev = torch.cuda.Event()
-        ev.record(stream)
         with self.lock:
-            self.slots[idx] = (h, d, ev)
             self.busy[idx] = False
+            if self.pending and self.pending[-1][1].cuda_stream != stream.cuda_stream:
+                self._fence_locked()
+            self.pending.append((idx, stream))
+            if len(self.pending) >= self.FENCE_EVERY:
+                self._fence_locked()
 
 
 _rings = {}

@@ -887,7 +887,8 @@ __global__ __launch_bounds__(64) void wsum_vec_kernel(
 // dla_wsum_multi_table: every 16-byte aligned parameter tensor of a round (fedavg.py:24 walks them
 // one by one) over a pass of up to 128 peers in ONE launch.  The (tensor x peer) pointer table does
 // not fit the kernel-argument block (128 google_speech ResNet-34 models: 14 080 pointers), so it
-// travels to the device as one table per call (one H2D copy on the stream).  Workgroup b finds its
+// travels to the device as one table per call (upload_table: a copy kernel, or a side-stream copy
+// that overlaps the kernel before it).  Workgroup b finds its
 // tensor from the tensors' first workgroups (uniform: scalar loads), then folds 64 vectors of it
 // exactly as wsum_vec_kernel does (8 bytes per lane, G peers' loads in flight, list order); a tensor
 // with a ragged tail has one more workgroup, which runs fold_tail.  A launch covers up to 256 tensors.
@@ -1840,6 +1841,10 @@ hipError_t launch_multi_vec_pass(const MultiIndex* idx, const MultiSeg* segs, in
   return launch_multi_vec<DT, 8, 8, ACC_IN>(idx, segs, n_seg, grid, k0, pm, weights, plain, s);
 }
 
+// The table's host -> device copy (defined with the library's stream / event state below); `moved` is
+// the call's algorithmic bytes (its kernels' duration scale).
+hipError_t upload_table(char* td, const char* th, size_t bytes, int64_t moved, hipStream_t s);
+
 template <int DT>
 hipError_t run_multi_table(const std::vector<int>& packed, const void* const* peer_ptrs, void* const* outs,
                            const int64_t* numels, const double* weights, int n, char* th, char* td, hipStream_t s,
@@ -1878,7 +1883,8 @@ hipError_t run_multi_table(const std::vector<int>& packed, const void* const* pe
     launches.push_back({off, mc, wg});
     off += multi_chunk_bytes(mc);
   }
-  hipError_t e = hipMemcpyAsync(td, th, static_cast<size_t>(multi_table_bytes(m, n)), hipMemcpyHostToDevice, s);
+  const int64_t moved = (static_cast<int64_t>(n) + 1) * out_bytes;
+  hipError_t e = upload_table(td, th, static_cast<size_t>(multi_table_bytes(m, n)), moved, s);
   if (e != hipSuccess) return e;
   for (int k0 = 0; k0 < n; k0 += kMaxPeersPerPass) {
     const int pm = n - k0 < kMaxPeersPerPass ? n - k0 : kMaxPeersPerPass;
@@ -2140,6 +2146,85 @@ hipError_t take_event(int dev, hipEvent_t* ev) {  // caller holds g_shard_mu; de
     }
   }
   return hipEventCreateWithFlags(ev, hipEventDisableTiming);
+}
+
+// The multi-tensor table's upload.  A copy-engine job between two kernels of the reduce's stream costs
+// ~24 us of idle GPU per call (kernel end -> DMA start 9 us, the 19.6 KB DMA 6 us, DMA end -> next kernel
+// 8 us: profiles/r05c, 16 google_speech ResNet-34 models, back to back), against ~6 us between two
+// kernels.  Policy (profiles/r05d, modes A/B'd under DLA_TABLE_COPY in the tuning build):
+//  * the stream still has work queued and the call moves >= 256 MiB (its kernel runs >= ~40 us: rounds
+//    back to back): the copy runs on a library side stream of the device WHILE the queued kernel runs,
+//    and the calling thread waits for it (~15-20 us) before enqueuing the reduce — nothing sits between
+//    the kernels (mode 3; a barrier packet waiting on the copy's event, mode 2, still costs ~11 us);
+//  * otherwise (an idle GPU, or short kernels the host wait would outlast): a copy kernel on the stream
+//    reads the page-locked table across PCIe (mode 1: 3-4 us, no copy-engine hand-off);
+//  * a table that is not device-mapped page-locked memory: hipMemcpyAsync on the stream (mode 0).
+// 16 x ResNet-34 bf16 back to back 134.5 -> 117.7 us, one call on an idle GPU 146.5 -> 139 us;
+// 64 x ResNet-8 225 -> 210 us; 128 x ResNet-34 bf16 894 -> 877 us; the small rounds unchanged.
+__global__ __launch_bounds__(256) void table_copy_kernel(const uint4* __restrict__ src, uint4* __restrict__ dst,
+                                                         int64_t n16) {
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; i < n16;
+       i += static_cast<int64_t>(gridDim.x) * 256)
+    dst[i] = src[i];
+}
+
+constexpr int64_t kTableSideCopyMinBytes = int64_t{256} << 20;
+std::map<int, hipStream_t> g_table_streams;  // device -> side stream of the table uploads (dla_shutdown frees)
+
+int table_copy_mode() {  // -1 = the policy; the tuning build's DLA_TABLE_COPY forces 0..3 (5: diagnostic)
+  static const int mode = [] {
+    const char* v = tuning_env("DLA_TABLE_COPY");
+    return v ? std::atoi(v) : -1;
+  }();
+  return mode;
+}
+
+hipError_t upload_table(char* td, const char* th, size_t bytes, int64_t moved, hipStream_t s) {
+  const bool mapped = (bytes & 15u) == 0 && is_mapped_host_ptr(th);
+  int mode = table_copy_mode();
+  if (mode < 0) {
+    mode = mapped ? 1 : 0;
+    if (moved >= kTableSideCopyMinBytes) {
+      const hipError_t q = hipStreamQuery(s);
+      if (q != hipSuccess && q != hipErrorNotReady) return q;
+      if (q == hipErrorNotReady) mode = 3;
+    }
+  }
+  if (mode == 5) {  // DIAGNOSTIC (tuning build only): upload a device slot once, then trust it holds the
+    // same table — valid only for a caller that repeats one identical call (profiles/r05_table_probe.py),
+    // to time the kernels back to back with nothing between them
+    static std::set<char*> seen;
+    std::lock_guard<std::mutex> lock(g_shard_mu);
+    if (!seen.insert(td).second) return hipSuccess;
+    return hipMemcpyAsync(td, th, bytes, hipMemcpyHostToDevice, s);
+  }
+  if (mode == 1 && mapped) {
+    const int64_t n16 = static_cast<int64_t>(bytes / 16);
+    int64_t grid = (n16 + 255) / 256;
+    if (grid > 256) grid = 256;
+    hipLaunchKernelGGL(table_copy_kernel, dim3(static_cast<unsigned>(grid)), dim3(256), 0, s,
+                       reinterpret_cast<const uint4*>(th), reinterpret_cast<uint4*>(td), n16);
+    return hipGetLastError();
+  }
+  if (mode == 2 || mode == 3) {
+    int dev = -1;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    std::unique_lock<std::mutex> lock(g_shard_mu);
+    hipStream_t& side = g_table_streams[dev];
+    if (!side && (e = hipStreamCreateWithFlags(&side, hipStreamNonBlocking)) != hipSuccess) return e;
+    hipEvent_t ev;
+    if ((e = take_event(dev, &ev)) != hipSuccess) return e;
+    const hipStream_t side_s = side;
+    lock.unlock();
+    e = hipMemcpyAsync(td, th, bytes, hipMemcpyHostToDevice, side_s);
+    if (e == hipSuccess) e = hipEventRecord(ev, side_s);
+    if (e == hipSuccess) e = mode == 2 ? hipStreamWaitEvent(s, ev, 0) : hipEventSynchronize(ev);
+    lock.lock();
+    g_event_pool.push_back({dev, ev});  // reusable once recorded: a stream wait holds its own reference
+    return e;
+  }
+  return hipMemcpyAsync(td, th, bytes, hipMemcpyHostToDevice, s);
 }
 
 int wsum_sharded_impl(int dtype, int n_shards, const int* dev_ids, const void* const* peers, const double* weights,
@@ -3236,6 +3321,10 @@ int dla_shutdown(void) {
     if (hipSetDevice(de.first) == hipSuccess) (void)hipEventDestroy(de.second);
   }
   g_event_pool.clear();
+  for (auto& ds : g_table_streams) {
+    if (hipSetDevice(ds.first) == hipSuccess) (void)hipStreamDestroy(ds.second);
+  }
+  g_table_streams.clear();
   for (const auto& pr : g_peer_enabled) {
     if (hipSetDevice(pr.first) == hipSuccess) (void)hipDeviceDisablePeerAccess(pr.second);
   }

@@ -168,8 +168,11 @@ int dla_wsum_multi(int dtype, int n_tensors, const void* const* peer_ptrs, void*
  * HBM, accdfl/core/gradient_aggregation/fedavg.py:24 walking every parameter of every model; the
  * simulator's large-N average, simulations/gl/gl_simulation.py:96-105).  The (tensor x peer)
  * pointer table and one record per tensor travel to the device as ONE table — written into the
- * caller's page-locked `table_host`, copied by one hipMemcpyAsync on `stream` into `table_dev`
- * (both at least dla_wsum_multi_table_bytes(n_tensors, n_peers) bytes, 16-byte aligned) — and
+ * caller's page-locked `table_host` and copied into `table_dev` (both at least
+ * dla_wsum_multi_table_bytes(n_tensors, n_peers) bytes, 16-byte aligned): by a copy kernel on `stream`
+ * reading table_host across PCIe, or — when `stream` still has work queued and the call moves
+ * >= 256 MiB — by a copy on a library side stream that overlaps that work, the call returning once the
+ * copy is done (v13; before: one hipMemcpyAsync on `stream`, ~24 us of idle GPU per call) — and
  * every 16-byte aligned F32 / BF16 / F16 tensor is folded by ONE launch per pass of up to
  * DLA_MAX_PEERS_PER_PASS peers, whatever the peer and tensor counts (128 google_speech ResNet-34
  * models: 14 080 tensors, 1 launch; dla_wsum_multi: 110).  Other tensors (unaligned, F64) take the

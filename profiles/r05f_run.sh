@@ -15,7 +15,7 @@ run() {
   case $rc in 124|137|134|139) exit $rc;; esac
   return 0
 }
-run 400 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -v -k "multi_table or device_modules or mixed" --timeout 200 --timeout-method thread > $out/table_tests.log 2>&1
+run 500 python -u -m pytest tests/test_gpu_parity.py tests/test_center_copy_layouts.py -m gpu -x -v -k "multi_table or device_modules or mixed or record_stream or reference_trees" --timeout 200 --timeout-method thread > $out/table_tests.log 2>&1
 run 300 python -u profiles/r05_table_probe.py > $out/probe.jsonl 2> $out/probe.err
 run 300 python -u profiles/r05_table_probe.py >> $out/probe.jsonl 2>> $out/probe.err
 run 300 python -u bench.py --device-configs-only > $out/device_configs.log 2>&1

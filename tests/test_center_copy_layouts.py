@@ -1,0 +1,273 @@
+"""The result module against ``copy.deepcopy(models[0])`` (fedavg.py:20) on reference-shaped module trees.
+
+_center_copy builds the deepcopy natively (csrc/walk.cpp: the tree clone, the parameters as parts of
+one allocation with a storage each, the buffers by one gather per dtype).  These differential tests run
+it on module trees with the reference models' exact parameter / buffer layouts (tests/golden/layouts.json,
+recorded from the reference's own create_model: google_speech ResNet-34 — 110 parameters, 108 BN
+buffers —, CIFAR-10 ResNet-8, the FEMNIST CNN), on the Shakespeare model's shape (an nn.LSTM, which
+has its own __setstate__ and _flat_weights; accdfl/core/models/shakespeare.py:14-33) and on a module
+carrying every kind of hook, and compare attribute for attribute with copy.deepcopy, plus the length of
+``pickle.dumps(state_dict())`` — the reference's serialize_model (accdfl/core/models/__init__.py:9-10)
+of the result.  CPU: _center_copy itself; -m gpu: the whole FedAvg.aggregate on CPU and device modules,
+values against the oracle port."""
+import copy
+import json
+import os
+import pickle
+import weakref
+from collections import OrderedDict
+
+import numpy as np
+import pytest
+import torch
+from torch import nn
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LAYOUTS = json.load(open(os.path.join(ROOT, "tests", "golden", "layouts.json")))
+
+
+class _RefModel(nn.Module):
+    """The attributes accdfl's Model base class adds (accdfl/core/models/Model.py:15-24)."""
+
+    def __init__(self):
+        super().__init__()
+        self.model_change = None
+        self._param_count_ot = None
+        self._param_count_total = None
+        self.accumulated_changes = None
+        self.shared_parameters_counter = None
+
+
+class _Block(nn.Module):
+    pass
+
+
+def _leaf(params: dict, buffers: dict) -> nn.Module:
+    """An nn layer with exactly these parameter / buffer shapes (conv, linear, batch norm)."""
+    w = params["weight"]
+    if "running_mean" in buffers:
+        return nn.BatchNorm2d(w[0])
+    if len(w) == 4:
+        return nn.Conv2d(w[1], w[0], tuple(w[2:]), bias="bias" in params)
+    if len(w) == 2:
+        return nn.Linear(w[1], w[0], bias="bias" in params)
+    raise ValueError(params)
+
+
+def tree_from_layout(name: str) -> nn.Module:
+    """A module tree whose named_parameters() / named_buffers() are the reference model's."""
+    lay = LAYOUTS[name]
+    leaves = OrderedDict()
+    for key, shape, _ in lay["params"]:
+        path, attr = key.rsplit(".", 1)
+        leaves.setdefault(path, ({}, {}))[0][attr] = shape
+    for key, shape, _ in lay["buffers"]:
+        path, attr = key.rsplit(".", 1)
+        leaves.setdefault(path, ({}, {}))[1][attr] = shape
+    # the containers: numbered children make an nn.Sequential (the reference's layerN / shortcut)
+    children = OrderedDict()
+    for path in leaves:
+        parts = path.split(".")
+        for i in range(len(parts)):
+            children.setdefault(".".join(parts[:i]), [])
+            child = ".".join(parts[: i + 1])
+            if child not in children[".".join(parts[:i])]:
+                children[".".join(parts[:i])].append(child)
+
+    def build(path):
+        if path in leaves:
+            return _leaf(*leaves[path])
+        kids = children[path]
+        names = [k.rsplit(".", 1)[-1] for k in kids]
+        if all(n.isdigit() for n in names):
+            return nn.Sequential(*[build(k) for k in kids])
+        m = _RefModel() if path == "" else _Block()
+        for k, n in zip(kids, names):
+            m.add_module(n, build(k))
+        return m
+
+    m = build("")
+    got = [[n, list(p.shape)] for n, p in m.named_parameters()]
+    assert got == [[n, s] for n, s, _ in lay["params"]], "layout of %s not reproduced" % name
+    assert [n for n, _ in m.named_buffers()] == [n for n, _, _ in lay["buffers"]]
+    return m
+
+
+class _Shakespeare(_RefModel):
+    """The Shakespeare next-character model's shape (accdfl/core/models/shakespeare.py:14-33)."""
+
+    def __init__(self, vocab=80):
+        super().__init__()
+        self.embedding = nn.Embedding(vocab, 8)
+        self.lstm = nn.LSTM(8, 256, batch_first=True, num_layers=2)
+        self.l1 = nn.Linear(256 * 80, vocab)
+
+
+class _Hooked(_RefModel):
+    """Every hook kind a module can carry (forward, forward pre, backward, state-dict, load hooks) and
+    a hook on a child."""
+
+    def __init__(self):
+        super().__init__()
+        self.a = nn.Linear(6, 5)
+        self.b = nn.Sequential(nn.Linear(5, 4), nn.BatchNorm1d(4))
+        self.register_forward_hook(_fwd_hook)
+        self.register_forward_pre_hook(_pre_hook)
+        self.register_full_backward_hook(_bwd_hook)
+        self._register_state_dict_hook(_sd_hook)
+        self.register_load_state_dict_post_hook(_load_post_hook)
+        self.b[0].register_forward_hook(_fwd_hook)
+
+    def forward(self, x):
+        return self.b(self.a(x))
+
+
+def _fwd_hook(m, i, o):
+    return o
+
+
+def _pre_hook(m, i):
+    return None
+
+
+def _bwd_hook(m, gi, go):
+    return None
+
+
+def _sd_hook(m, sd, prefix, local_metadata):
+    return sd
+
+
+def _load_post_hook(m, keys):
+    return None
+
+
+def _models(kind):
+    torch.manual_seed(7)
+    if kind in LAYOUTS:
+        m = tree_from_layout(kind)
+    elif kind == "shakespeare_lstm":
+        m = _Shakespeare()
+    else:
+        m = _Hooked()
+    for b in m.buffers():  # non-default running statistics and step counters
+        b.copy_(torch.rand(b.shape) * 10) if b.dtype.is_floating_point else b.fill_(11)
+    return m
+
+
+KINDS = ["google_speech_resnet34", "cifar10_resnet8", "femnist_cnn", "shakespeare_lstm", "hooked"]
+
+
+def _same_tree(x, y, memo_x, memo_y, path="model"):
+    """x (copy.deepcopy's) and y (ours) are the same object graph: same types, attribute / key
+    order, tensor metadata, buffer values, hooks, and the same identity structure."""
+    if id(x) in memo_x:
+        assert memo_y.get(id(y)) == memo_x[id(x)], "%s: identity structure differs" % path
+        return
+    memo_x[id(x)] = memo_y[id(y)] = len(memo_x)
+    assert type(x) is type(y), "%s: %s vs %s" % (path, type(x), type(y))
+    if isinstance(x, torch.Tensor):
+        assert x.shape == y.shape and x.dtype == y.dtype and x.stride() == y.stride(), path
+        assert x.requires_grad == y.requires_grad and x.device == y.device, path
+        if not isinstance(x, nn.Parameter):
+            assert torch.equal(x, y), path
+        return
+    if isinstance(x, nn.Module):
+        assert list(x.__dict__) == list(y.__dict__), path
+        for k in x.__dict__:
+            _same_tree(x.__dict__[k], y.__dict__[k], memo_x, memo_y, "%s.%s" % (path, k))
+        return
+    if isinstance(x, dict):
+        assert list(x) == list(y), path
+        for k in x:
+            _same_tree(x[k], y[k], memo_x, memo_y, "%s[%r]" % (path, k))
+        return
+    if isinstance(x, (list, tuple)):
+        assert len(x) == len(y), path
+        for i, (u, v) in enumerate(zip(x, y)):
+            _same_tree(u, v, memo_x, memo_y, "%s[%d]" % (path, i))
+        return
+    if isinstance(x, weakref.ref):  # nn.LSTM's _flat_weight_refs: to the copy's own parameters
+        _same_tree(x(), y(), memo_x, memo_y, path + "()")
+        return
+    if callable(x) and not isinstance(x, type):  # hooks: the same function objects (deepcopy keeps functions)
+        assert x is y, path
+        return
+    assert x == y, path
+
+
+def _sd_pickle_len(m) -> int:
+    return len(pickle.dumps(m.state_dict()))
+
+
+@pytest.mark.parametrize("native", [True, False], ids=["native_clone", "python_clone"])
+@pytest.mark.parametrize("kind", KINDS)
+def test_center_copy_of_reference_trees_is_a_deepcopy(kind, native, monkeypatch):
+    from accdfl_amd import _lib
+    from accdfl_amd.core.gradient_aggregation import fedavg as fa
+
+    if native and _lib.walk_module() is None:
+        pytest.skip("walk extension not built")
+    monkeypatch.setattr(fa, "_NATIVE_CLONE", native)
+    m = _models(kind)
+    for cls in {type(x) for x in m.modules()}:  # classified, as every aggregate does first
+        fa._plain_walk(cls)
+    want = copy.deepcopy(m)
+    for large in (False, True):  # fresh parameters / pooled pre-faulted memory for >= 1 MiB
+        got = fa._center_copy(m, large=large)
+        _same_tree(want, got, {}, {})
+        assert all(p is not q for p, q in zip(got.parameters(), m.parameters()))
+        assert [n for n, _ in got.named_parameters()] == [n for n, _ in m.named_parameters()]
+        for (n, b), c in zip(m.named_buffers(), got.buffers()):
+            assert torch.equal(b, c) and b.data_ptr() != c.data_ptr(), n
+        # the reference's serialize_model of the result pickles as many bytes as deepcopy's: every
+        # parameter has a storage of its own (walk.cpp alias_of), not a view of one shared allocation
+        with torch.no_grad():
+            for p, q in zip(got.parameters(), m.parameters()):
+                p.copy_(q)
+        assert _sd_pickle_len(got) == _sd_pickle_len(want)
+        sd = pickle.loads(pickle.dumps(got.state_dict()))  # our own bytes: safe to load
+        for k, v in m.state_dict().items():
+            assert torch.equal(sd[k], v), k
+    if kind == "shakespeare_lstm":  # the LSTM's flat weights point at the copy's own parameters
+        assert got.lstm._flat_weights[0] is got.lstm.weight_ih_l0
+        assert got.lstm._flat_weights[0] is not m.lstm.weight_ih_l0
+        out, _ = got.lstm(torch.zeros(1, 3, 8))
+        assert out.shape == (1, 3, 256)
+    if kind == "hooked":
+        assert len(got._forward_hooks) == 1 and len(got._forward_pre_hooks) == 1
+        assert len(got._backward_hooks) == 1 and len(got.b[0]._forward_hooks) == 1
+        assert got._forward_hooks is not m._forward_hooks
+        got(torch.zeros(3, 6, requires_grad=True)).sum().backward()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("where", ["cpu", "cuda:0"])
+@pytest.mark.parametrize("kind", KINDS)
+def test_fedavg_result_of_reference_trees(kind, where):
+    """The whole FedAvg.aggregate on 3 models of each tree (CPU modules: the host paths; device modules:
+    the device round): the result's object graph is deepcopy(models[0])'s, its serialize_model bytes as
+    long, its parameters the oracle port's bits (fedavg.py:20-25) and its buffers models[0]'s."""
+    from accdfl_amd.core.gradient_aggregation.fedavg import FedAvg
+    from oracle.fedavg_oracle import fedavg_modules_torch
+
+    models = []
+    for k in range(3):
+        m = _models(kind)
+        with torch.no_grad():
+            for p in m.parameters():
+                p.mul_(1.0 + 0.1 * k)
+        models.append(m)
+    w = [float(x) for x in np.random.default_rng(3).dirichlet(np.ones(3))]
+    ref = fedavg_modules_torch(models, w)
+    dev_models = [m.to(where) for m in copy.deepcopy(models)]
+    got = FedAvg.aggregate(dev_models, w)
+    torch.cuda.synchronize()
+    want = copy.deepcopy(dev_models[0])
+    _same_tree(want, got, {}, {})
+    for (n, p), q in zip(got.named_parameters(), ref.parameters()):
+        assert torch.equal(p.detach().cpu().view(torch.int32), q.detach().view(torch.int32)), n
+    for (n, b), c in zip(got.named_buffers(), dev_models[0].buffers()):
+        assert torch.equal(b, c) and b.data_ptr() != c.data_ptr(), n
+    cpu_got = got if where == "cpu" else copy.deepcopy(got).cpu()
+    assert _sd_pickle_len(cpu_got) == _sd_pickle_len(ref)

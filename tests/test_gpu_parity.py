@@ -1403,3 +1403,66 @@ def test_wsum_mixed_rejects_bad_arguments():
     with pytest.raises(_lib.DlaggError, match="aliases"):
         _lib.wsum_mixed_ptrs(_lib.DLA_F32, [_lib.DLA_F32, _lib.DLA_BF16], [a.data_ptr(), b.data_ptr()], [0.5, 0.5],
                              64, b.data_ptr(), 0)
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+def test_multi_table_back_to_back_rounds_reuse_slots_safely(dtype):
+    """24 table reduces enqueued back to back — alternating two streams, each round with its own
+    weights, its own outputs and a rotated peer order — with no host synchronisation in between: the
+    table ring reuses its 8 slots under one event per 4 calls, and the upload takes both policy branches
+    (a copy kernel on an idle stream; a side-stream copy overlapping the kernel queued before it, for
+    rounds of >= 256 MiB).  Every round's every element against the oracle afterwards."""
+    from accdfl_amd.core import wsum
+
+    n = 40
+    sizes = [3_300_007, 1_000_001, 257, 64, 5]  # ~ (n + 1) x 4.3 M elements: >= 256 MiB in f32 and bf16 x 2
+    big = dtype == "f32"
+    if not big:
+        sizes[0] = 6_600_013
+    g = torch.Generator().manual_seed(77)
+    peers_cpu = [[(torch.randn(sz, generator=g) * 0.05).to(TDT[dtype]) for sz in sizes] for _ in range(n)]
+    dev = [[t.cuda() for t in pl] for pl in peers_cpu]
+    streams = [torch.cuda.current_stream(), torch.cuda.Stream()]
+    streams[1].wait_stream(streams[0])
+    rounds = []
+    for r in range(24):
+        order = [(k + r) % n for k in range(n)]
+        w = [float(x) for x in np.random.default_rng(r).dirichlet(np.ones(n))]
+        outs = [torch.empty(sz, dtype=TDT[dtype], device="cuda") for sz in sizes]
+        s = streams[r % 2]
+        with torch.cuda.stream(s):
+            wsum.wsum_multi([dev[k] for k in order], w, outs)
+        for o in outs:
+            o.record_stream(s)
+        rounds.append((order, w, outs))
+    torch.cuda.synchronize()
+    for r, (order, w, outs) in enumerate(rounds):
+        for i, sz in enumerate(sizes):
+            flat = [gc.as_float(_bits(peers_cpu[k][i], dtype), dtype) for k in order]
+            want = c_wsum(flat, w, dtype)
+            assert same_bits(gc.as_float(_bits(outs[i], dtype), dtype), want, dtype), "round %d tensor %d" % (r, i)
+
+
+def test_device_result_record_stream_and_sharing():
+    """The result of a device round: its parameters are parts of one allocation, each with a storage of
+    its own (walk.cpp alias_of).  Pinned here as INTEGRATION.md §2 documents it:
+    record_stream on a result parameter is accepted (and a no-op: the caching allocator skips memory it
+    did not hand out), every parameter pickles only its own bytes, and state_dict clones are ordinary
+    allocator tensors (what a caller sends to another process instead)."""
+    import pickle
+
+    from accdfl_amd.core.gradient_aggregation.fedavg import FedAvg
+
+    models = [torch.nn.Sequential(torch.nn.Linear(300, 200), torch.nn.Linear(200, 10)).cuda() for _ in range(3)]
+    out = FedAvg.aggregate(models, None)
+    side = torch.cuda.Stream()
+    for p in out.parameters():
+        p.record_stream(side)  # accepted
+    sizes = [p.untyped_storage().nbytes() for p in out.parameters()]
+    assert sizes == [p.numel() * p.element_size() for p in out.parameters()]
+    cpu = {k: v.cpu() for k, v in out.state_dict().items()}
+    assert len(pickle.dumps(cpu)) == len(pickle.dumps({k: v.cpu() for k, v in models[0].state_dict().items()}))
+    clones = {k: v.clone() for k, v in out.state_dict().items()}
+    for k, v in clones.items():
+        assert v.untyped_storage().data_ptr() == v.data_ptr() and torch.equal(v, out.state_dict()[k])
+    torch.cuda.synchronize()
