@@ -2152,15 +2152,18 @@ hipError_t take_event(int dev, hipEvent_t* ev) {  // caller holds g_shard_mu; de
 // ~24 us of idle GPU per call (kernel end -> DMA start 9 us, the 19.6 KB DMA 6 us, DMA end -> next kernel
 // 8 us: profiles/r05c, 16 google_speech ResNet-34 models, back to back), against ~6 us between two
 // kernels.  Policy (profiles/r05d, modes A/B'd under DLA_TABLE_COPY in the tuning build):
-//  * the stream still has work queued and the call moves >= 256 MiB (its kernel runs >= ~40 us: rounds
-//    back to back): the copy runs on a library side stream of the device WHILE the queued kernel runs,
-//    and the calling thread waits for it (~15-20 us) before enqueuing the reduce — nothing sits between
-//    the kernels (mode 3; a barrier packet waiting on the copy's event, mode 2, still costs ~11 us);
+//  * the stream is still busy with this library's earlier table reduces (stream_busy_through) and the
+//    call moves >= 256 MiB (its kernel runs >= ~40 us: rounds back to back): the copy runs on a library
+//    side stream of the device WHILE the queued kernel runs, and the calling thread waits for it
+//    (~15-20 us) before enqueuing the reduce — nothing sits between the kernels (mode 3: 1.8 us from one
+//    kernel's end to the next one's start, as with no upload at all; a barrier packet waiting on the
+//    copy's event, mode 2, still costs ~11 us);
 //  * otherwise (an idle GPU, or short kernels the host wait would outlast): a copy kernel on the stream
 //    reads the page-locked table across PCIe (mode 1: 3-4 us, no copy-engine hand-off);
 //  * a table that is not device-mapped page-locked memory: hipMemcpyAsync on the stream (mode 0).
 // 16 x ResNet-34 bf16 back to back 134.5 -> 117.7 us, one call on an idle GPU 146.5 -> 139 us;
-// 64 x ResNet-8 225 -> 210 us; 128 x ResNet-34 bf16 894 -> 877 us; the small rounds unchanged.
+// 64 x ResNet-8 225 -> 205 us; 128 x ResNet-34 bf16 894 -> 851 us; the small rounds unchanged
+// (profiles/r05d, r05f, r05g).
 __global__ __launch_bounds__(256) void table_copy_kernel(const uint4* __restrict__ src, uint4* __restrict__ dst,
                                                          int64_t n16) {
   for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; i < n16;
@@ -2171,7 +2174,33 @@ __global__ __launch_bounds__(256) void table_copy_kernel(const uint4* __restrict
 constexpr int64_t kTableSideCopyMinBytes = int64_t{256} << 20;
 std::map<int, hipStream_t> g_table_streams;  // device -> side stream of the table uploads (dla_shutdown frees)
 
-int table_copy_mode() {  // -1 = the policy; the tuning build's DLA_TABLE_COPY forces 0..3 (5: diagnostic)
+// Is the reduce's stream still busy with the table reduces this library queued on it — will it be when a
+// side copy started now has finished?  Estimated on the host from the work queued (its algorithmic bytes at
+// 6 TB/s, the table kernel's measured rate), not asked of the runtime: hipStreamQuery costs ~4 us of GPU
+// time between the kernels (profiles/r05g: 120.2 vs 115.8 us start to start, 16 x ResNet-34).  Work other
+// than this library's on the stream is not seen: such a stream counts as idle (the copy kernel, correct
+// and 4-6 us slower back to back).
+struct StreamClock {
+  std::chrono::steady_clock::time_point busy_until;
+};
+std::mutex g_clock_mu;
+std::map<hipStream_t, StreamClock> g_stream_clock;
+
+bool stream_busy_through(hipStream_t s, int64_t moved) {
+  using clk = std::chrono::steady_clock;
+  constexpr double kBytesPerUs = 6.0e6;                   // ~6 TB/s
+  const auto side_copy = std::chrono::microseconds(25);  // side copy + the host's wait for it
+  const auto now = clk::now();
+  std::lock_guard<std::mutex> lock(g_clock_mu);
+  if (g_stream_clock.size() > 64) g_stream_clock.clear();  // streams come and go: keep the map small
+  StreamClock& c = g_stream_clock[s];
+  const bool busy = c.busy_until > now + side_copy;
+  const auto start = busy ? c.busy_until : now + side_copy;
+  c.busy_until = start + std::chrono::microseconds(static_cast<int64_t>(static_cast<double>(moved) / kBytesPerUs));
+  return busy;
+}
+
+int table_copy_mode() {  // -1 = the policy; the tuning build's DLA_TABLE_COPY forces 0..3
   static const int mode = [] {
     const char* v = tuning_env("DLA_TABLE_COPY");
     return v ? std::atoi(v) : -1;
@@ -2182,22 +2211,7 @@ int table_copy_mode() {  // -1 = the policy; the tuning build's DLA_TABLE_COPY f
 hipError_t upload_table(char* td, const char* th, size_t bytes, int64_t moved, hipStream_t s) {
   const bool mapped = (bytes & 15u) == 0 && is_mapped_host_ptr(th);
   int mode = table_copy_mode();
-  if (mode < 0) {
-    mode = mapped ? 1 : 0;
-    if (moved >= kTableSideCopyMinBytes) {
-      const hipError_t q = hipStreamQuery(s);
-      if (q != hipSuccess && q != hipErrorNotReady) return q;
-      if (q == hipErrorNotReady) mode = 3;
-    }
-  }
-  if (mode == 5) {  // DIAGNOSTIC (tuning build only): upload a device slot once, then trust it holds the
-    // same table — valid only for a caller that repeats one identical call (profiles/r05_table_probe.py),
-    // to time the kernels back to back with nothing between them
-    static std::set<char*> seen;
-    std::lock_guard<std::mutex> lock(g_shard_mu);
-    if (!seen.insert(td).second) return hipSuccess;
-    return hipMemcpyAsync(td, th, bytes, hipMemcpyHostToDevice, s);
-  }
+  if (mode < 0) mode = (moved >= kTableSideCopyMinBytes && stream_busy_through(s, moved)) ? 3 : mapped ? 1 : 0;
   if (mode == 1 && mapped) {
     const int64_t n16 = static_cast<int64_t>(bytes / 16);
     int64_t grid = (n16 + 255) / 256;

@@ -20,7 +20,9 @@ from accdfl_amd import _lib  # noqa: E402
 from ab_r03_kernels import bind_tiled  # noqa: E402
 
 SHAPES = {"ns": (8, 25_000_000, torch.float32, 16384), "c4share": (128, 2_662_045, torch.bfloat16, 4096),
-          "c4whole": (128, 21_296_355, torch.bfloat16, 4096)}
+          "c4whole": (128, 21_296_355, torch.bfloat16, 4096),
+          # round 5: the flat tile-interleaved slab of the same bytes as r34x16 (16 KiB tiles for 16 rows)
+          "r34flat16": (16, 21_296_355, torch.bfloat16, 16384)}
 
 
 MODULE_SHAPES = {"r34x16": ("google_speech_resnet34", 16), "r34x128": ("google_speech_resnet34", 128)}
