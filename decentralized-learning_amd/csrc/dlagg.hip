@@ -944,31 +944,19 @@ struct WeightTable {
   W w[KMAX];
 };
 
-// XCD-contiguous order of a grid's workgroups: the dispatcher hands workgroup b to XCD b % 8, so
-// consecutive blocks land on different XCDs and every XCD's resident waves span the whole active window
-// (each XCD translating every page of it).  Logical block L(b) gives XCD x the contiguous range
-// [x * per + min(x, rem), ...) of the grid instead — a bijection for any grid size.
-__device__ __attribute__((always_inline)) inline int64_t xcd_contiguous(int64_t b, int64_t grid) {
-  constexpr int64_t kXcds = 8;
-  const int64_t per = grid / kXcds, rem = grid % kXcds;
-  const int64_t x = b % kXcds, i = b / kXcds;
-  return x < rem ? x * (per + 1) + i : rem * (per + 1) + (x - rem) * per + i;
-}
-
 template <int DT, int KMAX, int G, bool ACC_IN, bool PLAIN_ST>
 __global__ __launch_bounds__(64) void wsum_multi_vec_kernel(const MultiIndex* __restrict__ idx,
                                                             const MultiSeg* __restrict__ segs, int n_seg, int k0,
                                                             int n_peers,
-                                                            const WeightTable<typename Ops<DT>::w_t, KMAX> wt,
-                                                            int xcd_remap) {
+                                                            const WeightTable<typename Ops<DT>::w_t, KMAX> wt) {
   static_assert(DT != DLA_F64, "dword folds: f32 / bf16 / f16");
   using O = Ops<DT>;
   using acc_t = typename O::acc_t;
   constexpr int VW = 2;
   using V = typename VecOf<VW>::T;
   constexpr int WE = O::WE;
-  const int64_t b = xcd_remap ? xcd_contiguous(blockIdx.x, gridDim.x) : static_cast<int64_t>(blockIdx.x);
-  const int lo = multi_segment(idx, static_cast<int>(b));
+  const int64_t b = blockIdx.x;
+  const int lo = multi_segment(idx, static_cast<int>(blockIdx.x));
   const int64_t n_vecs = segs[lo].n_vecs;
   const int64_t local = b - segs[lo].wg_begin;
   const PeerRef<typename O::w_t> tab{(ConstPeerTab)(segs[lo].ptrs + k0), wt.w};
@@ -1829,18 +1817,14 @@ hipError_t launch_multi_vec(const MultiIndex* idx, const MultiSeg* segs, int n_s
   for (int k = 0; k < pm; ++k) wt.w[k] = static_cast<W>(weights[k0 + k]);  // RNE double -> op-math
   const dim3 g(static_cast<unsigned>(grid)), bl(64);
   const int wgs = vec_wgs_cap_rows(DT, pm, grid * 64, true);  // every workgroup folds 64 vectors
-  static const int remap = [] {  // A/B knob of the tuning build (DLA_MULTI_XCD=1: XCD-contiguous blocks)
-    const char* v = tuning_env("DLA_MULTI_XCD");
-    return v ? std::atoi(v) : 0;
-  }();
   if (plain) {
     static const size_t st_lds = static_lds_of(&wsum_multi_vec_kernel<DT, KMAX, G, ACC_IN, true>);
     hipLaunchKernelGGL((wsum_multi_vec_kernel<DT, KMAX, G, ACC_IN, true>), g, bl, lds_pad_for(st_lds, wgs), s, idx,
-                       segs, n_seg, k0, pm, wt, remap);
+                       segs, n_seg, k0, pm, wt);
   } else {
     static const size_t st_lds = static_lds_of(&wsum_multi_vec_kernel<DT, KMAX, G, ACC_IN, false>);
     hipLaunchKernelGGL((wsum_multi_vec_kernel<DT, KMAX, G, ACC_IN, false>), g, bl, lds_pad_for(st_lds, wgs), s, idx,
-                       segs, n_seg, k0, pm, wt, remap);
+                       segs, n_seg, k0, pm, wt);
   }
   return hipGetLastError();
 }
