@@ -5,7 +5,8 @@
  *       -D__HIP_PLATFORM_AMD__ -Ldecentralized-learning_amd/lib -ldlagg -L/opt/rocm/lib -lamdhip64 -o c_abi_demo
  * Runs FedAvg (dla_wsum, a dla_plan with changed weights, the bucket-sharded dla_wsum_sharded and
  * the tile-interleaved dla_wsum_slab_tiled, host-resident peers through dla_host_round_* and the
- * chunked dla_host_reduce) and the
+ * chunked dla_host_reduce, peers staged by dla_slab_stage, peers of several dtypes through
+ * dla_wsum_mixed) and the
  * teacher-logit mean (dla_mean) on N peers and checks every element bit-for-bit against the reference's
  * sequential arithmetic written out in C (fedavg.py:21-25).  Exit status 0 = all equal.
  */
@@ -35,6 +36,22 @@
       return 3;                                                           \
     }                                                                     \
   } while (0)
+
+/* RNE float -> bf16 bits (NaN -> 0x7FC0), and back */
+static uint16_t to_bf16(float f) {
+  uint32_t u;
+  memcpy(&u, &f, 4);
+  if (isnan(f)) return 0x7FC0;
+  u += 0x7FFFu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+
+static float from_bf16(uint16_t h) {
+  uint32_t u = (uint32_t)h << 16;
+  float f;
+  memcpy(&f, &u, 4);
+  return f;
+}
 
 static int same_f32(float a, float b) {
   uint32_t x, y;
@@ -284,7 +301,83 @@ int main(void) {
     CHECK_HIP(hipStreamDestroy(cst));
   }
 
-  /* 8. errors come back as codes with a message */
+  /* 8. peers staged into a tile-interleaved slab row by row (dla_slab_stage: host -> device, one 2D
+   *    copy per row for the whole tiles) and reduced from it; a range past the slab is refused */
+  {
+    const int64_t T = dla_slab_tile_elems(DLA_F32, N, P);
+    const int64_t n_t = (P + T - 1) / T;
+    void* dev_tiled;
+    CHECK_HIP(hipMalloc(&dev_tiled, sizeof(float) * (size_t)(n_t * N * T)));
+    for (int k = 0; k < N; ++k)
+      CHECK_DLA(dla_slab_stage(DLA_F32, dev_tiled, T, N, n_t, k, 0, host[k], P, NULL));
+    CHECK_HIP(hipDeviceSynchronize());
+    CHECK_DLA(dla_wsum_slab_tiled(DLA_F32, dev_tiled, T, N, w, N, P, dev_out, NULL, NULL));
+    CHECK_HIP(hipMemcpy(out_host, dev_out, sizeof(float) * P, hipMemcpyDeviceToHost));
+    for (int64_t j = 0; j < P; ++j) {
+      volatile float acc = host[0][j] * 0.0f;
+      for (int k = 0; k < N; ++k) {
+        volatile float prod = (float)w[k] * host[k][j];
+        acc = acc + prod;
+      }
+      if (!same_f32(acc, out_host[j])) {
+        fprintf(stderr, "dla_slab_stage + dla_wsum_slab_tiled mismatch at %lld\n", (long long)j);
+        return 1;
+      }
+    }
+    if (dla_slab_stage(DLA_F32, dev_tiled, T, N, n_t, 0, n_t * T - 10, host[0], 11, NULL) != DLA_E_INVALID) {
+      fprintf(stderr, "expected DLA_E_INVALID for a range past the slab\n");
+      return 1;
+    }
+    CHECK_HIP(hipFree(dev_tiled));
+  }
+
+  /* 9. peers of several dtypes (dla_wsum_mixed): models[0] f32, then a peer in f64 and one in bf16 —
+   *    fedavg.py:25 rounds w * p in the peer's dtype and adds in the promoted type (f64 with the f64
+   *    peer, f32 with the bf16 one), rounding the sum to f32 */
+  {
+    double* h64 = (double*)malloc(sizeof(double) * P);
+    uint16_t* h16 = (uint16_t*)malloc(sizeof(uint16_t) * P);
+    void *d64, *d16;
+    for (int64_t j = 0; j < P; ++j) {
+      h64[j] = (double)host[1][j] * 1.0000001;
+      h16[j] = to_bf16(host[2][j]);
+    }
+    CHECK_HIP(hipMalloc(&d64, sizeof(double) * P));
+    CHECK_HIP(hipMalloc(&d16, sizeof(uint16_t) * P));
+    CHECK_HIP(hipMemcpy(d64, h64, sizeof(double) * P, hipMemcpyHostToDevice));
+    CHECK_HIP(hipMemcpy(d16, h16, sizeof(uint16_t) * P, hipMemcpyHostToDevice));
+    const void* mp[3] = {dev[0], d64, d16};
+    const int dts[3] = {DLA_F32, DLA_F64, DLA_BF16};
+    const double mw[3] = {0.2, 0.3, 0.5};
+    CHECK_DLA(dla_wsum_mixed(DLA_F32, dts, mp, mw, 3, P, dev_out, NULL));
+    CHECK_HIP(hipMemcpy(out_host, dev_out, sizeof(float) * P, hipMemcpyDeviceToHost));
+    for (int64_t j = 0; j < P; ++j) {
+      volatile float acc = host[0][j] * 0.0f;
+      volatile float p0 = (float)mw[0] * host[0][j];
+      acc = acc + p0;
+      volatile double p1 = mw[1] * h64[j];
+      volatile double s1 = (double)acc + p1;
+      acc = (float)s1;
+      volatile float p2f = (float)mw[2] * from_bf16(h16[j]);
+      const float p2 = from_bf16(to_bf16(p2f));
+      acc = acc + p2;
+      if (!same_f32(acc, out_host[j])) {
+        fprintf(stderr, "dla_wsum_mixed mismatch at %lld\n", (long long)j);
+        return 1;
+      }
+    }
+    const int bad[3] = {DLA_BF16, DLA_F64, DLA_BF16};  /* peers[0] must carry out_dtype */
+    if (dla_wsum_mixed(DLA_F32, bad, mp, mw, 3, P, dev_out, NULL) != DLA_E_INVALID) {
+      fprintf(stderr, "expected DLA_E_INVALID for peers[0] not in out_dtype\n");
+      return 1;
+    }
+    CHECK_HIP(hipFree(d64));
+    CHECK_HIP(hipFree(d16));
+    free(h64);
+    free(h16);
+  }
+
+  /* 10. errors come back as codes with a message */
   if (dla_wsum(DLA_F32, (const void* const*)dev, w, 0, P, dev_out, NULL) != DLA_E_INVALID ||
       strlen(dla_last_error()) == 0) {
     fprintf(stderr, "expected DLA_E_INVALID for n_peers = 0\n");
@@ -298,7 +391,7 @@ int main(void) {
   CHECK_HIP(hipFree(dev_out));
   free(out_host);
   printf("c_abi_demo ok: dla_wsum, dla_plan, dla_mean, dla_wsum_sharded, dla_wsum_slab_tiled, dla_host_round, "
-         "dla_host_reduce (+ launch / join) "
+         "dla_host_reduce (+ launch / join), dla_slab_stage, dla_wsum_mixed "
          "bit-exact on %d peers "
          "x %lld fp32\n", N, (long long)P);
   return 0;
