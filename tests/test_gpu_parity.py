@@ -1466,3 +1466,32 @@ def test_device_result_record_stream_and_sharing():
     for k, v in clones.items():
         assert v.untyped_storage().data_ptr() == v.data_ptr() and torch.equal(v, out.state_dict()[k])
     torch.cuda.synchronize()
+
+
+def test_grouped_device_round_with_a_late_mixed_dtype_model():
+    """A device round of >= 64 models is launched group by group (_device_round_grouped); when a model
+    of another dtype appears only in a later group, the grouped launches are abandoned and the round is
+    averaged by the promoted path — bit-exact against the mixed oracle, parameter by parameter."""
+    from accdfl_amd.core.gradient_aggregation.fedavg import FedAvg
+    from oracle.fedavg_oracle import fedavg_bits_mixed
+
+    n = 70
+    shapes = [(300,), (17, 5), (64,)]
+    g = torch.Generator().manual_seed(70)
+    dts = ["f32"] * n
+    dts[40] = "bf16"
+    dts[55] = "f64"
+    models = []
+    for k in range(n):
+        m = torch.nn.Module()
+        m.ps = torch.nn.ParameterList([torch.nn.Parameter((torch.randn(s, generator=g, dtype=torch.float64) * 0.05)
+                                                          .to(TDT[dts[k]]).cuda()) for s in shapes])
+        models.append(m)
+    w = [float(x) for x in np.random.default_rng(70).dirichlet(np.ones(n))]
+    out = FedAvg.aggregate(models, w)
+    torch.cuda.synchronize()
+    for i, p in enumerate(out.parameters()):
+        assert p.dtype == torch.float32
+        flat = [gc.as_float(gc.from_torch(m.ps[i], d), d).reshape(-1) for m, d in zip(models, dts)]
+        want = fedavg_bits_mixed(flat, dts, w)
+        assert same_bits(gc.from_torch(p, "f32").reshape(-1), want.view(np.uint32), "f32"), i
