@@ -1407,6 +1407,9 @@ unsigned vec_lds_pad() {
 // over >= 1 GiB fold 16 peers per round under W = 8 (32 x 10 M f32 199.3 -> 191.5, 64 x 4.93 M f32 192.2
 // -> 184.3, 128 x 21.3 M bf16 813.8 -> 803.3, profiles/r03ai) and below it run uncapped (configs[4]'s
 // 681 MB share and configs[3']'s 316 MB bucket lose with any cap).
+// Round 5 lowered the floor to 160 MiB for passes of exactly 8 peers (the north star's 4-way strong-split
+// bucket, 8 x 6.25 M f32 = 200 MB: W = 14 33.7-34.0 us against 34.8-34.9 uncapped; its 8-way bucket,
+// 100 MB, and the 64-peer buckets tie or lose with any cap, profiles/r05p/cap.jsonl).
 // In the tuning build DLA_VEC_WGS_PER_CU=W overrides the policy and DLA_VEC_CAP_TABLE=1 restores the
 // round-3 table (A/B sweeps).
 int vec_wgs_env() {
@@ -1444,7 +1447,7 @@ int vec_wgs_cap(int n_peers, int G, int64_t n_vecs, int natural) {
   const int env = vec_wgs_env();
   if (env >= 0) return env;
   const int64_t in_bytes = static_cast<int64_t>(n_peers) * n_vecs * 8;
-  if (in_bytes < (int64_t{256} << 20)) return 0;
+  if (in_bytes < (n_peers == 8 ? (int64_t{160} << 20) : (int64_t{256} << 20))) return 0;
   static const bool table = [] {
     const char* v = tuning_env("DLA_VEC_CAP_TABLE");
     return v && std::atoi(v) == 1;
