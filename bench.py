@@ -116,7 +116,9 @@ def parse():
     ap.add_argument("--layout", default="slab", choices=["slab", "rows"],
                     help="HBM layout of the headline's peers: the PeerSlab tile-interleaved slab (default) or "
                          "one buffer per peer")
-    ap.add_argument("--strong-steps", type=int, default=20)
+    ap.add_argument("--strong-steps", type=int, default=200,
+                    help="timed steps of each strong-scaling line: the barrier that closes the timed region is "
+                         "paid once per line, so short steps need many (an 8-way north-star bucket is ~19 us)")
     ap.add_argument("--leg-timeout", type=float, default=300.0,
                     help="seconds any one leg (the headline included) may take on any rank; past it the run "
                          "ends at once with a non-zero exit, rank 0 printing the line measured so far")
