@@ -440,7 +440,7 @@ def _device_round(models: List[nn.Module], weights, layout) -> "nn.Module | None
     flat = torch.empty(total, dtype=dtype, device=device)
     ptrs = (ctypes.c_void_p * table.size).from_buffer(table)
     outs = (ctypes.c_void_p * len(numels)).from_buffer(byte_offs + flat.data_ptr())
-    _wsum.wsum_multi_ptrs(dtype, ptrs, outs, nums, weights, device)
+    _wsum.wsum_multi_ptrs(dtype, ptrs, outs, nums, weights, device, total_elems=sum(numels))
     # models[0]'s own objects, checked after the launch (the GPU starts sooner; a tree the result cannot be
     # built over leaves `flat` unused, and the per-tensor path launches into its own tensors)
     objs = mod.tensors(models[0], _PLAIN_SET)
@@ -498,7 +498,7 @@ def _device_round_grouped(models: List[nn.Module], weights) -> "nn.Module | None
     flat = torch.empty(total, dtype=dtype, device=device)
     outs = (ctypes.c_void_p * len(numels)).from_buffer(byte_offs + flat.data_ptr())
     _wsum.wsum_multi_ptrs(dtype, (ctypes.c_void_p * table.size).from_buffer(table), outs, nums,
-                          weights[a0:b0_], device)
+                          weights[a0:b0_], device, total_elems=sum(numels))
     for a, b in bounds[1:]:
         # each later group checked against models[0]'s layout (shapes, dtype, device) in its own walk
         lay = _device_layout(models[a:b], ref=models[0])
@@ -557,7 +557,7 @@ def _device_round_per_tensor(models: List[nn.Module], weights, layout) -> "nn.Mo
     ptrs = (ctypes.c_void_p * table.size).from_buffer(table)
     outs = (ctypes.c_void_p * len(params))(*[c.data_ptr() for c in params])
     nums = (ctypes.c_int64 * len(numels))(*numels)
-    _wsum.wsum_multi_ptrs(dtype, ptrs, outs, nums, weights, device)
+    _wsum.wsum_multi_ptrs(dtype, ptrs, outs, nums, weights, device, total_elems=sum(numels))
     return _clone_value(models[0], memo)
 
 

@@ -24,6 +24,7 @@ _CODES = {
 }
 
 SUPPORTED_DTYPES = tuple(_CODES)
+_ESIZE = {torch.float32: 4, torch.bfloat16: 2, torch.float16: 2, torch.float64: 8}
 
 
 def dtype_code(dtype: torch.dtype) -> int:
@@ -242,22 +243,33 @@ _rings = {}
 _rings_lock = threading.Lock()
 
 
+_table_bytes = {}  # (n_tensors, n_peers) -> dla_wsum_multi_table_bytes
+
+
 def wsum_multi_ptrs(dtype: torch.dtype, ptrs, out_ptrs, numels, weights: Sequence[float], device: torch.device,
-                    stream: Optional[torch.cuda.Stream] = None, acc_in: bool = False) -> None:
+                    stream: Optional[torch.cuda.Stream] = None, acc_in: bool = False,
+                    total_elems: Optional[int] = None) -> None:
     """wsum_multi on raw pointers the caller has validated (device-resident, contiguous, one dtype,
     numels[i] elements each; ptrs tensor-major [n_tensors * n_peers]).  Rounds of more than
-    MULTI_TABLE_MIN_PEERS - 1 peers go through dla_wsum_multi_table (one launch per 128-peer pass)."""
+    MULTI_TABLE_MIN_PEERS - 1 peers go through dla_wsum_multi_table (one launch per 128-peer pass).
+    ``total_elems``: sum(numels) when the caller knows it (a device round's flat plan: no pass over a
+    ctypes array of numels on the launch path)."""
     code = dtype_code(dtype)
     n = len(weights)
     s = stream if stream is not None else torch.cuda.current_stream(device)
     table = acc_in or n >= MULTI_TABLE_MIN_PEERS or (
-        n > 8 and (n + 1) * sum(numels) * torch.empty((), dtype=dtype).element_size() >= MULTI_TABLE_MIN_BYTES)
+        n > 8 and (n + 1) * (sum(numels) if total_elems is None else total_elems) * _ESIZE[dtype]
+        >= MULTI_TABLE_MIN_BYTES)
     if table and (dtype != torch.float64 or acc_in):  # fp64 folds per tensor inside the table call
         with _rings_lock:
             ring = _rings.get(device)
             if ring is None:
                 ring = _rings[device] = _TableRing(device)
-        idx, h, d = ring.take(_lib.wsum_multi_table_bytes(len(out_ptrs), n))
+        key = (len(out_ptrs), n)
+        nbytes = _table_bytes.get(key)
+        if nbytes is None:
+            nbytes = _table_bytes[key] = _lib.wsum_multi_table_bytes(*key)
+        idx, h, d = ring.take(nbytes)
         try:
             _lib.wsum_multi_table_ptrs(code, ptrs, out_ptrs, numels, weights, h.data_ptr(), d.data_ptr(),
                                        int(s.cuda_stream), acc_in=acc_in)
