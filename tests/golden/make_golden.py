@@ -247,7 +247,8 @@ def save_mixed_cases():
                                 [3.0 / 7.0, 4.0 / 7.0])
                 seed += 10
     spec = [[(64,), (17,)]] * 4
-    for order in (("f32", "bf16", "f16", "f64"), ("bf16", "f64", "f16", "f32"), ("f16", "bf16", "f64", "f32")):
+    for order in (("f32", "bf16", "f16", "f64"), ("bf16", "f64", "f16", "f32"), ("f16", "bf16", "f64", "f32"),
+                  ("f64", "f32", "bf16", "f16")):
         d = [[x] * 2 for x in order]
         save_mixed_case("mixed_specials_%s_n4" % order[0], d, make_peers_mixed(spec, d, 9300, fill=specials),
                         dirichlet(4, 12))

@@ -1495,3 +1495,36 @@ def test_grouped_device_round_with_a_late_mixed_dtype_model():
         flat = [gc.as_float(gc.from_torch(m.ps[i], d), d).reshape(-1) for m, d in zip(models, dts)]
         want = fedavg_bits_mixed(flat, dts, w)
         assert same_bits(gc.from_torch(p, "f32").reshape(-1), want.view(np.uint32), "f32"), i
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16", "f16"])
+def test_multi_table_ieee_specials(dtype, monkeypatch):
+    """The table kernel (dla_wsum_multi_table, 40 peers) on IEEE specials — signed zeros, +-Inf, NaN,
+    subnormals, values that overflow in the sum — in ragged tensors, against the oracle bit for bit (NaN
+    as NaN): the fold is wsum_vec_kernel's, reached through the device-side table."""
+    from accdfl_amd.core import wsum
+
+    monkeypatch.setattr(wsum, "MULTI_TABLE_MIN_PEERS", 33)
+    n = 40
+    sizes = [3, 17, 64, 1000, 4099]
+    specials = torch.tensor([-0.0, 0.0, float("inf"), float("-inf"), float("nan"), 1e-41, 3.0e38, -3.0e38,
+                             6.0e-8, 65500.0, 1.0 + 2.0 ** -9, -1.0 - 2.0 ** -8], dtype=torch.float64)
+    g = torch.Generator().manual_seed(41)
+    peers_cpu = []
+    for k in range(n):
+        pl = []
+        for sz in sizes:
+            v = torch.randn(sz, generator=g, dtype=torch.float64) * 0.05
+            idx = torch.randint(0, sz, (max(1, sz // 5),), generator=g)
+            v[idx] = specials[torch.randint(0, len(specials), (len(idx),), generator=g)]
+            pl.append(v.to(TDT[dtype]))
+        peers_cpu.append(pl)
+    dev = [[t.cuda() for t in pl] for pl in peers_cpu]
+    w = [float(x) for x in np.random.default_rng(41).dirichlet(np.ones(n))]
+    outs = [torch.empty(sz, dtype=TDT[dtype], device="cuda") for sz in sizes]
+    wsum.wsum_multi(dev, w, outs)
+    torch.cuda.synchronize()
+    for i, sz in enumerate(sizes):
+        want = fedavg_bits([gc.as_float(_bits(peers_cpu[k][i], dtype), dtype) for k in range(n)], w, dtype)
+        got = gc.as_float(_bits(outs[i], dtype), dtype)
+        assert same_bits(got, want, dtype), "tensor %d (numel %d)" % (i, sz)
