@@ -1528,3 +1528,63 @@ def test_multi_table_ieee_specials(dtype, monkeypatch):
         want = fedavg_bits([gc.as_float(_bits(peers_cpu[k][i], dtype), dtype) for k in range(n)], w, dtype)
         got = gc.as_float(_bits(outs[i], dtype), dtype)
         assert same_bits(got, want, dtype), "tensor %d (numel %d)" % (i, sz)
+
+
+@pytest.mark.parametrize("n", [3, 40])
+def test_models_split_between_host_and_device(n):
+    """Models whose parameters live partly on the GPU and partly on the CPU, the same split in every model
+    (the reference's c1.add_(w * p1) works for such models: each pair shares a device).  The result keeps
+    every parameter where models[0] has it, bit-exact against the oracle port."""
+    from accdfl_amd.core.gradient_aggregation.fedavg import FedAvg
+    from oracle.fedavg_oracle import fedavg_modules_torch
+
+    g = torch.Generator().manual_seed(n)
+    models, cpu_models = [], []
+    for k in range(n):
+        m = torch.nn.Module()
+        m.a = torch.nn.Parameter(torch.randn(1000, generator=g) * 0.05)
+        m.b = torch.nn.Parameter(torch.randn(33, 7, generator=g) * 0.05)
+        m.c = torch.nn.Parameter(torch.randn(4099, generator=g) * 0.05)
+        cpu_models.append(m)
+        mm = torch.nn.Module()
+        mm.a = torch.nn.Parameter(m.a.detach().clone().cuda())
+        mm.b = torch.nn.Parameter(m.b.detach().clone())  # stays on the CPU
+        mm.c = torch.nn.Parameter(m.c.detach().clone().cuda())
+        models.append(mm)
+    w = [float(x) for x in np.random.default_rng(n).dirichlet(np.ones(n))]
+    want = fedavg_modules_torch(cpu_models, w)
+    out = FedAvg.aggregate(models, w)
+    torch.cuda.synchronize()
+    assert [p.device.type for p in out.parameters()] == ["cuda", "cpu", "cuda"]
+    for (name, p), q in zip(out.named_parameters(), want.parameters()):
+        assert torch.equal(p.detach().cpu().view(torch.int32), q.detach().view(torch.int32)), name
+
+
+@pytest.mark.parametrize("where", ["cpu", "cuda:0"])
+def test_non_contiguous_parameters(where):
+    """Parameters that are strided views (a transposed weight, a column slice) — the reference's torch ops
+    take them as they are; the result keeps each parameter's shape and strides (deepcopy), bit-exact."""
+    from accdfl_amd.core.gradient_aggregation.fedavg import FedAvg
+    from oracle.fedavg_oracle import fedavg_modules_torch
+
+    g = torch.Generator().manual_seed(9)
+    models = []
+    for k in range(5):
+        m = torch.nn.Module()
+        m.t = torch.nn.Parameter((torch.randn(300, 200, generator=g) * 0.05).t())
+        m.s = torch.nn.Parameter((torch.randn(64, 96, generator=g) * 0.05)[:, ::3])
+        m.d = torch.nn.Parameter(torch.randn(777, generator=g) * 0.05)
+        models.append(m.to(where))
+    w = [float(x) for x in np.random.default_rng(9).dirichlet(np.ones(5))]
+    want = fedavg_modules_torch([m.cpu() if where == "cpu" else _cpu_copy(m) for m in models], w)
+    out = FedAvg.aggregate(models, w)
+    torch.cuda.synchronize()
+    for (name, p), q, p0 in zip(out.named_parameters(), want.parameters(), models[0].parameters()):
+        assert p.shape == p0.shape and p.stride() == p0.stride() and p.device == p0.device, name
+        assert torch.equal(p.detach().cpu().view(torch.int32), q.detach().view(torch.int32)), name
+
+
+def _cpu_copy(m):
+    import copy
+
+    return copy.deepcopy(m).cpu()
