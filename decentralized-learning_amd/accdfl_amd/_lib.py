@@ -412,6 +412,7 @@ def wsum_ptrs(dtype_code: int, peer_ptrs: Sequence[int], weights: Sequence[float
     """dla_wsum / dla_wsum_ex on raw device pointers."""
     L = lib()
     n = len(peer_ptrs)
+    _check_tables("wsum", n, 1, weights=weights)
     if cfg is None:
         rc = L.so.dla_wsum(dtype_code, _ptr_array(peer_ptrs), _dbl_array(weights), n, n_elems, out_ptr, stream_ptr)
     else:
@@ -425,6 +426,9 @@ def wsum_mixed_ptrs(out_code: int, peer_codes: Sequence[int], peer_ptrs: Sequenc
     """dla_wsum_mixed: one parameter whose peers have several dtypes (peer_codes[0] == out_code)."""
     L = lib()
     n = len(peer_ptrs)
+    _check_tables("wsum_mixed", n, 1, weights=weights)
+    if len(peer_codes) != n:
+        raise ValueError("wsum_mixed: %d dtypes for %d peers" % (len(peer_codes), n))
     rc = L.so.dla_wsum_mixed(out_code, (ctypes.c_int * n)(*peer_codes), _ptr_array(peer_ptrs), _dbl_array(weights), n,
                              n_elems, out_ptr, stream_ptr)
     L.check(rc, "dla_wsum_mixed")
@@ -445,6 +449,7 @@ def mean_ptrs(dtype_code: int, peer_ptrs: Sequence[int], n_elems: int, out_ptr: 
 def wsum_slab_ptr(dtype_code: int, base_ptr: int, pitch_elems: int, weights: Sequence[float], n_peers: int,
                   n_elems: int, out_ptr: int, stream_ptr: int) -> None:
     L = lib()
+    _check_tables("wsum_slab", n_peers, 1, weights=weights)
     rc = L.so.dla_wsum_slab(dtype_code, base_ptr, pitch_elems, _dbl_array(weights), n_peers, n_elems, out_ptr,
                             stream_ptr)
     L.check(rc, "dla_wsum_slab")
@@ -458,6 +463,8 @@ def wsum_multi_ptrs(dtype_code: int, peer_ptrs: Sequence[int], out_ptrs: Sequenc
     n = len(weights)
     if len(peer_ptrs) != t * n:
         raise ValueError("peer_ptrs must hold n_tensors * n_peers pointers")
+    if len(numels) != t:
+        raise ValueError("wsum_multi: %d numels for %d tensors" % (len(numels), t))
     num = numels if isinstance(numels, ctypes.Array) else (ctypes.c_int64 * t)(*[int(x) for x in numels])
     pa = peer_ptrs if isinstance(peer_ptrs, ctypes.Array) else _ptr_array(peer_ptrs)
     oa = out_ptrs if isinstance(out_ptrs, ctypes.Array) else _ptr_array(out_ptrs)
@@ -483,6 +490,8 @@ def wsum_multi_table_ptrs(dtype_code: int, peer_ptrs, out_ptrs, numels, weights:
         peer_ptrs = (ctypes.c_void_p * len(peer_ptrs))(*peer_ptrs)
     if len(peer_ptrs) != t * n:
         raise ValueError("peer_ptrs must hold n_tensors * n_peers pointers")
+    if len(numels) != t:
+        raise ValueError("wsum_multi_table: %d numels for %d tensors" % (len(numels), t))
     if not isinstance(numels, ctypes.Array):
         numels = (ctypes.c_int64 * t)(*[int(x) for x in numels])
     if acc_in:
@@ -517,12 +526,25 @@ def host_copy_batch(dst_ptrs: Sequence[int], src_ptrs: Sequence[int], nbytes: Se
         L.check(rc, "dla_host_copy_batch")
 
 
+def _check_tables(what: str, n_peers: int, n_tensors: int, tensor_ptrs=None, out_ptrs=None, weights=None):
+    """The host-round entry points read n_peers x n_tensors peer pointers, n_tensors outputs and
+    n_peers weights from the tables they are given: refuse shorter (or longer) tables here instead of
+    letting the library read past their end."""
+    if tensor_ptrs is not None and len(tensor_ptrs) != n_peers * n_tensors:
+        raise ValueError("%s: %d peer pointers for %d tensors of %d peers" % (what, len(tensor_ptrs), n_tensors, n_peers))
+    if out_ptrs is not None and len(out_ptrs) != n_tensors:
+        raise ValueError("%s: %d output pointers for %d tensors" % (what, len(out_ptrs), n_tensors))
+    if weights is not None and len(weights) != n_peers:
+        raise ValueError("%s: %d weights for %d peers" % (what, len(weights), n_peers))
+
+
 def host_round_start(dtype_code: int, n_peers: int, tensor_ptrs: Sequence[int], numels, weights: Sequence[float],
                      rows_ptr: int, pitch_elems: int, result_ptr: int, stream_ptr: int) -> None:
     """dla_host_round_start: pack the peers' host tensors (peer-major) into the page-locked rows
     and enqueue the reduce into the page-locked result.  ``numels``: a sequence or a ctypes
     int64 array (reused across rounds of one layout)."""
     L = lib()
+    _check_tables("host_round_start", n_peers, len(numels), tensor_ptrs, weights=weights)
     if not isinstance(numels, ctypes.Array):
         numels = (ctypes.c_int64 * len(numels))(*numels)
     if not isinstance(tensor_ptrs, ctypes.Array):
@@ -542,6 +564,7 @@ def host_reduce(dtype_code: int, n_peers: int, tensor_ptrs, numels, weights: Seq
     ``outs_ready`` (a ctypes.c_int): dla_host_reduce_deferred — ``out_ptrs`` must then be a ctypes
     array the caller fills in place, then sets ``outs_ready.value`` to 1 (or -1 to give up)."""
     L = lib()
+    _check_tables("host_reduce", n_peers, len(numels), tensor_ptrs, out_ptrs, weights)
     if not isinstance(numels, ctypes.Array):
         numels = (ctypes.c_int64 * len(numels))(*numels)
     if not isinstance(tensor_ptrs, ctypes.Array):
@@ -592,6 +615,7 @@ def host_reduce_launch(device: int, dtype_code: int, n_peers: int, tensor_ptrs, 
     """dla_host_reduce_launch: dla_host_reduce_deferred on a library thread; returns at once.
     ``out_ptrs`` (a ctypes array) is filled by the caller, then ``outs_ready.value`` set to 1 (or -1)."""
     L = lib()
+    _check_tables("host_reduce_launch", n_peers, len(numels), tensor_ptrs, out_ptrs, weights)
     if not isinstance(numels, ctypes.Array):
         numels = (ctypes.c_int64 * len(numels))(*numels)
     if not isinstance(tensor_ptrs, ctypes.Array):
@@ -607,6 +631,7 @@ def host_reduce_launch(device: int, dtype_code: int, n_peers: int, tensor_ptrs, 
 def host_round_finish(dtype_code: int, numels, result_ptr: int, out_ptrs: Sequence[int], stream_ptr: int) -> None:
     """dla_host_round_finish: wait for the reduce, then unpack the result into out_ptrs."""
     L = lib()
+    _check_tables("host_round_finish", 0, len(numels), out_ptrs=out_ptrs)
     if not isinstance(numels, ctypes.Array):
         numels = (ctypes.c_int64 * len(numels))(*numels)
     rc = L.so.dla_host_round_finish(dtype_code, len(numels), numels, result_ptr,
@@ -622,6 +647,7 @@ def wsum_sharded_ptrs(dtype_code: int, dev_ids: Sequence[int], peer_ptrs: Sequen
     g = len(dev_ids)
     if len(out_ptrs) != g or len(stream_ptrs) != g:
         raise ValueError("one out pointer and one stream per shard")
+    _check_tables("wsum_sharded", len(peer_ptrs), 1, weights=weights)
     rc = L.so.dla_wsum_sharded(dtype_code, g, (ctypes.c_int * g)(*dev_ids), _ptr_array(peer_ptrs),
                                _dbl_array(weights), len(peer_ptrs), n_elems, _ptr_array(out_ptrs), gather,
                                _ptr_array(stream_ptrs))

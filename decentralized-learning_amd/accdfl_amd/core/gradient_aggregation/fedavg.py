@@ -801,7 +801,9 @@ def _bucket_native(st: _NativeStaging, dev, flats: List[List[torch.Tensor]], num
     parts = [_flat_slices(f, numels, s, e) for f in flats]
     sizes = [t.numel() for t in parts[0]]
     ptrs = [t.data_ptr() for pl in parts for t in pl]
-    outs = _flat_slices(center, numels, s, e) if h_out is None else [h_out[s:e]]
+    # one output pointer per tensor slice, as dla_host_reduce reads them (a non-dense result lands in
+    # h_out, cut at the same tensor boundaries)
+    outs = _flat_slices(center if h_out is None else list(torch.split(h_out, numels)), numels, s, e)
     compute = torch.cuda.current_stream(dev)
     st.copy_stream.wait_stream(compute)  # earlier users of the device staging are done
     with torch.cuda.device(dev):
@@ -963,6 +965,8 @@ def _reduce_param(device, center: torch.Tensor, terms: List[torch.Tensor], weigh
 def _reduce_param_mixed(device, center: torch.Tensor, terms: List[torch.Tensor], weights: List[float]):
     """A parameter whose contributors do not share models[0]'s dtype (dla_wsum_mixed: products
     rounded in each peer's dtype, sums in the centre's after promotion, fedavg.py:25)."""
+    if center.numel() == 0:
+        return
     dev_terms = [t.detach().to(device).contiguous() for t in terms]
     out = torch.empty(center.numel(), dtype=center.dtype, device=device)
     _wsum.wsum_mixed([t.view(-1) for t in dev_terms], weights, out)

@@ -2741,15 +2741,15 @@ int dla_wsum_mixed(int out_dtype, const int* peer_dtypes, const void* const* pee
   if (n_peers < 1 || !peers || !weights || !peer_dtypes)
     return fail(DLA_E_INVALID, "dla_wsum_mixed: n_peers must be >= 1 with peers, weights and dtypes");
   if (n_elems < 0) return fail(DLA_E_INVALID, "dla_wsum_mixed: n_elems < 0");
-  for (int k = 0; k < n_peers; ++k) {
+  for (int k = 0; k < n_peers; ++k)
     if (elem_size(peer_dtypes[k]) == 0)
       return fail(DLA_E_INVALID, "dla_wsum_mixed: unknown dtype of peer " + std::to_string(k));
-    if (!peers[k]) return fail(DLA_E_INVALID, "dla_wsum_mixed: null peer pointer " + std::to_string(k));
-  }
   if (peer_dtypes[0] != out_dtype)
     return fail(DLA_E_INVALID, "dla_wsum_mixed: peers[0] is models[0], whose deepcopy is the result: "
                                "its dtype must be out_dtype (fedavg.py:20)");
-  if (n_elems == 0) return DLA_OK;
+  if (n_elems == 0) return DLA_OK;  // a 0-element parameter: its tensors may carry null pointers
+  for (int k = 0; k < n_peers; ++k)
+    if (!peers[k]) return fail(DLA_E_INVALID, "dla_wsum_mixed: null peer pointer " + std::to_string(k));
   if (!out) return fail(DLA_E_INVALID, "dla_wsum_mixed: null out");
   for (int k = 1; k < n_peers; ++k)
     if (peers[k] == out) return fail(DLA_E_ALIAS, "dla_wsum_mixed: out aliases peer " + std::to_string(k));

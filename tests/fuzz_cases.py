@@ -1,0 +1,157 @@
+"""Seeded random FedAvg rounds for the fuzz parity tests (test_fuzz_fedavg.py).
+
+Each case is a list of peer nn.Modules and a weights argument drawn from one seed, covering what
+/root/reference/accdfl/core/gradient_aggregation/fedavg.py:13-26 accepts and computes:
+
+* 1 to 130 models (one and two 128-peer passes), 1 to 6 parameters each, 0 to 70 000 elements,
+  0-3 dimensions, some of them transposed (non-contiguous) views;
+* one dtype for the round (f32 / bf16 / f16 / f64), or dtypes that differ between models or
+  between parameters (the promotion of :25);
+* models with fewer or more parameters than models[0] (the zip truncation of :24), models with
+  no parameter at all, a buffer that is not averaged;
+* weights that are None (:14-15), Dirichlet, signed, Python ints, numpy float32 values, 0-d
+  tensors, or carry zeros, NaN, infinities, subnormals and huge values;
+* element values with NaN, infinities, signed zeros, subnormals and values near each dtype's
+  maximum sprinkled in.
+
+expected(models, weights) restates the reference per parameter with the C oracle
+(oracle/fedavg_ref.c through c_oracle.py: test infrastructure only)."""
+import numpy as np
+import torch
+from torch import nn
+
+from c_oracle import c_wsum, c_wsum_mixed
+
+DTS = ["f32", "bf16", "f16", "f64"]
+TDT = {"f32": torch.float32, "bf16": torch.bfloat16, "f16": torch.float16, "f64": torch.float64}
+NAME = {v: k for k, v in TDT.items()}
+_SPECIAL = [float("nan"), float("inf"), float("-inf"), -0.0, 0.0, 1e-45, -1e-42, 3e38, 6.5e4, 1e-8, 1e300]
+_NUMELS = [0, 1, 2, 3, 4, 5, 7, 8, 15, 16, 17, 63, 64, 65, 255, 1000, 4097, 12_345, 65_537, 70_001]
+_PEERS = [1, 1, 2, 2, 3, 4, 5, 7, 8, 8, 9, 16, 17, 31, 33, 64, 128, 129, 130]
+
+N_CASES = 96
+
+
+class _Peer(nn.Module):
+    def __init__(self, params, buf=None):
+        super().__init__()
+        for i, p in enumerate(params):
+            setattr(self, "p%d" % i, p)
+        if buf is not None:
+            self.register_buffer("stat", buf)
+
+
+def _shape_of(rng, numel):
+    if numel == 0:
+        return [(0,), (0, 3), (4, 0)][rng.integers(3)]
+    dims = int(rng.integers(0, 4)) if numel == 1 else int(rng.integers(1, 4))
+    if dims == 0:
+        return ()
+    if dims == 1:
+        return (numel,)
+    divs = [d for d in range(1, min(numel, 400) + 1) if numel % d == 0]
+    a = int(divs[rng.integers(len(divs))])
+    if dims == 2:
+        return (a, numel // a)
+    divs2 = [d for d in range(1, min(numel // a, 64) + 1) if (numel // a) % d == 0]
+    b = int(divs2[rng.integers(len(divs2))])
+    return (a, b, numel // a // b)
+
+
+def _values(rng, numel, dt, specials):
+    x = rng.standard_normal(numel) * (10.0 ** rng.integers(-3, 3))
+    if specials and numel:
+        for i in rng.integers(0, numel, size=min(numel, int(rng.integers(1, 6)))):
+            x[i] = _SPECIAL[rng.integers(len(_SPECIAL))]
+    with np.errstate(all="ignore"):
+        return torch.from_numpy(x).to(TDT[dt])
+
+
+def _param(rng, shape, dt, transposed, specials):
+    numel = int(np.prod(shape)) if shape else 1
+    if transposed and len(shape) == 2:
+        t = _values(rng, numel, dt, specials).view(shape[1], shape[0]).t()  # non-contiguous
+    else:
+        t = _values(rng, numel, dt, specials).view(shape)
+    return nn.Parameter(t, requires_grad=bool(rng.integers(0, 4) > 0))
+
+
+def _weights(rng, n):
+    mode = rng.integers(0, 8)
+    if mode == 0:
+        return None, "none"
+    if mode == 1:
+        return [float(x) for x in rng.dirichlet(np.ones(n))], "dirichlet"
+    if mode == 2:
+        return [float(x) for x in rng.standard_normal(n)], "signed"
+    if mode == 3:
+        return [int(x) for x in rng.integers(-3, 4, size=n)], "ints"
+    if mode == 4:
+        return [np.float32(x) for x in rng.dirichlet(np.ones(n))], "np.float32"
+    if mode == 5:
+        dt = [torch.float32, torch.float64][rng.integers(2)]
+        return [torch.tensor(float(x), dtype=dt) for x in rng.dirichlet(np.ones(n))], "0-d tensors"
+    w = [float(x) for x in rng.dirichlet(np.ones(n))]
+    for i in rng.integers(0, n, size=min(n, 3)):
+        w[i] = [0.0, -0.0, float("nan"), float("inf"), 1e-40, 1e30, -2.5][rng.integers(7)]
+    return w, "special"
+
+
+def make_case(seed: int, device="cpu"):
+    """(models, weights, description) of case ``seed``."""
+    rng = np.random.default_rng(7919 * seed + 17)
+    n = int(_PEERS[rng.integers(len(_PEERS))])
+    n_params = int(rng.integers(1, 7))
+    shapes = [_shape_of(rng, int(_NUMELS[rng.integers(len(_NUMELS))])) for _ in range(n_params)]
+    transposed = [bool(rng.integers(0, 3) == 0) for _ in range(n_params)]
+    dmode = rng.integers(0, 10)
+    base = DTS[rng.integers(4)] if rng.integers(0, 3) else "f32"
+    if dmode < 6:  # one dtype for the whole round
+        dts = [[base] * n_params for _ in range(n)]
+    elif dmode < 8:  # per model
+        per = [base] + [DTS[rng.integers(4)] if rng.integers(0, 3) == 0 else base for _ in range(n - 1)]
+        dts = [[d] * n_params for d in per]
+    else:  # per model and parameter
+        dts = [[DTS[rng.integers(4)] if rng.integers(0, 4) == 0 else base for _ in range(n_params)]
+               for _ in range(n)]
+    trunc = rng.integers(0, 5) == 0
+    lens = [n_params] + [int(rng.integers(0, n_params + 1)) if trunc and rng.integers(0, 2) else n_params
+                         for _ in range(n - 1)]
+    if trunc and rng.integers(0, 2):
+        lens[0] = int(rng.integers(1, n_params + 1))  # models[0] shorter than others
+    specials = rng.integers(0, 4) == 0
+    buf = rng.integers(0, 3) == 0
+    models = []
+    for k in range(n):
+        ps = [_param(rng, shapes[i], dts[k][i], transposed[i], specials) for i in range(lens[k])]
+        b = torch.full((3,), float(k)) if buf else None
+        models.append(_Peer(ps, b).to(device))
+    weights, wmode = _weights(rng, n)
+    desc = "seed %d: n=%d shapes=%s lens=%s dtypes=%s weights=%s specials=%s" % (
+        seed, n, shapes, sorted(set(lens)), sorted({d for row in dts for d in row}), wmode, bool(specials))
+    return models, weights, desc
+
+
+def bits(t: torch.Tensor) -> np.ndarray:
+    dt = NAME[t.dtype]
+    tdt = {"f32": torch.int32, "bf16": torch.int16, "f16": torch.int16, "f64": torch.int64}[dt]
+    udt = {"f32": np.uint32, "bf16": np.uint16, "f16": np.uint16, "f64": np.uint64}[dt]
+    return t.detach().cpu().contiguous().reshape(-1).view(tdt).numpy().view(udt)
+
+
+def expected(models, weights):
+    """fedavg.py:14-25 per parameter of models[0] (C oracle), as [(dtype name, flat bits)]."""
+    n = len(models)
+    w = [float(1. / n) for _ in range(n)] if not weights else [float(x) for x in weights]
+    plist = [list(m.parameters()) for m in models]
+    out = []
+    for i, c in enumerate(plist[0]):
+        ks = [k for k in range(n) if len(plist[k]) > i]
+        dts = [NAME[plist[k][i].dtype] for k in ks]
+        flats = [bits(plist[k][i]) for k in ks]
+        if len(set(dts)) == 1:
+            res = c_wsum(flats, [w[k] for k in ks], dts[0]).reshape(-1)
+        else:
+            res = c_wsum_mixed(flats, dts, [w[k] for k in ks]).reshape(-1)
+        out.append((dts[0], res))
+    return out

@@ -233,6 +233,29 @@ def test_host_reduce_argument_errors(lib_path):
                          0, outs_ready=ctypes.c_int(0))
 
 
+def test_host_round_tables_must_match_their_counts(lib_path):
+    """The bindings refuse pointer / weight tables whose length differs from what the library reads
+    (n_peers x n_tensors peers, n_tensors outputs, n_peers weights) before calling it: a short table
+    would be read past its end (the round-5 fuzz found a caller passing one output for several tensors)."""
+    import numpy as np
+
+    from accdfl_amd import _lib
+
+    a = np.ones(10, dtype=np.float32)
+    buf = np.zeros(256, dtype=np.float32).ctypes.data
+    two = [a.ctypes.data, a.ctypes.data]
+    with pytest.raises(ValueError, match="output pointers for 2 tensors"):
+        _lib.host_reduce(0, 2, two * 2, [5, 5], [0.5, 0.5], [a.ctypes.data], 0, 10, 64, buf, buf, buf, buf, 0, 0)
+    with pytest.raises(ValueError, match="3 peer pointers for 1 tensors of 2 peers"):
+        _lib.host_reduce(0, 2, two + two[:1], [10], [0.5, 0.5], [a.ctypes.data], 0, 10, 64, buf, buf, buf, buf, 0, 0)
+    with pytest.raises(ValueError, match="1 weights for 2 peers"):
+        _lib.host_reduce(0, 2, two, [10], [0.5], [a.ctypes.data], 0, 10, 64, buf, buf, buf, buf, 0, 0)
+    with pytest.raises(ValueError, match="1 weights for 2 peers"):
+        _lib.host_round_start(0, 2, two, [10], [0.5], buf, 64, buf, 0)
+    with pytest.raises(ValueError, match="2 output pointers for 1 tensors"):
+        _lib.host_round_finish(0, [10], buf, [buf, buf], 0)
+
+
 class _OddModule(nn.Module):
     """Tied weights, nested containers, an LSTM (its own __setstate__ / __getstate__), buffers
     (one non-persistent), a forward hook, plain attributes sharing a dict."""

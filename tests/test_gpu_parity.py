@@ -1403,6 +1403,47 @@ def test_wsum_mixed_rejects_bad_arguments():
     with pytest.raises(_lib.DlaggError, match="aliases"):
         _lib.wsum_mixed_ptrs(_lib.DLA_F32, [_lib.DLA_F32, _lib.DLA_BF16], [a.data_ptr(), b.data_ptr()], [0.5, 0.5],
                              64, b.data_ptr(), 0)
+    # a 0-element parameter: its tensors carry null pointers, and the call is a no-op (as dla_wsum)
+    _lib.wsum_mixed_ptrs(_lib.DLA_F32, [_lib.DLA_F32, _lib.DLA_BF16], [0, 0], [0.5, 0.5], 0, 0, 0)
+    with pytest.raises(_lib.DlaggError, match="null peer pointer 1"):
+        _lib.wsum_mixed_ptrs(_lib.DLA_F32, [_lib.DLA_F32, _lib.DLA_BF16], [a.data_ptr(), 0], [0.5, 0.5], 64,
+                             a.data_ptr(), 0)
+
+
+@pytest.mark.parametrize("rows", [(0, 3), (4, 0), (0,)])
+def test_zero_element_parameters_beside_mixed_and_transposed_ones(rows):
+    """A model whose parameters include 0-element ones (data_ptr 0), a mixed-dtype one and a transposed
+    one, on the host-staged path and on the device: fedavg.py:21-25 leaves the empty ones empty (found by
+    tests/test_fuzz_fedavg.py: the mixed path refused their null pointers, and a non-dense result
+    handed dla_host_reduce one output pointer for several tensors)."""
+    from torch import nn
+
+    from accdfl_amd.core.gradient_aggregation.fedavg import FedAvg
+    from c_oracle import c_wsum_mixed
+
+    g = torch.Generator().manual_seed(5)
+
+    class M(nn.Module):
+        def __init__(self, k):
+            super().__init__()
+            self.e = nn.Parameter(torch.zeros(rows))
+            self.t = nn.Parameter(torch.randn(300, 700, generator=g).t())  # non-contiguous
+            self.m = nn.Parameter(torch.randn(1000, generator=g).to(torch.bfloat16 if k == 2 else torch.float32))
+            self.e2 = nn.Parameter(torch.zeros(rows, dtype=torch.bfloat16 if k == 1 else torch.float32))
+
+    for dev in ("cpu", "cuda"):
+        models = [M(k).to(dev) for k in range(3)]
+        w = [0.2, 0.3, 0.5]
+        out = FedAvg.aggregate(models, w)
+        torch.cuda.synchronize()
+        assert out.e.shape == rows and out.e2.shape == rows and out.e2.dtype == torch.float32
+        assert out.t.stride() == models[0].t.stride()
+        want_t = c_wsum([m.t.detach().cpu().contiguous().reshape(-1).numpy() for m in models], w, "f32")
+        assert same_bits(out.t.detach().cpu().contiguous().reshape(-1).numpy(), want_t, "f32")
+        peers = [m.m.detach().cpu() for m in models]
+        want_m = c_wsum_mixed([p.view(torch.int16).numpy().view(np.uint16) if p.dtype == torch.bfloat16
+                               else p.numpy() for p in peers], ["f32", "f32", "bf16"], w)
+        assert same_bits(out.m.detach().cpu().numpy(), want_m, "f32")
 
 
 @pytest.mark.parametrize("dtype", ["f32", "bf16"])
