@@ -519,7 +519,18 @@ def loads_state_dict(data, copy: bool = True, alloc: Optional[Callable[[int], to
         raise UnsafePayloadError("accdfl_amd: payload is not a state_dict")
     if copy:
         meta = getattr(obj, "_metadata", None)
-        obj = collections.OrderedDict((k, v.clone()) for k, v in obj.items())
+        clones = collections.OrderedDict((k, v.clone()) for k, v in obj.items())
+        storages = [v.untyped_storage().data_ptr() for v in obj.values() if v.numel()]
+        if len(set(storages)) == len(storages) and all(c.stride() == v.stride() or c.numel() == 0
+                                                       for c, v in zip(clones.values(), obj.values())):
+            obj = clones  # every tensor dense and on a storage of its own: a clone is what pickle.loads gives
+        else:
+            # entries sharing a storage (tied weights) or strided views: keep both as pickle.loads does
+            # (deepcopy copies each storage once and rebuilds every view on it)
+            import copy as _copy
+
+            del clones
+            obj = _copy.deepcopy(collections.OrderedDict(obj))
         if meta is not None:
             obj._metadata = meta
     return obj
@@ -619,17 +630,20 @@ def dumps_state_dict(state_dict: Dict[str, torch.Tensor]) -> bytes:
     reference's own bytes are not reproducible anyway: storage keys are memory addresses)."""
     big = []
     skeleton = collections.OrderedDict()
+    refs = {}  # id(entry) -> its placeholder: an entry listed twice pickles once, as pickle.dumps memoizes it
     for k, v in state_dict.items():
-        if isinstance(v, DeviceSource):
+        if id(v) in refs:
+            skeleton[k] = refs[id(v)]
+        elif isinstance(v, DeviceSource):
             if v.nbytes() >= _SENTINEL_BYTES and _BYTES_ADDR_OK:
                 token = os.urandom(_SENTINEL_BYTES)
-                skeleton[k] = _TensorRef(v.meta, token)
+                skeleton[k] = refs[id(v)] = _TensorRef(v.meta, token)
                 big.append((token, v))
             else:
                 skeleton[k] = v.to_cpu()  # small: through the CPU like any tensor
         elif torch.is_tensor(v) and v.numel() * v.element_size() >= _SENTINEL_BYTES and _owns_storage(v):
             token = os.urandom(_SENTINEL_BYTES)
-            skeleton[k] = _TensorRef(v, token)
+            skeleton[k] = refs[id(v)] = _TensorRef(v, token)
             big.append((token, v))
         else:
             skeleton[k] = v
