@@ -184,7 +184,12 @@ class DeviceModelManager(ModelManager):
         peer = WirePeer(sd)
         self.incoming_trained_models[peer_pk] = peer
         if self.slab is None:
-            self.slab = self._slab_cls.for_model(self.template, capacity=self._capacity, device=self._device)
+            try:
+                self.slab = self._slab_cls.for_model(self.template, capacity=self._capacity, device=self._device)
+            except TypeError:
+                pass  # parameters of several dtypes: no slab; the round falls back to FedAvg.aggregate
+        if self.slab is None:
+            return
         if ph is not None:
             t1 = time.perf_counter()
             ph["decode_gather_ms"].append((t1 - t0) * 1e3)

@@ -218,7 +218,12 @@ def _parse_storage_blob(blob, alloc=None) -> torch.TypedStorage:
         if alloc is not None:
             dst = alloc(nbytes)
             _gather(*span.sub(start, start + nbytes), dst)
-            data = dst.view(dtype)
+            # the storage must START at dst: dst is a slice of a larger buffer (the ingress bump
+            # allocator), whose untyped_storage() is the whole buffer — the tensor rebuilt on it
+            # (_rebuild_tensor_v2, offset 0) would read the buffer's first bytes.  A storage slice
+            # aliases dst's bytes and keeps the buffer alive.
+            a = dst.storage_offset()
+            return torch.TypedStorage(wrap_storage=dst.untyped_storage()[a:a + nbytes], dtype=dtype, _internal=True)
         else:
             data = torch.frombuffer(bytearray(span.read(start, start + nbytes)), dtype=dtype)
     else:

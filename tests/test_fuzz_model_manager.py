@@ -17,7 +17,7 @@ from oracle.fedavg_oracle import same_bits
 
 pytestmark = pytest.mark.gpu
 
-N_CASES = 32
+N_CASES = 64
 
 
 class _Net(nn.Module):

@@ -97,6 +97,21 @@ def test_wire_fuzz(seed):
             for k in sd:
                 _same(sd[k], got[k], "seed %d %s copy=%s entry %s" % (seed, name, copy, k))
             check_tie(got, "seed %d %s copy=%s: tied entries" % (seed, name, copy))
+    # a block list gathered into ONE bump-allocated buffer (the DeviceModelManager's ingress path):
+    # every gathered tensor must view its own part of the buffer
+    blocks = _blocks(rng, ref_bytes)
+    buf = torch.zeros(len(ref_bytes) + 256 * (len(sd) + 1), dtype=torch.uint8)
+    off = [0]
+
+    def alloc(nbytes):
+        a = off[0]
+        off[0] = a + (nbytes + 255) // 256 * 256
+        return buf[a:a + nbytes]
+
+    got = wire.loads_state_dict(blocks, copy=False, alloc=alloc)
+    for k in sd:
+        _same(sd[k], got[k], "seed %d blocks into one ingress buffer, entry %s" % (seed, k))
+    check_tie(got, "seed %d blocks into one ingress buffer: tied entries" % seed)
     ours = wire.dumps_state_dict(sd)
     for name, got in (("pickle.loads", pickle.loads(ours)), ("wire", wire.loads_state_dict(ours))):
         assert list(got) == list(sd), (seed, name)

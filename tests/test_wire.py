@@ -103,6 +103,42 @@ def test_device_model_manager_wire_round():
         assert same_bits(back[name].numpy(), want[name].numpy(), "f32"), name
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("block", [4096, 60_000])
+def test_multi_tensor_eva_blocks_into_the_slab(block):
+    """Peers of a many-tensor model (a GNLeNet-sized layout) arriving as EVA block lists: every tensor
+    that crosses a block is gathered into the peer's ONE page-locked ingress buffer, each at its own
+    offset, and must be read from there (round 5's fuzz found every gathered tensor after the first
+    viewing the buffer's first bytes).  The round against the C oracle, bit for bit."""
+    from types import SimpleNamespace
+
+    from accdfl_amd.core import wire
+    from accdfl_amd.core.gradient_aggregation import GradientAggregationMethod
+    from accdfl_amd.core.model_manager import DeviceModelManager
+    from c_oracle import c_wsum
+
+    shapes = [(32, 3, 5, 5), (32,), (32, 32, 5, 5), (32,), (64, 32, 5, 5), (64,), (10, 1024), (10,)]
+
+    class Net(nn.Module):
+        def __init__(self, seed):
+            super().__init__()
+            g = torch.Generator().manual_seed(seed)
+            for i, s in enumerate(shapes):
+                setattr(self, "p%d" % i, nn.Parameter(torch.randn(s, generator=g)))
+
+    models = [Net(k) for k in range(5)]
+    mm = DeviceModelManager(None, SimpleNamespace(gradient_aggregation=GradientAggregationMethod.FEDAVG),
+                            template=Net(99), capacity=2)
+    for k, m in enumerate(models):
+        data = wire.serialize_model(m)
+        mm.process_incoming_serialized(b"peer%d" % k, [data[i:i + block] for i in range(0, len(data), block)])
+    weights = [0.1, 0.2, 0.3, 0.25, 0.15]
+    out = mm.aggregate_trained_models(weights)
+    for i, p in enumerate(out.parameters()):
+        want = c_wsum([list(m.parameters())[i].detach().reshape(-1).numpy() for m in models], weights, "f32")
+        assert same_bits(p.detach().reshape(-1).numpy(), want, "f32"), "parameter %d" % i
+
+
 def test_device_source_entries_encode_like_tensors():
     """wire.DeviceSource (aggregate_serialized's parameter entries): small entries go through the CPU
     like any tensor, so a state dict whose entries are slices of one flat tensor encodes to exactly
