@@ -155,3 +155,42 @@ def expected(models, weights):
             res = c_wsum_mixed(flats, dts, [w[k] for k in ks]).reshape(-1)
         out.append((dts[0], res))
     return out
+
+
+N_LARGE = 12
+
+
+def make_large_case(seed: int):
+    """(models, weights, description): a CPU round above the small-round bound (>= 48 MiB of input), so
+    FedAvg.aggregate streams it through dla_host_reduce in element chunks that cut across tensors:
+    2-16 models of 1-6 parameters, 3-24 M elements each, one dtype, some peers page-locked, now and
+    then a transposed parameter (the general host-staged path) or a shorter model (zip truncation)."""
+    rng = np.random.default_rng(104_729 * seed + 5)
+    n = int([2, 3, 4, 8, 9, 16][rng.integers(6)])
+    dt = ["f32", "bf16", "f16", "f64", "f32"][rng.integers(5)]
+    es = {"f32": 4, "bf16": 2, "f16": 2, "f64": 8}[dt]
+    total = min(int(rng.integers(3_000_000, 24_000_000)), 80_000_000 // n)  # <= 80 M peer elements per case
+    total = max(total, (56 << 20) // (n * es))  # above the 48 MiB small-round bound
+    n_params = int(rng.integers(1, 7))
+    cuts = np.sort(rng.choice(np.arange(1, total), size=n_params - 1, replace=False)) if n_params > 1 else []
+    numels = np.diff(np.concatenate([[0], cuts, [total]])).astype(int).tolist()
+    transposed = rng.integers(0, 5) == 0
+    trunc = rng.integers(0, 5) == 0 and n_params > 1
+    pinned = [bool(rng.integers(0, 3) == 0) for _ in range(n)]
+    models = []
+    for k in range(n):
+        ps = []
+        for i, m in enumerate(numels):
+            if trunc and k == n - 1 and i == n_params - 1:
+                break
+            t = _values(rng, m, dt, specials=(seed % 3 == 0))
+            if pinned[k]:
+                t = t.pin_memory()
+            if transposed and i == 0 and m % 2 == 0:
+                t = t.view(2, m // 2).t()
+            ps.append(nn.Parameter(t))
+        models.append(_Peer(ps))
+    weights = [float(x) for x in rng.dirichlet(np.ones(n))] if rng.integers(0, 3) else None
+    desc = "large seed %d: n=%d %s numels=%s transposed=%s truncated=%s pinned=%s" % (
+        seed, n, dt, numels, bool(transposed), bool(trunc), pinned)
+    return models, weights, desc

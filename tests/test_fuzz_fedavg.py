@@ -108,3 +108,20 @@ def test_fedavg_fuzz_case_matches_oracle(seed, where):
     after = _snapshot(models)
     for k, (x, y) in enumerate(zip(before, after)):
         assert all(np.array_equal(a, b) for a, b in zip(x, y)), "%s: model %d changed" % (desc, k)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(fz.N_LARGE))
+def test_fedavg_large_host_round_fuzz(seed):
+    """Rounds above the small-round bound through the chunked host paths (fuzz_cases.make_large_case)."""
+    from accdfl_amd.core.gradient_aggregation.fedavg import FedAvg
+
+    models, weights, desc = fz.make_large_case(seed)
+    want = fz.expected(models, weights)
+    out = FedAvg.aggregate(models, weights)
+    got = list(out.parameters())
+    ref = list(models[0].parameters())
+    assert len(got) == len(want), desc
+    for i, (g, r, (d, w)) in enumerate(zip(got, ref, want)):
+        assert g.device.type == "cpu" and g.shape == r.shape and g.stride() == r.stride(), "%s: parameter %d" % (desc, i)
+        assert same_bits(fz.bits(g), w, d), "%s: parameter %d" % (desc, i)
