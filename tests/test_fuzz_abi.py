@@ -168,3 +168,30 @@ def test_slab_stage_and_tiled_reduce_fuzz(seed):
     want = c_wsum([_bits(h, dt) for h in hosts], w, dt)
     assert same_bits(_bits(out, dt), want, dt), \
         "seed %d: %s rows=%d n=%d numel=%d tile=%d" % (seed, dt, rows, n, numel, tile)
+
+
+@pytest.mark.parametrize("seed", range(N_CASES // 2))
+def test_mean_fuzz(seed):
+    """dla_mean (scripts/distill.py:124-129's teacher-logit mean): (((+0 + p_0) + p_1) + ... ) / N in
+    the storage type, correctly rounded division, peers and out at random offsets, out aliasing
+    peers[0] across 128-peer passes; against numpy's sequential sum and IEEE division."""
+    from accdfl_amd import _lib
+
+    rng = np.random.default_rng(6000 + seed)
+    dt = ["f32", "f64"][rng.integers(2)]
+    n = int(_PEERS[rng.integers(len(_PEERS))])
+    numel = min(int([1, 3, 64, 1000, 4097, 65_537, 300_001][rng.integers(7)]), _BUDGET // n)
+    hosts = [_host(rng, numel, dt, rng.integers(0, 3) == 0) for _ in range(n)]
+    peers = [_Placed(h, int(rng.integers(0, 4)) if rng.integers(0, 2) else 0) for h in hosts]
+    alias = rng.integers(0, 3) == 0
+    out = peers[0] if alias else _Placed(torch.zeros(numel, dtype=TDT[dt]), int(rng.integers(0, 4)))
+    npdt = np.float32 if dt == "f32" else np.float64
+    acc = np.zeros(numel, dtype=npdt)
+    with np.errstate(all="ignore"):
+        for h in hosts:
+            acc = acc + h.numpy().astype(npdt)
+        want = (acc / npdt(n)).view(UDT[dt])
+    _lib.mean_ptrs(CODE[dt], [p.ptr for p in peers], numel, out.ptr, torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert same_bits(_bits(out.view(), dt), want, dt), "seed %d: %s n=%d numel=%d alias=%s" % (seed, dt, n, numel,
+                                                                                              alias)

@@ -125,3 +125,41 @@ def test_fedavg_large_host_round_fuzz(seed):
     for i, (g, r, (d, w)) in enumerate(zip(got, ref, want)):
         assert g.device.type == "cpu" and g.shape == r.shape and g.stride() == r.stride(), "%s: parameter %d" % (desc, i)
         assert same_bits(fz.bits(g), w, d), "%s: parameter %d" % (desc, i)
+
+
+@pytest.mark.gpu
+def test_concurrent_device_rounds_from_threads():
+    """Four threads, each on a stream of its own, run fuzz rounds of device models back to back with no
+    host synchronisation between their rounds: the table ring (8 slots, one event per 4 calls) and the
+    upload policy are shared by every thread.  Every round's result against the C oracle afterwards."""
+    import threading
+
+    from accdfl_amd.core.gradient_aggregation.fedavg import FedAvg
+
+    seeds = [s for s in SEEDS if len(fz.make_case(s)[0]) >= 33][:6]
+    cases = [fz.make_case(s, device="cuda:0") for s in seeds]
+    wants = [fz.expected(m, w) for m, w, _ in cases]
+    results, errors = [], []
+
+    def worker(t):
+        try:
+            s = torch.cuda.Stream()
+            with torch.cuda.stream(s):
+                for r in range(12):
+                    c = (t + r) % len(cases)
+                    models, weights, _ = cases[c]
+                    results.append((c, FedAvg.aggregate(models, weights), s))
+        except Exception as e:  # noqa: BLE001  (re-raised below)
+            errors.append(e)
+
+    threads = [threading.Thread(target=worker, args=(t,)) for t in range(4)]
+    for th in threads:
+        th.start()
+    for th in threads:
+        th.join(timeout=120)
+    assert not errors, errors[0]
+    torch.cuda.synchronize()
+    assert len(results) == 48
+    for c, out, _ in results:
+        for i, (g, (d, w)) in enumerate(zip(out.parameters(), wants[c])):
+            assert same_bits(fz.bits(g), w, d), "%s: parameter %d" % (cases[c][2], i)

@@ -202,3 +202,25 @@ def _run_sharded(world, n_peers, n_elems, reducer, dtype="f32"):
             err = np.abs(res["rs"].astype(np.float64) - want.view(np.float32).astype(np.float64))
             assert np.all(err <= bound + 1e-45), "reduce-scatter mode rank %d: max err %g" % (rank, err.max())
     assert covered == n_elems
+
+
+def test_bucket_bounds_properties_fuzz():
+    """bucket_bounds over 2 000 seeded (n_elems, world, alignment) draws: the buckets tile [0, n_elems)
+    in rank order with no gap or overlap, every non-empty bucket starts on the alignment, and no
+    bucket exceeds the ceil-divided, aligned share."""
+    from accdfl_amd.core.sharding import bucket_bounds
+
+    rng = np.random.default_rng(11)
+    for _ in range(2000):
+        n = int(rng.choice([0, 1, 7, 63, 64, 65, 1000, 4099, 21_296_355, int(rng.integers(0, 1 << 26))]))
+        world = int(rng.integers(1, 17))
+        align = int(rng.choice([1, 16, 32, 64, 128]))
+        b = bucket_bounds(n, world, align)
+        assert len(b) == world
+        assert b[0][0] == 0 and b[-1][1] == n
+        for (s0, e0), (s1, e1) in zip(b, b[1:]):
+            assert e0 == s1 and s0 <= e0
+        share = -(-(-(-n // world) if n else 0) // align) * align
+        for s, e in b:
+            assert s <= e and e - s <= share
+            assert s == e or s % align == 0
