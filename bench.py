@@ -1327,6 +1327,69 @@ def dfl_round(msgs, p, device, reps=3):
                     "-> reduce -> D2H into the pooled result -> serialize_model bytes"}
 
 
+def dfl_round_layout(name, n, dt, device, reps=3):
+    """§8 f1-f3 on a real many-tensor layout: the DFL aggregator round of ``n`` models of ``name``
+    (e.g. configs[4]'s google_speech ResNet-34, 110 parameter tensors and 108 BN buffers in bf16)
+    arriving as EVA blocks of their serialize_model bytes — most tensors cross the 60 000-byte blocks,
+    so each is gathered into the peer's page-locked ingress buffer at its own offset and sent to its
+    PeerSlab tiles — then the average as serialize_model bytes straight from HBM
+    (aggregate_serialized).  ``parity_ok``: every parameter of the decoded payload equals
+    FedAvg.aggregate on the same modules (the device path, no wire), bit for bit."""
+    import pickle
+    from types import SimpleNamespace
+
+    from accdfl_amd.core import wire
+    from accdfl_amd.core.gradient_aggregation import GradientAggregationMethod
+    from accdfl_amd.core.gradient_aggregation.fedavg import FedAvg
+    from accdfl_amd.core.model_manager import DeviceModelManager
+
+    models, p = _layout_models(name, n, dt, pinned=False, seed=4200)
+    view = pickle.dumps({"peer%d" % j: j for j in range(16)})
+    msgs = []
+    for m in models:
+        mb = wire.serialize_model(m)
+        msgs.append((wire.payload_blocks(mb + view, EVA_BLOCK), len(mb)))
+    mm = DeviceModelManager(None, SimpleNamespace(gradient_aggregation=GradientAggregationMethod.FEDAVG), 0,
+                            capacity=n, template=models[0], device=device)
+    w = [float(x) for x in np.random.default_rng(n).dirichlet(np.ones(n))]
+
+    def one():
+        mm.reset_incoming_trained_models()
+        t0 = time.perf_counter()
+        for k, (blocks, ml) in enumerate(msgs):
+            head, _ = wire.split_blocks(blocks, ml)
+            mm.process_incoming_serialized(b"peer%d" % k, head)
+        t1 = time.perf_counter()
+        mm.slab.copy_stream.synchronize()
+        t2 = time.perf_counter()
+        data = mm.aggregate_serialized(w)
+        t3 = time.perf_counter()
+        return (t1 - t0, t2 - t0, t3 - t2, t3 - t0), data
+
+    one()
+    runs = [one() for _ in range(reps)]
+    med = [statistics.median(r[0][i] for r in runs) for i in range(4)]
+    got = wire.loads_state_dict(runs[-1][1])
+    dev_models = [m.to(device) for m in models]
+    want = FedAvg.aggregate(dev_models, w)
+    torch.cuda.synchronize()
+    names = [k for k, _ in want.named_parameters()]
+    ok = all(torch.equal(got[k].view(torch.int16 if dt != torch.float32 else torch.int32),
+                         v.detach().cpu().view(torch.int16 if dt != torch.float32 else torch.int32))
+             for k, v in zip(names, want.parameters()))
+    in_bytes = n * p * torch.empty((), dtype=dt).element_size()
+    n_cross = sum(1 for s in _layout(name)[0] if int(np.prod(s) if s else 1) * torch.empty((), dtype=dt).element_size()
+                  >= EVA_BLOCK)
+    return {"layout": name, "peers": n, "params": p, "parameter_tensors": len(names), "dtype": str(dt),
+            "eva_block_bytes": EVA_BLOCK, "tensors_of_at_least_one_block": n_cross,
+            "ingress_ms": round(med[0] * 1e3, 2), "ingress_complete_ms": round(med[1] * 1e3, 2),
+            "ingress_GBps": round(in_bytes / med[1] / 1e9, 2),
+            "aggregate_serialized_ms": round(med[2] * 1e3, 2), "round_ms": round(med[3] * 1e3, 2),
+            "parity_ok": bool(ok),
+            "parity": "every parameter of the decoded aggregate_serialized payload == FedAvg.aggregate on the same "
+                      "modules on the device (no wire), bit for bit"}
+
+
 def dfl_round_reference_style(msgs, p, reps=2):
     """The same round the way the reference runs it, on this host's CPU: b''.join of the EVA
     blocks (accdfl/util/eva/transfer/incoming.py:35), the model_data_len slice
@@ -2067,6 +2130,10 @@ def main():
                 msgs = dfl_messages(n, p)
                 return dfl_round(msgs, p, device)
             result["dfl_round"] = legs.run("dfl_round", dfl)
+            result["dfl_round_layout"] = legs.run(
+                "dfl_round_layout", lambda L: dfl_round_layout("google_speech_resnet34", 16, torch.bfloat16, device))
+            parity["dfl_round_layout (wire ingress of 110 tensors == device FedAvg)"] = \
+                result["dfl_round_layout"].get("parity_ok")
         if not args.no_cpu_baseline and args.dtype == "f32":
             result["cpu_baseline"] = legs.run("cpu_baseline",
                                               lambda L: cpu_baseline_all(args, result, n, p, headline_host),
