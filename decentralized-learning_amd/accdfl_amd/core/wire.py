@@ -296,6 +296,9 @@ class _BlockReader:
         self.views = [None] * len(self.blocks)
         self.pos = 0
         self.n = int(lens.sum())
+        # the block the last read ended in: (its view, its start, its end) — most reads (the pickle's
+        # opcodes and their arguments) fall inside it and skip the bisection
+        self.cur = (b"", 0, 0)
 
     @property
     def left(self) -> int:
@@ -309,9 +312,13 @@ class _BlockReader:
 
     def take(self, k: int):
         a = self.pos
+        b = a + k
+        v, s0, e0 = self.cur
+        if s0 <= a and b <= e0:  # inside the current block
+            self.pos = b
+            return v[a - s0:b - s0]
         if k > self.n - a:
             raise UnsafePayloadError("truncated payload")
-        b = a + k
         self.pos = b
         if k == 0:
             return b""
@@ -319,8 +326,11 @@ class _BlockReader:
         i = bisect.bisect_right(st, a) - 1
         o = a - st[i]
         if o + k <= lens[i]:
-            return self._view(i)[o:o + k]
+            v = self._view(i)
+            self.cur = (v, st[i], st[i] + lens[i])
+            return v[o:o + k]
         j = bisect.bisect_right(st, b - 1) - 1
+        self.cur = (self._view(j), st[j], st[j] + lens[j])  # the next read starts in block j (or after it)
         if k <= 4096:  # a short read across a block boundary: joined
             pieces = [self._view(i)[o:]]
             pieces += [self._view(q) for q in range(i + 1, j)]
