@@ -121,14 +121,24 @@ def make_case(seed: int, device="cpu"):
         lens[0] = int(rng.integers(1, n_params + 1))  # models[0] shorter than others
     specials = rng.integers(0, 4) == 0
     buf = rng.integers(0, 3) == 0
+    # tied parameters (one Parameter under two names: parameters() lists it once, fedavg.py:21/24), drawn
+    # from a generator of their own so the other draws of the case stay as they were
+    trng = np.random.default_rng(seed + 99_991)
+    tie = None
+    if n_params > 1 and trng.integers(0, 6) == 0:
+        i, j = sorted(int(x) for x in trng.choice(n_params, size=2, replace=False))
+        tie = (i, j, [True] * n)  # every model: tying only some would misalign their parameter lists
     models = []
     for k in range(n):
         ps = [_param(rng, shapes[i], dts[k][i], transposed[i], specials) for i in range(lens[k])]
+        if tie is not None and tie[2][k] and lens[k] > tie[1]:
+            ps[tie[1]] = ps[tie[0]]
         b = torch.full((3,), float(k)) if buf else None
         models.append(_Peer(ps, b).to(device))
     weights, wmode = _weights(rng, n)
-    desc = "seed %d: n=%d shapes=%s lens=%s dtypes=%s weights=%s specials=%s" % (
-        seed, n, shapes, sorted(set(lens)), sorted({d for row in dts for d in row}), wmode, bool(specials))
+    desc = "seed %d: n=%d shapes=%s lens=%s dtypes=%s weights=%s specials=%s tie=%s" % (
+        seed, n, shapes, sorted(set(lens)), sorted({d for row in dts for d in row}), wmode, bool(specials),
+        None if tie is None else tie[:2])
     return models, weights, desc
 
 

@@ -68,13 +68,15 @@ def test_fuzz_cases_cover_the_contract():
         if len(models) > 128:
             seen.add("two passes")
         seen.add("weights=" + desc.split("weights=")[1].split(" specials=")[0])
+        if "tie=None" not in desc:
+            seen.add("tied")
         if "specials=True" in desc:
             seen.add("specials")
         if list(models[0].buffers()):
             seen.add("buffer")
     want = {"f32", "bf16", "f16", "f64", "mixed", "truncation", "empty model", "transposed", "0 elements", "0-d",
             "two passes", "weights=none", "weights=dirichlet", "weights=signed", "weights=ints",
-            "weights=np.float32", "weights=0-d tensors", "weights=special", "specials", "buffer"}
+            "weights=np.float32", "weights=0-d tensors", "weights=special", "specials", "buffer", "tied"}
     assert want <= seen, sorted(want - seen)
 
 

@@ -41,8 +41,10 @@ def _layout(rng):
     return [fz._shape_of(rng, m) for m in numels], dts, bool(rng.integers(0, 3) == 0)
 
 
-def _model(rng, shapes, dts, buf, k, specials):
+def _model(rng, shapes, dts, buf, k, specials, tie=None):
     ps = [nn.Parameter(fz._values(rng, int(np.prod(s)) if s else 1, d, specials).view(s)) for s, d in zip(shapes, dts)]
+    if tie is not None:  # one Parameter under two names: parameters() lists it once, state_dict() twice
+        ps[tie[1]] = ps[tie[0]]
     return _Net(ps, torch.full((4,), float(k)) if buf else None)
 
 
@@ -69,12 +71,15 @@ def test_device_model_manager_fuzz(seed):
     rng = np.random.default_rng(4000 + seed)
     shapes, dts, buf = _layout(rng)
     specials = rng.integers(0, 4) == 0
-    template = _model(rng, shapes, dts, buf, -1, False)
+    trng = np.random.default_rng(seed + 77_777)  # ties drawn apart: the case's other draws are unchanged
+    tie = tuple(sorted(int(x) for x in trng.choice(len(shapes), 2, replace=False))) \
+        if len(shapes) > 1 and trng.integers(0, 5) == 0 else None
+    template = _model(rng, shapes, dts, buf, -1, False, tie)
     mm = DeviceModelManager(None, SimpleNamespace(gradient_aggregation=GradientAggregationMethod.FEDAVG), 0,
                             capacity=int(rng.integers(1, 9)), template=template)
     for rnd in range(2):
         n = int([1, 2, 3, 5, 8, 9, 16, 17, 40][rng.integers(9)])
-        models = [_model(rng, shapes, dts, buf, k, specials) for k in range(n)]
+        models = [_model(rng, shapes, dts, buf, k, specials, tie) for k in range(n)]
         how = []
         for k, m in enumerate(models):
             mode = int(rng.integers(0, 5))
@@ -90,10 +95,11 @@ def test_device_model_manager_fuzz(seed):
                 payload = data if mode == 2 else memoryview(data) if mode == 3 else _blocks(rng, data)
                 mm.process_incoming_serialized(key, payload)
             if k == 0 and rng.integers(0, 2):  # a re-send of peer 0 with other values: ignored
-                mm.process_incoming_trained_model(key, _model(rng, shapes, dts, buf, 99, False))
+                mm.process_incoming_trained_model(key, _model(rng, shapes, dts, buf, 99, False, tie))
         weights = None if rng.integers(0, 3) == 0 else [float(x) for x in rng.dirichlet(np.ones(n))]
         want = fz.expected(models, weights)
-        desc = "seed %d round %d: n=%d shapes=%s dtypes=%s arrivals=%s" % (seed, rnd, n, shapes, sorted(set(dts)), how)
+        desc = "seed %d round %d: n=%d shapes=%s dtypes=%s arrivals=%s tie=%s" % (seed, rnd, n, shapes, sorted(set(dts)),
+                                                                           how, tie)
         out = mm.aggregate_trained_models(weights)
         torch.cuda.synchronize()
         _check(list(out.parameters()), want, desc)
@@ -101,7 +107,10 @@ def test_device_model_manager_fuzz(seed):
             assert torch.equal(out.stat.cpu(), torch.full((4,), 0.0)), desc  # models[0]'s buffer (:20)
         payload = mm.aggregate_serialized(weights)
         sd = wire.loads_state_dict(payload)
-        _check([sd["p%d" % i] for i in range(len(shapes))], want, desc + " (aggregate_serialized)")
+        names = [nm for nm, _ in out.named_parameters()]  # tied: the first name of each parameter
+        _check([sd[nm] for nm in names], want, desc + " (aggregate_serialized)")
+        if tie is not None:  # the alias carries the same average
+            _check([sd["p%d" % tie[1]]], [want[names.index("p%d" % tie[0])]], desc + " (tied alias)")
         if buf:
             assert torch.equal(sd["stat"].cpu(), torch.full((4,), 0.0)), desc
         mm.reset_incoming_trained_models()
