@@ -224,3 +224,21 @@ def test_bucket_bounds_properties_fuzz():
         for s, e in b:
             assert s <= e and e - s <= share
             assert s == e or s % align == 0
+
+
+def _random_sharding_cases(k=4, seed=29):
+    rng = np.random.default_rng(seed)
+    out = []
+    for _ in range(k):
+        world = int(rng.choice([2, 3, 4, 5, 8]))
+        n_peers = int(rng.choice([3, 7, 16, 40, 128, 130]))
+        out.append((world, n_peers, int(rng.integers(1, 300_000)), str(rng.choice(["f32", "bf16"]))))
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,n_peers,n_elems,dtype", _random_sharding_cases())
+def test_sharded_fedavg_hip_reducer_random_shapes(world, n_peers, n_elems, dtype):
+    """Seeded random world sizes, peer counts and lengths (ragged and empty trailing buckets, one and two
+    kernel passes) through the bucket-sharded and peer-sharded exchanges with the libdlagg reducer."""
+    _run_sharded(world, n_peers, n_elems, "hip", dtype)
