@@ -242,3 +242,9 @@ def test_sharded_fedavg_hip_reducer_random_shapes(world, n_peers, n_elems, dtype
     """Seeded random world sizes, peer counts and lengths (ragged and empty trailing buckets, one and two
     kernel passes) through the bucket-sharded and peer-sharded exchanges with the libdlagg reducer."""
     _run_sharded(world, n_peers, n_elems, "hip", dtype)
+
+
+@pytest.mark.parametrize("world,n_peers,n_elems,dtype", _random_sharding_cases(k=2, seed=31))
+def test_sharded_fedavg_random_shapes(world, n_peers, n_elems, dtype):
+    """The same seeded random shapes on the CPU (the NumPy oracle as each rank's bucket reducer)."""
+    _run_sharded(world, n_peers, min(n_elems, 50_000), "oracle", dtype)
