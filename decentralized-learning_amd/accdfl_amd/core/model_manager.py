@@ -25,6 +25,11 @@ from accdfl_amd.core import wire
 from accdfl_amd.core.gradient_aggregation.fedavg import FedAvg, _center_copy
 
 
+def _one_dtype(model: nn.Module) -> bool:
+    """The model's parameters share one dtype (what a PeerSlab row holds)."""
+    return len({p.dtype for p in model.parameters()}) == 1
+
+
 class ModelManager:
     """Holds received peer models and aggregates them (model_manager.py:20-58)."""
 
@@ -123,14 +128,13 @@ class DeviceModelManager(ModelManager):
         if peer_pk in self.incoming_trained_models:
             return
         self.incoming_trained_models[peer_pk] = incoming_model
-        try:
-            if self.slab is None:
-                self.slab = self._slab_cls.for_model(incoming_model, capacity=self._capacity, device=self._device)
-            if self.slab.matches(list(incoming_model.parameters())) and len(self._staged) == self.slab.n:
-                self.slab.stage(incoming_model)
-                self._staged.append((peer_pk, incoming_model, self._fingerprint(incoming_model)))
-        except TypeError:
-            pass  # mixed-dtype model: the round falls back to FedAvg.aggregate (_uniform is False)
+        if self.slab is None:
+            if not _one_dtype(incoming_model):
+                return  # mixed-dtype model: the round falls back to FedAvg.aggregate (_uniform is False)
+            self.slab = self._slab_cls.for_model(incoming_model, capacity=self._capacity, device=self._device)
+        if self.slab.matches(list(incoming_model.parameters())) and len(self._staged) == self.slab.n:
+            self.slab.stage(incoming_model)
+            self._staged.append((peer_pk, incoming_model, self._fingerprint(incoming_model)))
 
     def _ingress_alloc(self, pos: int, nbytes: int):
         """Bump allocator over registry position ``pos``'s page-locked ingress buffer (grown to
@@ -183,16 +187,14 @@ class DeviceModelManager(ModelManager):
         params = wire.parameter_tensors(sd, self.template)
         peer = WirePeer(sd)
         self.incoming_trained_models[peer_pk] = peer
-        if self.slab is None:
-            try:
-                self.slab = self._slab_cls.for_model(self.template, capacity=self._capacity, device=self._device)
-            except TypeError:
-                pass  # parameters of several dtypes: no slab; the round falls back to FedAvg.aggregate
-        if self.slab is None:
-            return
         if ph is not None:
             t1 = time.perf_counter()
             ph["decode_gather_ms"].append((t1 - t0) * 1e3)
+        if self.slab is None and _one_dtype(self.template):
+            self.slab = self._slab_cls.for_model(self.template, capacity=self._capacity, device=self._device)
+        if self.slab is None:
+            return  # parameters of several dtypes: no slab; the round falls back to FedAvg.aggregate
+        if ph is not None:
             e0 = torch.cuda.Event(enable_timing=True)
             e0.record(self.slab.copy_stream)
         if self.slab.matches(params) and len(self._staged) == self.slab.n:

@@ -536,8 +536,12 @@ def loads_state_dict(data, copy: bool = True, alloc: Optional[Callable[[int], to
         meta = getattr(obj, "_metadata", None)
         clones = collections.OrderedDict((k, v.clone()) for k, v in obj.items())
         storages = [v.untyped_storage().data_ptr() for v in obj.values() if v.numel()]
-        if len(set(storages)) == len(storages) and all(c.stride() == v.stride() or c.numel() == 0
-                                                       for c, v in zip(clones.values(), obj.values())):
+        # a clone is exact only for a tensor that is the whole of its own storage: same strides, offset 0,
+        # and the storage no larger than the tensor (pickle.loads keeps a view's storage and offset)
+        if len(set(storages)) == len(storages) and all(
+                c.numel() == 0 or (c.stride() == v.stride() and v.storage_offset() == 0
+                                   and v.untyped_storage().nbytes() == v.numel() * v.element_size())
+                for c, v in zip(clones.values(), obj.values())):
             obj = clones  # every tensor dense and on a storage of its own: a clone is what pickle.loads gives
         else:
             # entries sharing a storage (tied weights) or strided views: keep both as pickle.loads does
@@ -655,7 +659,8 @@ def dumps_state_dict(state_dict: Dict[str, torch.Tensor]) -> bytes:
                 skeleton[k] = refs[id(v)] = _TensorRef(v.meta, token)
                 big.append((token, v))
             else:
-                skeleton[k] = v.to_cpu()  # small: through the CPU like any tensor
+                # small: through the CPU like any tensor, once (an entry listed twice stays one tensor)
+                skeleton[k] = refs[id(v)] = v.to_cpu()
         elif torch.is_tensor(v) and v.numel() * v.element_size() >= _SENTINEL_BYTES and _owns_storage(v):
             token = os.urandom(_SENTINEL_BYTES)
             skeleton[k] = refs[id(v)] = _TensorRef(v, token)

@@ -2649,6 +2649,14 @@ int multi_table_impl(int dtype, int n_tensors, const void* const* peer_ptrs, voi
   if (!is_device_ptr(table_dev)) return fail(DLA_E_INVALID, "dla_wsum_multi_table: table_dev must be device memory");
   if ((reinterpret_cast<uintptr_t>(table_host) & 15u) || (reinterpret_cast<uintptr_t>(table_dev) & 15u))
     return fail(DLA_E_INVALID, "dla_wsum_multi_table: table buffers must be 16-byte aligned");
+  // The table's upload keys its side stream, its event and the mapped-table check on the current device:
+  // make that the device holding table_dev (the reduce's device) for this call, whatever the caller had
+  // current (models reduced on cuda:1 while device 0 is current).
+  DeviceGuard guard;
+  const int tdev = owner_device(table_dev);
+  int cur = -1;
+  if (tdev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != tdev && hipSetDevice(tdev) != hipSuccess)
+    return fail(DLA_E_INVALID, "dla_wsum_multi_table: cannot select the table's device " + std::to_string(tdev));
   hipStream_t s = static_cast<hipStream_t>(stream);
   char* th = static_cast<char*>(table_host);
   char* td = static_cast<char*>(table_dev);

@@ -178,7 +178,13 @@ int dla_wsum_multi(int dtype, int n_tensors, const void* const* peer_ptrs, void*
  * models: 14 080 tensors, 1 launch; dla_wsum_multi: 110).  Other tensors (unaligned, F64) take the
  * per-tensor path.  Same arguments and arithmetic as dla_wsum_multi; outs[t] may alias tensor t of
  * peer 0.  The caller leaves table_host and table_dev untouched until the stream has passed this
- * work (e.g. an event recorded after the call).  ABI v8. */
+ * work (e.g. an event recorded after the call).  ABI v8.
+ * Blocking: the side-stream upload makes the CALLING THREAD wait for the table copy (~15-20 us) before
+ * the reduce is enqueued.  The library takes that branch only when the call moves >= 256 MiB and its
+ * own estimate (the algorithmic bytes of the table reduces it queued on `stream` at ~6 TB/s) says the
+ * stream is still busy; work on `stream` from anyone else is not seen by the estimate, so on a stream
+ * that also carries e.g. training kernels the call may block for the copy while those run.  Otherwise
+ * the call never blocks.  The table's device (table_dev's) is made current for the call and restored. */
 int64_t dla_wsum_multi_table_bytes(int n_tensors, int n_peers);
 int dla_wsum_multi_table(int dtype, int n_tensors, const void* const* peer_ptrs, void* const* outs,
                          const int64_t* numels, const double* weights, int n_peers, void* table_host,

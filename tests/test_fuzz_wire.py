@@ -51,6 +51,8 @@ def _tensor(rng, dtype):
         return t[:, 1::2]                 # strided slice with a storage offset
     if form == 2 and dims == 3 and t.shape[1] % 2 == 0:
         return t.view(r, 2, -1)
+    if form == 3 and t.shape[0] > 1:
+        return t[1:]                      # contiguous, but a storage offset and a larger storage
     return t
 
 
@@ -89,13 +91,18 @@ def test_wire_fuzz(seed):
             assert got["tied"].untyped_storage().data_ptr() == got[tied].untyped_storage().data_ptr(), ctx
 
     ref_bytes = pickle.dumps(sd)  # the reference's serialize_model
+    ref = pickle.loads(ref_bytes)  # the reference's decode: views keep their storage and offset
     for name, payload in (("bytes", ref_bytes), ("memoryview", memoryview(ref_bytes)),
                           ("blocks", _blocks(rng, ref_bytes))):
         for copy in (True, False):
             got = wire.loads_state_dict(payload, copy=copy)
             assert list(got) == list(sd), (seed, name)
             for k in sd:
-                _same(sd[k], got[k], "seed %d %s copy=%s entry %s" % (seed, name, copy, k))
+                ctx = "seed %d %s copy=%s entry %s" % (seed, name, copy, k)
+                _same(sd[k], got[k], ctx)
+                if copy and ref[k].numel():
+                    assert got[k].storage_offset() == ref[k].storage_offset(), ctx
+                    assert got[k].untyped_storage().nbytes() == ref[k].untyped_storage().nbytes(), ctx
             check_tie(got, "seed %d %s copy=%s: tied entries" % (seed, name, copy))
     # a block list gathered into ONE bump-allocated buffer (the DeviceModelManager's ingress path):
     # every gathered tensor must view its own part of the buffer
@@ -118,3 +125,17 @@ def test_wire_fuzz(seed):
         for k in sd:
             _same(sd[k], got[k], "seed %d dumps_state_dict -> %s entry %s" % (seed, name, k))
         check_tie(got, "seed %d dumps_state_dict -> %s: tied entries" % (seed, name))
+
+
+@pytest.mark.parametrize("numel", [1, 5, 1000])
+def test_tied_device_source_pickles_once(numel):
+    """One small DeviceSource (< 64 KiB: encoded through the CPU) listed under two keys (a tied parameter
+    of the averaged model): pickle.dumps of the equivalent dict ties the two entries, so the payload must
+    too.  (The large, out-of-band form is memoized by its placeholder and covered on the GPU.)"""
+    flat = torch.arange(numel + 3, dtype=torch.float32)
+    src = wire.DeviceSource(flat, 3, (numel,))
+    sd = OrderedDict([("a", src), ("b", src), ("c", torch.ones(2))])
+    got = pickle.loads(wire.dumps_state_dict(sd))
+    assert list(got) == ["a", "b", "c"]
+    assert torch.equal(got["a"], flat[3:]) and torch.equal(got["b"], flat[3:])
+    assert got["a"].untyped_storage().data_ptr() == got["b"].untyped_storage().data_ptr()

@@ -143,26 +143,63 @@ def test_sharded_peers_freed_right_after_across_gpus():
     _freed_peers_case([torch.device("cuda", 0), torch.device("cuda", 1)], torch.device("cuda", 1))
 
 
-@pytest.mark.skipif(torch.cuda.device_count() < 2, reason="needs two GPUs (xGMI peer reads)")
-def test_models_on_two_gpus_through_fedavg():
-    """Peers really on two GPUs: FedAvg.aggregate takes the sharded multi-device path (peer
-    access over xGMI) and matches the oracle bit for bit."""
+@pytest.mark.parametrize("n_gpus", [2, 4, 8])
+def test_models_on_several_gpus_through_fedavg(n_gpus):
+    """Peers really on 2 / 4 / 8 GPUs (configs[3]'s and configs[4]'s device counts): FedAvg.aggregate
+    takes the sharded multi-device path (peer access over xGMI) and matches the oracle bit for bit;
+    wsum_sharded over every one of those GPUs, direct and gather."""
+    if torch.cuda.device_count() < n_gpus:
+        pytest.skip("needs %d GPUs (xGMI peer reads); this box has %d" % (n_gpus, torch.cuda.device_count()))
+    from accdfl_amd.core import wsum
     from accdfl_amd.core.gradient_aggregation.fedavg import FedAvg
 
     c = gc.load("gnlenet_n8_dirichlet")
-    models = [m.to("cuda:%d" % (k % 2)) for k, m in enumerate(gc.build_models(c, "cpu"))]
+    models = [m.to("cuda:%d" % (k % n_gpus)) for k, m in enumerate(gc.build_models(c, "cpu"))]
     out = FedAvg.aggregate(models, c.weights)
     torch.cuda.synchronize()
     for p, want in zip(out.parameters(), c.out):
         assert p.device == torch.device("cuda", 0)
         assert same_bits(gc.from_torch(p, c.dtype), want, c.dtype)
-    n, numel = 8, 12_000_017
-    peers = [t.to("cuda:%d" % (k % 2)) for k, t in enumerate(_peers(n, numel, "f32", 9))]
+    # 64 peers (configs[3]'s count) of a ResNet-8-sized flat model spread round-robin over the GPUs
+    n, numel = (8, 12_000_017) if n_gpus == 2 else (64, 4_932_344)
+    peers = [t.to("cuda:%d" % (k % n_gpus)) for k, t in enumerate(_peers(n, numel, "f32", 9))]
     w = [float(x) for x in np.random.default_rng(9).dirichlet(np.ones(n))]
     want = c_wsum([p.cpu().numpy() for p in peers], w, "f32")
-    from accdfl_amd.core import wsum
-
+    devs = [torch.device("cuda", d) for d in range(n_gpus)]
     for mode in ("direct", "gather"):
-        out = wsum.wsum_sharded(peers, w, [torch.device("cuda", 0), torch.device("cuda", 1)], mode=mode)
+        out = wsum.wsum_sharded(peers, w, devs, mode=mode)
         torch.cuda.synchronize()
         assert same_bits(out.cpu().numpy(), want, "f32"), mode
+
+
+@pytest.mark.skipif(torch.cuda.device_count() < 2, reason="needs two GPUs")
+def test_table_reduce_on_a_device_that_is_not_current():
+    """The multi-tensor table path (>= 33 peers) for tensors on cuda:1 while device 0 is current (ADVICE
+    r05): the table's upload must run on the tensors' device, through the raw call and FedAvg.aggregate."""
+    from accdfl_amd.core import wsum
+    from accdfl_amd.core.gradient_aggregation.fedavg import FedAvg
+
+    torch.cuda.set_device(0)
+    d1 = torch.device("cuda", 1)
+    n, numels = 40, [1000, 4099, 64, 70_001]
+    g = torch.Generator().manual_seed(41)
+    host = [[(torch.randn(m, generator=g) * 0.05) for _ in range(n)] for m in numels]
+    w = [float(x) for x in np.random.default_rng(41).dirichlet(np.ones(n))]
+    dev = [[t.to(d1) for t in row] for row in host]
+    outs = [torch.empty(m, device=d1) for m in numels]
+    ptrs = [t.data_ptr() for row in dev for t in row]
+    wsum.wsum_multi_ptrs(torch.float32, ptrs, [o.data_ptr() for o in outs], numels, w, d1,
+                         stream=torch.cuda.current_stream(d1))
+    torch.cuda.synchronize(d1)
+    assert torch.cuda.current_device() == 0
+    for o, row in zip(outs, host):
+        assert same_bits(o.cpu().numpy(), c_wsum([t.numpy() for t in row], w, "f32"), "f32")
+    c = gc.load("gnlenet_n8_dirichlet")
+    models = [m.to(d1) for m in gc.build_models(c, "cpu")] * 5  # 40 models: the table path
+    w40 = [x / 5 for x in c.weights] * 5
+    out = FedAvg.aggregate(models, w40)
+    torch.cuda.synchronize(d1)
+    for i, p in enumerate(out.parameters()):
+        assert p.device == d1
+        want = c_wsum([c.params[k % len(c.params)][i] for k in range(len(models))], w40, c.dtype)
+        assert same_bits(gc.from_torch(p, c.dtype), want, c.dtype), i

@@ -145,6 +145,142 @@ def test_sharded_fedavg_over_rccl(world, n_peers, n_elems, dtype):
     _run_sharded(world, n_peers, n_elems, "nccl", dtype)
 
 
+def _hashed_rows(peers, a, b, dtype, chunk=1 << 18):
+    """Peers ``peers``' elements [a, b) of a synthetic model whose every element is a hash of (peer,
+    index): any rank builds any slice of any peer without generating whole rows (configs[4]'s 128 x
+    21.3 M bf16 model would be 5.4 GB per rank).  Values: uniform in +-0.05 scaled by 2^-0..-7, the
+    bf16 form the RNE cast of the f32 one.  Returns a CPU tensor [len(peers), b - a]."""
+    peers = np.asarray(list(peers), dtype=np.uint64)
+    out = torch.empty((len(peers), max(0, b - a)), dtype=_TORCH[dtype])
+    with np.errstate(over="ignore"):
+        for c0 in range(a, b, chunk):
+            c1 = min(b, c0 + chunk)
+            x = (np.arange(c0, c1, dtype=np.uint64)[None, :] * np.uint64(0x9E3779B97F4A7C15)
+                 + (peers[:, None] + np.uint64(1)) * np.uint64(0xD1B54A32D192ED03))
+            x ^= x >> np.uint64(31)
+            x *= np.uint64(0xBF58476D1CE4E5B9)
+            x ^= x >> np.uint64(29)
+            u = ((x >> np.uint64(40)).astype(np.float32) * np.float32(2.0 ** -24) - np.float32(0.5)) * np.float32(0.1)
+            u *= np.exp2(-((x >> np.uint64(13)) & np.uint64(7)).astype(np.float32))
+            out[:, c0 - a:c1 - a] = torch.from_numpy(u).to(_TORCH[dtype])
+    return out
+
+
+def _rccl_worker(rank, world, port, n_peers, n_elems, root, q, dtype, backend="nccl"):
+    """One rank of a full-size RCCL case: builds its bucket of every peer and its own whole peers, runs
+    the bucket-sharded all-gather, the exact all-to-all and (f32) the reduce-scatter mode, and checks ITS
+    bucket of each gathered result against the C oracle over the same bucket; the parent checks that every
+    rank gathered the same bytes (sha256), so every bucket of every rank's result is oracle-checked.
+    backend "gloo": the same steps on CPU tensors with the NumPy oracle as the reducer (CPU rehearsal)."""
+    import hashlib
+    import sys
+
+    for p in (os.path.join(root, "decentralized-learning_amd"), root, os.path.join(root, "tests")):
+        sys.path.insert(0, p)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
+    torch.set_num_threads(2)
+    if backend == "nccl":
+        dev = torch.device("cuda", rank)
+        torch.cuda.set_device(dev)
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    else:
+        dev = torch.device("cpu")
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from c_oracle import c_wsum
+        from accdfl_amd.core.sharding import BucketShardedFedAvg
+
+        weights = [float(x) for x in np.random.default_rng(n_peers).dirichlet(np.ones(n_peers))]
+        # RCCL: the libdlagg reducer (the sharding module's default)
+        sh = BucketShardedFedAvg(n_elems, _TORCH[dtype], device=dev,
+                                 reducer=None if backend == "nccl" else _oracle_reducer(dtype))
+        s, e = sh.local_range
+        mine = _hashed_rows(range(n_peers), s, e, dtype)
+        want = c_wsum(list(_to_bits(mine, dtype)) if dtype == "bf16" else list(mine.numpy()), weights, dtype)
+        want = want.view(_BITS[dtype][0])
+        padded = torch.zeros((n_peers, sh.bucket_len), dtype=_TORCH[dtype], device=dev)
+        padded[:, : e - s] = mine.to(dev)
+        full = sh.all_gather(sh.reduce_bucket(list(padded), weights))
+        del padded
+        res = {"range": (s, e)}
+
+        def check(name, t):
+            bits = _to_bits(t, dtype)
+            res[name + "_ok"] = bool(np.array_equal(bits[s:e], want)) and bits.size == n_elems
+            res[name + "_sha"] = hashlib.sha256(bits.tobytes()).hexdigest()
+
+        check("bucket", full)
+        m = n_peers // world
+        local = _hashed_rows(range(rank * m, (rank + 1) * m), 0, n_elems, dtype).to(dev)
+        check("peer", sh.aggregate_peer_sharded(local, weights))
+        if dtype == "f32":
+            rs = sh.aggregate_peer_sharded(local, weights, exact=False).cpu().numpy()[s:e].astype(np.float64)
+            vals = mine.numpy().astype(np.float64)
+            bound = n_peers * 2.0 ** -23 * np.sum(np.abs(np.asarray(weights)[:, None] * vals), axis=0)
+            err = np.abs(rs - want.view(np.float32).astype(np.float64))
+            res["rs_ok"] = bool(np.all(err <= bound + 1e-45))
+        q.put((rank, res))
+    finally:
+        dist.destroy_process_group()
+
+
+# BASELINE configs[3] (64 peers over 4 GPUs; ResNet-8's 4 932 344 f32 parameters: each rank's bucket is
+# configs[3']'s 1 233 086-element share) and configs[4] (128 google_speech ResNet-34 models, 21 296 355
+# bf16 parameters, over 8 GPUs: 2 662 144 elements per rank)
+@pytest.mark.gpu
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("world,n_peers,n_elems,dtype", [(4, 64, 4_932_344, "f32"), (8, 128, 21_296_355, "bf16")])
+def test_sharded_fedavg_over_rccl_at_config_size(world, n_peers, n_elems, dtype):
+    """configs[3] and configs[4]'s own splits over RCCL at full model size: all-gather and all-to-all
+    bit-exact against the C oracle bucket by bucket, reduce-scatter within its stated bound."""
+    if not torch.cuda.is_available() or torch.cuda.device_count() < world:
+        pytest.skip("needs %d GPUs (one per rank, RCCL over xGMI); this box has %d"
+                    % (world, torch.cuda.device_count() if torch.cuda.is_available() else 0))
+    _run_config_split(world, n_peers, n_elems, dtype, "nccl")
+
+
+@pytest.mark.parametrize("world,n_peers,n_elems,dtype", [(4, 64, 40_009, "f32"), (8, 128, 21_297, "bf16")])
+def test_config_split_rehearsal_on_cpu(world, n_peers, n_elems, dtype):
+    """The full-size RCCL cases' worker, its per-rank oracle check and the digest agreement, rehearsed
+    over gloo on the CPU at the same world sizes and peer counts (1/500 and 1/1000 of the elements)."""
+    _run_config_split(world, n_peers, n_elems, dtype, "gloo")
+
+
+def _run_config_split(world, n_peers, n_elems, dtype, backend):
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rccl_worker, args=(r, world, port, n_peers, n_elems, root, q, dtype, backend))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        results = dict(q.get(timeout=600) for _ in range(world))
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    assert sum(r["range"][1] - r["range"][0] for r in results.values()) == n_elems
+    for name in ("bucket", "peer"):
+        assert all(r[name + "_ok"] for r in results.values()), (name, {k: r[name + "_ok"] for k, r in results.items()})
+        assert len({r[name + "_sha"] for r in results.values()}) == 1, name
+    assert results[0]["bucket_sha"] == results[0]["peer_sha"]
+    if dtype == "f32":
+        assert all(r["rs_ok"] for r in results.values())
+
+
+def test_hashed_rows_slices_agree():
+    """_hashed_rows: a slice built alone equals the same slice of the whole rows (what lets every rank of
+    the full-size RCCL cases build only its bucket)."""
+    whole = _hashed_rows(range(5), 0, 1000, "bf16", chunk=128)
+    assert torch.equal(_hashed_rows([1, 3], 300, 777, "bf16"), whole[[1, 3], 300:777])
+    f = _hashed_rows(range(3), 0, 4096, "f32")
+    assert f.abs().max() <= 0.05 and f.std() > 0.001 and len(set(f[0].tolist())) > 4000
+
+
 def test_reduce_scatter_mode_is_fp32_fp64_only():
     """exact=False (reduce-scatter, re-associated) states its bound for fp32 / fp64 sums only."""
     from accdfl_amd.core.sharding import BucketShardedFedAvg
