@@ -1380,14 +1380,56 @@ def dfl_round_layout(name, n, dt, device, reps=3):
     in_bytes = n * p * torch.empty((), dtype=dt).element_size()
     n_cross = sum(1 for s in _layout(name)[0] if int(np.prod(s) if s else 1) * torch.empty((), dtype=dt).element_size()
                   >= EVA_BLOCK)
+    native = all(getattr(v, "_sd", 0) is None for v in list(mm.incoming_trained_models.values())[1:])
+    # the per-peer phase split of one more round (decode = native scan + batched gather, stage = the call
+    # that enqueues the peer's copy; copy_busy: the copy stream's own time for the peers' H2D)
+    mm.reset_incoming_trained_models()
+    ph = mm.start_phases()
+    for k, (blocks, ml) in enumerate(msgs):
+        head, _ = wire.split_blocks(blocks, ml)
+        mm.process_incoming_serialized(b"peer%d" % k, head)
+    mm.slab.copy_stream.synchronize()
+    mm.phases = None
+    busy = sum(a.elapsed_time(b) for a, b in ph["copy_events"])
+    phases = {"decode_gather_ms": round(sum(ph["decode_gather_ms"]), 2),
+              "stage_issue_ms": round(sum(ph["stage_issue_ms"]), 2), "copy_busy_ms": round(busy, 2),
+              "copy_GBps": round(in_bytes / (busy / 1e3) / 1e9, 2) if busy else None}
+    ref = dfl_round_layout_reference_style(msgs, _layout_models(name, 1, dt, pinned=False, seed=4200)[0][0])
     return {"layout": name, "peers": n, "params": p, "parameter_tensors": len(names), "dtype": str(dt),
             "eva_block_bytes": EVA_BLOCK, "tensors_of_at_least_one_block": n_cross,
             "ingress_ms": round(med[0] * 1e3, 2), "ingress_complete_ms": round(med[1] * 1e3, 2),
             "ingress_GBps": round(in_bytes / med[1] / 1e9, 2),
             "aggregate_serialized_ms": round(med[2] * 1e3, 2), "round_ms": round(med[3] * 1e3, 2),
+            "native_ingress": native, "phases": phases,
+            "reference_style_ingress_ms": ref,
+            "ingress_speedup_vs_reference_style": round(ref / (med[1] * 1e3), 1) if ref else None,
             "parity_ok": bool(ok),
             "parity": "every parameter of the decoded aggregate_serialized payload == FedAvg.aggregate on the same "
-                      "modules on the device (no wire), bit for bit"}
+                      "modules on the device (no wire), bit for bit",
+            "path": "EVA blocks -> split at model_data_len -> native scan of the state-dict pickle (csrc/walk.cpp) -> "
+                    "ONE batched gather of every storage into the page-locked ingress buffer, parameters back to "
+                    "back -> ONE 2D H2D per peer into the tile-interleaved PeerSlab -> reduce -> payload bytes "
+                    "from HBM (aggregate_serialized)"}
+
+
+def dfl_round_layout_reference_style(msgs, template, reps=2):
+    """The same many-tensor ingress the reference's way, on this host's CPU, for the same payloads:
+    b''.join of the EVA blocks (accdfl/util/eva/transfer/incoming.py:35), the model_data_len slice
+    (accdfl/dfl/community.py:587), pickle.loads + load_state_dict into a fresh model
+    (accdfl/core/models/__init__.py:13-16; create_model's allocation stood for by a deepcopy of the
+    template).  Median ms for all peers (bytes this process made: pickle.loads is the reference's)."""
+    import copy
+    import pickle
+
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        for blocks, ml in msgs:
+            data = b"".join(blocks)
+            m = copy.deepcopy(template)
+            m.load_state_dict(pickle.loads(data[:ml]))
+        ts.append(time.perf_counter() - t0)
+    return round(statistics.median(ts) * 1e3, 1)
 
 
 def dfl_round_reference_style(msgs, p, reps=2):

@@ -14,6 +14,7 @@ from __future__ import annotations
 
 import collections
 import copy
+import functools
 import time
 from typing import Dict, List, Optional
 
@@ -63,8 +64,19 @@ class WirePeer:
     ``wire.loads_state_dict``: its state dict, without the ``create_model`` +
     ``load_state_dict`` the reference runs (accdfl/core/models/__init__.py:13-16)."""
 
-    def __init__(self, state_dict):
-        self.state_dict = state_dict
+    def __init__(self, state_dict=None, make=None):
+        """``state_dict``: the decoded tensors; or ``make``: a callable building them on first use (the
+        native ingress path: the tensors over the page-locked ingress buffer are made only if the round
+        reads them — models[0]'s buffers, or a fallback round)."""
+        self._sd = state_dict
+        self._make = make
+
+    @property
+    def state_dict(self):
+        if self._sd is None:
+            self._sd = self._make()
+            self._make = None
+        return self._sd
 
     def materialize(self, template: nn.Module) -> nn.Module:
         """The module the reference's ``unserialize_model`` would build."""
@@ -108,6 +120,7 @@ class DeviceModelManager(ModelManager):
         # on: decode + gather into the ingress buffer (CPU), the stage call (CPU) and HIP timing events
         # around each arrival's copies on the slab's copy stream (bench.py dfl_round's phase split)
         self.phases: Optional[dict] = None
+        self._spec = None  # (template, parameter names, shapes): _row_spec's cache
 
     def start_phases(self) -> dict:
         self.phases = {"decode_gather_ms": [], "stage_issue_ms": [], "copy_events": []}
@@ -136,9 +149,9 @@ class DeviceModelManager(ModelManager):
             self.slab.stage(incoming_model)
             self._staged.append((peer_pk, incoming_model, self._fingerprint(incoming_model)))
 
-    def _ingress_alloc(self, pos: int, nbytes: int):
-        """Bump allocator over registry position ``pos``'s page-locked ingress buffer (grown to
-        ``nbytes``); waits until the H2D that last read that buffer has finished."""
+    def _ingress_buffer(self, pos: int, nbytes: int) -> torch.Tensor:
+        """Registry position ``pos``'s page-locked ingress buffer (grown to ``nbytes``), once the H2D that
+        last read it has finished."""
         while len(self._ingress) <= pos:
             self._ingress.append(None)
             self._ingress_ev.append(None)
@@ -148,6 +161,12 @@ class DeviceModelManager(ModelManager):
         buf = self._ingress[pos]
         if buf is None or buf.numel() < nbytes:
             buf = self._ingress[pos] = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
+        return buf
+
+    def _ingress_alloc(self, pos: int, nbytes: int):
+        """Bump allocator over registry position ``pos``'s page-locked ingress buffer (grown to
+        ``nbytes``); waits until the H2D that last read that buffer has finished."""
+        buf = self._ingress_buffer(pos, nbytes)
         off = [0]
 
         def alloc(n: int) -> torch.Tensor:
@@ -158,6 +177,14 @@ class DeviceModelManager(ModelManager):
             return buf[a:a + n]
         return alloc
 
+    def _row_spec(self):
+        """The template's parameter names and shapes in parameters() order (the slab row's layout),
+        cached per template module."""
+        if self._spec is None or self._spec[0] is not self.template:
+            named = list(self.template.named_parameters())
+            self._spec = (self.template, [n for n, _ in named], [tuple(p.shape) for _, p in named])
+        return self._spec[1], self._spec[2]
+
     def process_incoming_serialized(self, peer_pk: bytes, data):
         """A model straight from the wire (§8 f1), decoded without executing the payload and
         staged into HBM, with no ``create_model`` / ``load_state_dict``.  ``data`` is the
@@ -165,24 +192,71 @@ class DeviceModelManager(ModelManager):
         ``memoryview(result.data)[:model_data_len]``: no slice copy, accdfl/dfl/community.py:587)
         or the block list of the EVA transfer before its ``b''.join``
         (accdfl/util/eva/transfer/incoming.py:35; ``wire.split_blocks`` splits a DFL message's
-        blocks): its tensors are then gathered into a page-locked ingress buffer and sent to
-        HBM from there asynchronously.  The decoded tensors view ``data`` / that buffer, which
-        stays valid for this round (the buffer is reused one round later)."""
+        blocks).
+
+        The payload is scanned natively (``wire.scan_state_dict``: the restricted opcode subset, no
+        tensor built, no element byte copied); every storage is then gathered out of the payload into a
+        page-locked ingress buffer by ONE batched memcpy, with the parameters back to back in
+        ``parameters()`` order, so the peer's PeerSlab row goes to HBM as ONE asynchronous copy.  The
+        peer's state dict (``WirePeer.state_dict``) is built over that buffer only if the round reads it.
+        Payloads the native scan does not take (the extension absent, views, shared or mistyped
+        parameter storages, anything outside a state dict's pickle) are decoded by the Python decoder
+        as before; an unsafe payload is refused by it (``wire.UnsafePayloadError``).  The decoded
+        tensors view the ingress buffer (or ``data``), which stays valid for this round (the buffer is
+        reused one round later)."""
         if peer_pk in self.incoming_trained_models:
             return
         if self.template is None:
             raise ValueError("DeviceModelManager needs a template module to decode wire payloads")
-        alloc = None
-        pos = -1
         if not self.incoming_trained_models:
             self._ingress_next = 0  # a new round (also when the caller replaced the registry dict)
+        if self.slab is None and _one_dtype(self.template):
+            self.slab = self._slab_cls.for_model(self.template, capacity=self._capacity, device=self._device)
+        ph = self.phases
+        t0 = time.perf_counter() if ph is not None else 0.0
+        lay = None
+        if self.slab is not None and len(self._staged) == self.slab.n:
+            names, shapes = self._row_spec()
+            if shapes == self.slab.shapes:
+                scan = wire.scan_state_dict(data)
+                lay = scan.row_layout(names, self.slab.dtype, shapes) if scan is not None else None
+        if lay is None:
+            self._ingress_python(peer_pk, data, ph, t0)
+            return
+        offsets, total, row = lay
+        pos = self._ingress_next
+        self._ingress_next += 1
+        buf = self._ingress_buffer(pos, total)[:total]
+        scan.gather(buf, offsets)
+        scan.release_payload()
+        peer = WirePeer(make=functools.partial(scan.state_dict, buf, offsets))
+        self.incoming_trained_models[peer_pk] = peer
+        if ph is not None:
+            t1 = time.perf_counter()
+            ph["decode_gather_ms"].append((t1 - t0) * 1e3)
+            e0 = torch.cuda.Event(enable_timing=True)
+            e0.record(self.slab.copy_stream)
+        self.slab.stage_flat(buf[:row].view(self.slab.dtype))
+        self._staged.append((peer_pk, peer, ()))
+        if ph is not None:
+            e1 = torch.cuda.Event(enable_timing=True)
+            e1.record(self.slab.copy_stream)
+            ph["stage_issue_ms"].append((time.perf_counter() - t1) * 1e3)
+            ph["copy_events"].append((e0, e1))
+        ev = torch.cuda.Event()
+        ev.record(self.slab.copy_stream)
+        self._ingress_ev[pos] = ev
+
+    def _ingress_python(self, peer_pk: bytes, data, ph, t0):
+        """process_incoming_serialized through the Python decoder (wire.loads_state_dict): block lists
+        gathered tensor by tensor into the ingress buffer, each parameter staged on its own."""
+        alloc = None
+        pos = -1
         if isinstance(data, (list, tuple)):
             pos = self._ingress_next
             self._ingress_next += 1
             n_tensors = len(self.template.state_dict())
             alloc = self._ingress_alloc(pos, sum(len(b) for b in data) + 256 * (n_tensors + 1))
-        ph = self.phases
-        t0 = time.perf_counter() if ph is not None else 0.0
         sd = wire.loads_state_dict(data, copy=False, alloc=alloc)  # views of `data` / the ingress buffer
         params = wire.parameter_tensors(sd, self.template)
         peer = WirePeer(sd)
@@ -190,8 +264,6 @@ class DeviceModelManager(ModelManager):
         if ph is not None:
             t1 = time.perf_counter()
             ph["decode_gather_ms"].append((t1 - t0) * 1e3)
-        if self.slab is None and _one_dtype(self.template):
-            self.slab = self._slab_cls.for_model(self.template, capacity=self._capacity, device=self._device)
         if self.slab is None:
             return  # parameters of several dtypes: no slab; the round falls back to FedAvg.aggregate
         if ph is not None:

@@ -555,6 +555,109 @@ def loads_state_dict(data, copy: bool = True, alloc: Optional[Callable[[int], to
     return obj
 
 
+class StateDictScan:
+    """A ``serialize_model`` payload scanned in native code (csrc/walk.cpp ``scan_state_dict``: the same
+    restricted opcode subset and allow-list as ``_vm_loads``, run over the block list in place, no tensor
+    built and no element byte copied).  ``entries`` maps each state-dict key to its description
+    ``(tag, storage index, storage offset, sizes, strides, requires_grad)`` — tied entries share one
+    description object — and ``storages`` lists ``(dtype name, numel, payload position, nbytes)``.
+
+    ``gather(buf, offsets)`` copies every storage's bytes out of the payload into ``buf`` (a host uint8
+    tensor; storage i at byte ``offsets[i]``) with one batched memcpy; ``state_dict(buf, offsets)`` then
+    makes the tensors over ``buf`` — one storage per pickled storage, as pickle.loads gives."""
+
+    __slots__ = ("entries", "storages", "addrs", "lens", "owner")
+
+    def __init__(self, entries, storages, addrs, lens, owner):
+        self.entries, self.storages, self.addrs, self.lens, self.owner = entries, storages, addrs, lens, owner
+
+    def gather(self, buf: torch.Tensor, offsets: np.ndarray) -> None:
+        from accdfl_amd import _lib
+
+        if not self.storages:
+            return
+        t0 = time.perf_counter() if GATHER_MS is not None else 0.0
+        st = np.asarray([(p, n) for _, _, p, n in self.storages], dtype=np.int64).reshape(-1, 2)
+        dst = offsets.astype(np.int64) + buf.data_ptr()
+        d, s, n = _lib.walk_module().span_pieces(self.addrs, self.lens, np.ascontiguousarray(st[:, 0]),
+                                                 np.ascontiguousarray(st[:, 1]), dst)
+        if len(n):
+            _lib.host_copy_batch(d, s, n, streaming=_INGRESS_NT and int(n.sum()) >= (4 << 20) and buf.is_pinned())
+        if GATHER_MS is not None:
+            GATHER_MS.append((time.perf_counter() - t0) * 1e3)
+
+    def release_payload(self) -> None:
+        """Forget the payload's blocks once gathered (the state dict is built from the buffer alone)."""
+        self.addrs = self.lens = self.owner = None
+
+    def state_dict(self, buf: torch.Tensor, offsets: np.ndarray) -> "collections.OrderedDict[str, torch.Tensor]":
+        from accdfl_amd import _lib
+
+        return _lib.walk_module().build_state_dict(buf, offsets.astype(np.int64), self.entries, self.storages,
+                                                   collections.OrderedDict)
+
+    def row_layout(self, names: Sequence[str], dtype: torch.dtype, shapes: Sequence[tuple]):
+        """Where a PeerSlab row's parameters can come from in one piece: when the entries ``names``
+        (``template.named_parameters()`` order) are dense tensors of ``dtype`` and ``shapes``, each the
+        whole of a storage of its own, ``(offsets, total bytes, row bytes)`` — a byte offset per storage
+        that puts those parameters back to back from byte 0 (the row the slab stages with ONE copy), every
+        other storage after them, 256-byte aligned.  None otherwise (a missing key, a view, a shared or
+        mis-typed storage): the caller decodes through the general path."""
+        dname = str(dtype).replace("torch.", "")
+        offsets = np.full(len(self.storages), -1, dtype=np.int64)
+        off = 0
+        for name, shape in zip(names, shapes):
+            d = self.entries.get(name)
+            if d is None:
+                return None
+            _, sidx, soff, size, stride, _ = d
+            sdt, numel, _, nbytes = self.storages[sidx]
+            if soff != 0 or size != shape or sdt != dname or offsets[sidx] >= 0:
+                return None
+            n = 1
+            for s in size:
+                n *= s
+            if numel != n or stride != _contiguous_strides(size):
+                return None
+            offsets[sidx] = off
+            off += nbytes
+        row = off
+        off = -(-off // 256) * 256
+        for i, (_, _, _, nbytes) in enumerate(self.storages):
+            if offsets[i] < 0:
+                offsets[i] = off
+                off += -(-nbytes // 256) * 256
+        return offsets, max(off, 1), row
+
+
+def _contiguous_strides(size) -> tuple:
+    st, acc = [], 1
+    for s in reversed(size):
+        st.append(acc)
+        acc *= s
+    return tuple(reversed(st))
+
+
+def scan_state_dict(data) -> Optional[StateDictScan]:
+    """``data`` (bytes, a memoryview or an EVA block list) scanned natively, or None when the native
+    extension is absent or the payload holds anything outside a state dict's pickle (the Python decoder
+    then decodes it or refuses it with its own error)."""
+    from accdfl_amd import _lib
+
+    mod = _lib.walk_module()
+    if mod is None or not hasattr(mod, "scan_state_dict"):
+        return None
+    blocks = list(data) if isinstance(data, (list, tuple)) else [data]
+    addrs, lens = _block_table(blocks)
+    if len(lens) and not lens.all():
+        keep = np.flatnonzero(lens)
+        addrs, lens = addrs[keep], lens[keep]
+    res = mod.scan_state_dict(np.ascontiguousarray(addrs), np.ascontiguousarray(lens), collections.OrderedDict)
+    if res is None:
+        return None
+    return StateDictScan(res[0], res[1], addrs, lens, blocks)
+
+
 _STORAGE_NAMES = {v: k for k, v in _STORAGE_DTYPES.items()}
 _SENTINEL_BYTES = 1 << 16   # >= the pickler's 64 KiB frame target: written outside any frame
 

@@ -139,6 +139,93 @@ def test_multi_tensor_eva_blocks_into_the_slab(block):
         assert same_bits(p.detach().reshape(-1).numpy(), want, "f32"), "parameter %d" % i
 
 
+def _layout_module(name, dtype, seed):
+    """A module with the parameter and buffer layout `name` of tests/golden/layouts.json (the reference's
+    models' state-dict layouts), seeded values."""
+    lay = json.load(open(os.path.join(os.path.dirname(GOLDEN), "layouts.json")))[name]
+    m = nn.Module()
+    g = torch.Generator().manual_seed(seed)
+    m.ps = nn.ParameterList([nn.Parameter((torch.randn(s, generator=g) * 0.05).to(dtype)) for _, s, _ in lay["params"]])
+    for j, (_, s, d) in enumerate(lay["buffers"]):
+        m.register_buffer("b%d" % j, torch.randn(s, generator=g).to(getattr(torch, d)) if d != "int64"
+                          else torch.full(s, seed + j, dtype=torch.int64))
+    return m
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("form", ["blocks", "bytes", "memoryview"])
+def test_real_layout_round_through_the_native_ingress(form):
+    """4 google_speech ResNet-34 bf16 peers (110 parameters, 108 BN buffers) through
+    the native ingress (one scan, one batched gather, ONE slab copy per peer; the peers' state dicts never
+    built), then aggregate_serialized and aggregate_trained_models against FedAvg.aggregate of the same
+    modules on the device, bit for bit, with the first arrival's buffers."""
+    from types import SimpleNamespace
+
+    from accdfl_amd.core import wire
+    from accdfl_amd.core.gradient_aggregation import GradientAggregationMethod
+    from accdfl_amd.core.gradient_aggregation.fedavg import FedAvg
+    from accdfl_amd.core.model_manager import DeviceModelManager
+
+    models = [_layout_module("google_speech_resnet34", torch.bfloat16, 10 + k) for k in range(4)]
+    w = [float(x) for x in np.random.default_rng(4).dirichlet(np.ones(4))]
+    mm = DeviceModelManager(None, SimpleNamespace(gradient_aggregation=GradientAggregationMethod.FEDAVG),
+                            template=_layout_module("google_speech_resnet34", torch.bfloat16, 0), capacity=4)
+    want = FedAvg.aggregate([m.cuda() for m in models], w)
+    torch.cuda.synchronize()
+    models = [m.cpu() for m in models]
+    for rnd in range(2):  # the second round reuses the ingress buffers and the slab
+        mm.reset_incoming_trained_models()
+        for k, m in enumerate(models):
+            data = wire.serialize_model(m)
+            payload = {"blocks": wire.payload_blocks(data, 60_000), "bytes": data, "memoryview": memoryview(data)}[form]
+            mm.process_incoming_serialized(b"peer%d" % k, payload)
+        peers = list(mm.incoming_trained_models.values())
+        assert mm.slab.n == 4 and all(p._sd is None for p in peers), "the native path builds no state dict"
+        direct = wire.loads_state_dict(mm.aggregate_serialized(w))
+        out = mm.aggregate_trained_models(w)
+        assert all(p._sd is None for p in peers[1:])  # only models[0]'s buffers were read
+        for (name, p), q in zip(want.named_parameters(), out.parameters()):
+            assert torch.equal(p.detach().cpu().view(torch.int16), q.detach().view(torch.int16)), (rnd, name)
+            assert torch.equal(p.detach().cpu().view(torch.int16), direct[name].view(torch.int16)), (rnd, name)
+        for name, b in models[0].named_buffers():
+            assert torch.equal(direct[name], b) and torch.equal(dict(out.named_buffers())[name], b), (rnd, name)
+
+
+@pytest.mark.gpu
+def test_ingress_falls_back_for_strided_parameters():
+    """A payload whose parameter is a transposed view (its storage is not the parameter's dense bytes):
+    the native row layout refuses it and the Python decoder stages the round, bit-exact."""
+    from types import SimpleNamespace
+
+    from accdfl_amd.core import wire
+    from accdfl_amd.core.gradient_aggregation import GradientAggregationMethod
+    from accdfl_amd.core.model_manager import DeviceModelManager
+    from c_oracle import c_wsum
+
+    class Net(nn.Module):
+        def __init__(self, seed):
+            super().__init__()
+            g = torch.Generator().manual_seed(seed)
+            self.a = nn.Parameter(torch.randn(70, 300, generator=g).t())  # strides (1, 300)
+            self.b = nn.Parameter(torch.randn(5000, generator=g))
+
+    models = [Net(k) for k in range(3)]
+    mm = DeviceModelManager(None, SimpleNamespace(gradient_aggregation=GradientAggregationMethod.FEDAVG),
+                            template=Net(99), capacity=3)
+    for k, m in enumerate(models):
+        data = wire.serialize_model(m)
+        sc = wire.scan_state_dict(data)
+        names, shapes = mm._row_spec()
+        assert sc is not None and sc.row_layout(names, torch.float32, shapes) is None
+        mm.process_incoming_serialized(b"p%d" % k, wire.payload_blocks(data, 4096))
+    assert mm.slab.n == 3 and all(p._sd is not None for p in mm.incoming_trained_models.values())
+    w = [0.5, 0.3, 0.2]
+    out = mm.aggregate_trained_models(w)
+    for i, p in enumerate(out.parameters()):
+        want = c_wsum([list(m.parameters())[i].detach().contiguous().reshape(-1).numpy() for m in models], w, "f32")
+        assert same_bits(p.detach().contiguous().reshape(-1).numpy(), want, "f32"), i
+
+
 def test_device_source_entries_encode_like_tensors():
     """wire.DeviceSource (aggregate_serialized's parameter entries): small entries go through the CPU
     like any tensor, so a state dict whose entries are slices of one flat tensor encodes to exactly
