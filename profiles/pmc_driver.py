@@ -25,7 +25,22 @@ SHAPES = {"ns": (8, 25_000_000, torch.float32, 16384), "c4share": (128, 2_662_04
           "r34flat16": (16, 21_296_355, torch.bfloat16, 16384)}
 
 
-MODULE_SHAPES = {"r34x16": ("google_speech_resnet34", 16), "r34x128": ("google_speech_resnet34", 128)}
+MODULE_SHAPES = {"r34x16": ("google_speech_resnet34", 16), "r34x128": ("google_speech_resnet34", 128),
+                 # round 6: the same models with each model's parameters as 256-byte
+                 # aligned views of ONE allocation per model instead of one caching-allocator block each
+                 "r34x16c": ("google_speech_resnet34", 16), "r34x128c": ("google_speech_resnet34", 128)}
+
+
+def contiguous_model(numels, dtype, dev):
+    """One model's parameters as views of one allocation, each starting 256-byte aligned."""
+    es = torch.tensor([], dtype=dtype).element_size()
+    al = 256 // es
+    offs, o = [], 0
+    for m in numels:
+        offs.append(o)
+        o += -(-m // al) * al
+    flat = torch.empty(max(o, 1), dtype=dtype, device=dev)
+    return [flat[a:a + m] for a, m in zip(offs, numels)]
 
 
 def module_round(key, reps, dev):
@@ -40,7 +55,10 @@ def module_round(key, reps, dev):
     numels = [int(np.prod(s)) if s else 1 for s in shapes]
     # separate allocations, uninitialised (no fill kernels: under --pmc every dispatch is serialised and
     # 14 080 fills would take minutes; the values do not change the reduce's timing or its traffic)
-    peers = [[torch.empty(m, dtype=torch.bfloat16, device=dev) for m in numels] for _ in range(n)]
+    if key.endswith("c"):
+        peers = [contiguous_model(numels, torch.bfloat16, dev) for _ in range(n)]
+    else:
+        peers = [[torch.empty(m, dtype=torch.bfloat16, device=dev) for m in numels] for _ in range(n)]
     outs = [torch.empty(m, dtype=torch.bfloat16, device=dev) for m in numels]
     ptrs = (ctypes.c_void_p * (n * len(numels)))(*[peers[k][t].data_ptr() for t in range(len(numels))
                                                    for k in range(n)])
