@@ -1038,11 +1038,53 @@ def host_inclusive_configs(reps=3):
             row["tensors"] = len(list(models[0].parameters()))
             row[mem + "_ms"] = ms
             row[mem + "_GB/s"] = round((n + 1) * p * es / (ms / 1e3) / 1e9, 2)
+            if mem == "pageable":
+                log("host-inclusive %s (staged on arrival)" % name)
+                row.update(staged_on_arrival(models, w))
             del models
         row["h2d_bytes"] = n * p * es
         res[name] = row
     release_staging()
     return res
+
+
+def staged_on_arrival(models, w, reps=3):
+    """The same CPU modules handed to DeviceModelManager one by one as they would arrive
+    (accdfl/core/model_manager.py:42-47 process_incoming_trained_model; the GL / DL call sites,
+    accdfl/gl/community.py:110-117, accdfl/dl/community.py:98-106): each is staged into the HBM PeerSlab
+    on arrival, and the next arrives only after its copy has finished (a gap at least as long as each
+    H2D).  ``staged_on_arrival_ms``: from the LAST arrival (its process_incoming_trained_model call) to
+    aggregate_trained_models returning the CPU result module — the last model's H2D, the reduce, the
+    D2H into the result and deepcopy(models[0]).  ``staged_parity_ok``: the result equals FedAvg.aggregate
+    of the same modules (the host path), every parameter bit for bit."""
+    from types import SimpleNamespace
+
+    from accdfl_amd.core.gradient_aggregation import GradientAggregationMethod
+    from accdfl_amd.core.gradient_aggregation.fedavg import FedAvg
+    from accdfl_amd.core.model_manager import DeviceModelManager
+
+    n = len(models)
+    mm = DeviceModelManager(None, SimpleNamespace(gradient_aggregation=GradientAggregationMethod.FEDAVG), 0,
+                            capacity=n)
+    ts, out = [], None
+    for _ in range(reps + 1):
+        mm.reset_incoming_trained_models()
+        for k, m in enumerate(models[:-1]):
+            mm.process_incoming_trained_model(b"p%d" % k, m)
+            mm.slab.copy_stream.synchronize()  # the next model arrives after this one's H2D
+        time.sleep(0.002)
+        t0 = time.perf_counter()
+        mm.process_incoming_trained_model(b"last", models[-1])
+        out = mm.aggregate_trained_models(w)
+        ts.append(time.perf_counter() - t0)
+    uniform = mm._uniform()
+    want = FedAvg.aggregate(models, w)
+    ok = all(torch.equal(a.detach().view(-1).view(torch.uint8), b.detach().view(-1).view(torch.uint8))
+             for a, b in zip(out.parameters(), want.parameters()))
+    del mm
+    torch.cuda.empty_cache()
+    return {"staged_on_arrival_ms": round(statistics.median(ts[1:]) * 1e3, 3), "staged_slab_path": uniform,
+            "staged_parity_ok": bool(ok)}
 
 
 # (layout, peers, dtype) of the device-resident module rounds: FedAvg.aggregate on modules that live in
@@ -1594,6 +1636,8 @@ def cpu_baseline_all(args, result, n, p, headline=None):
             if g and "pageable_ms" in g:
                 g["cpu_port_ms"] = row["cpu_port_ms"]
                 g["pageable_over_cpu"] = round(row["cpu_port_ms"] / g["pageable_ms"], 1)
+                if g.get("staged_on_arrival_ms"):
+                    g["staged_over_cpu"] = round(row["cpu_port_ms"] / g["staged_on_arrival_ms"], 1)
     return cb
 
 

@@ -26,6 +26,25 @@ from accdfl_amd.core import wire
 from accdfl_amd.core.gradient_aggregation.fedavg import FedAvg, _center_copy
 
 
+def _native_fingerprint(model: nn.Module) -> Optional[bytes]:
+    """DeviceModelManager._fingerprint in native code (csrc/walk.cpp fingerprint: the same (identity,
+    data pointer, version) of every parameter, as bytes), or None when the extension is absent or the
+    model's tree holds a module class with its own parameter walk.  Classes not met before are classified
+    once (fedavg._plain_walk), so a model gets the same kind of fingerprint at staging and at aggregation."""
+    from accdfl_amd import _lib
+    from accdfl_amd.core.gradient_aggregation import fedavg as _fa
+
+    mod = _lib.walk_module()
+    if mod is None or not hasattr(mod, "fingerprint"):
+        return None
+    fp = mod.fingerprint(model, _fa._PLAIN_SET)
+    if fp is None:
+        fresh = [type(sub) for sub in model.modules() if type(sub) not in _fa._plain_walk_cls]
+        if any([_fa._plain_walk(cls) for cls in fresh]):
+            fp = mod.fingerprint(model, _fa._PLAIN_SET)
+    return fp
+
+
 def _one_dtype(model: nn.Module) -> bool:
     """The model's parameters share one dtype (what a PeerSlab row holds)."""
     return len({p.dtype for p in model.parameters()}) == 1
@@ -135,6 +154,9 @@ class DeviceModelManager(ModelManager):
         re-register it (or call ``reset_incoming_trained_models``)."""
         if isinstance(model, WirePeer):
             return ()
+        fp = _native_fingerprint(model)
+        if fp is not None:
+            return fp
         return tuple((id(p), p.data_ptr(), p._version) for p in model.parameters())
 
     def process_incoming_trained_model(self, peer_pk: bytes, incoming_model: nn.Module):

@@ -31,11 +31,12 @@ MODULE_SHAPES = {"r34x16": ("google_speech_resnet34", 16), "r34x128": ("google_s
                  "r34x16c": ("google_speech_resnet34", 16), "r34x128c": ("google_speech_resnet34", 128)}
 
 
-def contiguous_model(numels, dtype, dev):
-    """One model's parameters as views of one allocation, each starting 256-byte aligned."""
+def contiguous_model(numels, dtype, dev, shift_bytes=0):
+    """One model's parameters as views of one allocation, each starting 256-byte aligned; with
+    ``shift_bytes`` every view starts that many bytes (a multiple of 256) further into the allocation."""
     es = torch.tensor([], dtype=dtype).element_size()
     al = 256 // es
-    offs, o = [], 0
+    offs, o = [], shift_bytes // es
     for m in numels:
         offs.append(o)
         o += -(-m // al) * al

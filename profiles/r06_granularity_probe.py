@@ -34,9 +34,13 @@ def main():
         byts = (n + 1) * p * 2
         steps = 20 if n > 16 else 100
         row = {"models": n, "tensors_per_model": len(numels), "bytes": byts}
-        for layout in ("separate", "contiguous", "separate"):  # separate twice: drift between the two
+        # separate twice: drift between the runs; "staggered": contiguous, model k shifted by k x 4.25 KiB
+        # (do same-offset reads of the models landing on the same channels explain "contiguous"?)
+        for layout in ("separate", "contiguous", "staggered", "separate_again"):
             if layout == "contiguous":
                 peers = [contiguous_model(numels, torch.bfloat16, dev) for _ in range(n)]
+            elif layout == "staggered":
+                peers = [contiguous_model(numels, torch.bfloat16, dev, shift_bytes=k * 4352) for k in range(n)]
             else:
                 peers = [[torch.empty(m, dtype=torch.bfloat16, device=dev) for m in numels] for _ in range(n)]
             for ts in peers:
@@ -53,7 +57,7 @@ def main():
 
             ev = statistics.median(bench.time_kernel(once, steps, 5, 1, settle_s=0.05)[1] for _ in range(3))
             us = ev / steps * 1e6
-            key = layout if layout not in row else layout + "_again"
+            key = layout
             row[key + "_us"] = round(us, 2)
             row[key + "_frac_of_8TBps"] = round(byts / (us * 1e-6) / 8e12, 4)
             del peers, outs

@@ -67,6 +67,8 @@ def test_gl_gossip_merge(manager):
         age_sum = remote_age + my_age
         weights = [my_age / age_sum, remote_age / age_sum] if age_sum > 0 else None
         my_age = max(remote_age, my_age)
+        if manager == "DeviceModelManager":
+            assert mm._uniform(), "both models staged into HBM on arrival: the slab path"
         result = mm.aggregate_trained_models(weights=weights)
         _check(result, [detached, incoming], weights or [0.5, 0.5])
         mm.model = result
@@ -89,6 +91,48 @@ def test_dl_round_assigns_registry_directly():
     result = mm.aggregate_trained_models()
     _check(result, [m for _, m in received], [0.2] * 5)
     assert all(p.device.type == "cpu" for p in result.parameters())
+
+
+def test_dl_round_staged_on_arrival():
+    """accdfl/dl/community.py:98-106 with the models staged into HBM as they arrive: the receive handler
+    also hands each (CPU) model to DeviceModelManager.process_incoming_trained_model; aggregate_models
+    then runs the reference's own lines — the registry overwritten with a dict of the same models in the
+    same order, each moved to the CPU (a no-op for CPU modules) — and the round reduces the staged slab
+    rows (no H2D at aggregation), bit-exact, two rounds in a row."""
+    from accdfl_amd.core.model_manager import DeviceModelManager
+
+    mm = DeviceModelManager(GNLeNetLike(0), _settings(), 0, capacity=4)
+    for rnd in range(2):
+        incoming_models = []
+        for i in range(5):  # on_receive: unserialized CPU models, staged as they arrive
+            pk, model = b"n%d" % i, GNLeNetLike(20 + 10 * rnd + i)
+            incoming_models.append((pk, model))
+            mm.process_incoming_trained_model(pk, model)
+        mm.incoming_trained_models = dict((x, y) for x, y in incoming_models)
+        for pk in mm.incoming_trained_models.keys():
+            mm.incoming_trained_models[pk] = mm.incoming_trained_models[pk].to(torch.device("cpu"))
+        assert mm._uniform(), "the registry still holds exactly the staged rows"
+        result = mm.aggregate_trained_models()
+        _check(result, [m for _, m in incoming_models], [0.2] * 5)
+        assert all(p.device.type == "cpu" for p in result.parameters())
+        mm.model = result
+        mm.reset_incoming_trained_models()
+
+
+def test_staged_model_written_after_arrival_is_reread():
+    """A model staged on arrival and then written in place (its version counter moves) no longer matches
+    its slab row: the round averages the registry as it stands at aggregation time (fedavg.py:23-25)."""
+    from accdfl_amd.core.model_manager import DeviceModelManager
+
+    mm = DeviceModelManager(GNLeNetLike(0), _settings(), 0, capacity=3)
+    models = [GNLeNetLike(60 + i) for i in range(3)]
+    for i, m in enumerate(models):
+        mm.process_incoming_trained_model(b"n%d" % i, m)
+    assert mm._uniform()
+    with torch.no_grad():
+        models[1].ps[0].mul_(2.0)
+    assert not mm._uniform()
+    _check(mm.aggregate_trained_models(), models, [1 / 3.] * 3)
 
 
 def test_dfl_aggregator_round_on_wire_bytes():
