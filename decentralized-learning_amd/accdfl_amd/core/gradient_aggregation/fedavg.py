@@ -427,31 +427,25 @@ def _device_round(models: List[nn.Module], weights, layout) -> "nn.Module | None
     peers, whatever the tensor count (fedavg.py:23-25).  Stream-ordered like any torch op.
 
     The host work around the launch is batched (a 16-model ResNet-34 round spent 2 ms
-    of Python around a 0.13 ms reduce): the result's parameters are views of ONE device allocation
-    (each 256-byte aligned, as the table kernel wants), so the reduce is launched right after the walk;
-    models[0]'s device buffers are copied by one gather kernel per dtype into another allocation
-    (torch's flatten / unflatten of dense tensors) instead of one deepcopy dispatch per buffer; the
-    module tree is cloned while the kernel runs."""
+    of Python around a 0.13 ms reduce): the result's parameters are made natively before the launch
+    (walk.cpp param_fresh: one caching-allocator tensor each, as deepcopy makes them, so record_stream
+    and CUDA IPC work on the result — round 6; rounds 4-5 made them parts of one allocation the
+    allocator did not know); models[0]'s device buffers are copied by one fused copy per dtype instead
+    of one deepcopy dispatch per buffer; the module tree is cloned while the kernel runs."""
     dtype, device, numels, table = layout
     mod = _lib.walk_module()
-    if mod is None:
+    if mod is None or not hasattr(mod, "param_fresh"):
         return _device_round_per_tensor(models, weights, layout)
-    offs, total, byte_offs, nums = _flat_plan(dtype, numels)
-    flat = torch.empty(total, dtype=dtype, device=device)
-    ptrs = (ctypes.c_void_p * table.size).from_buffer(table)
-    outs = (ctypes.c_void_p * len(numels)).from_buffer(byte_offs + flat.data_ptr())
-    _wsum.wsum_multi_ptrs(dtype, ptrs, outs, nums, weights, device, total_elems=sum(numels))
-    # models[0]'s own objects, checked after the launch (the GPU starts sooner; a tree the result cannot be
-    # built over leaves `flat` unused, and the per-tensor path launches into its own tensors)
     objs = mod.tensors(models[0], _PLAIN_SET)
     if objs is None or len(objs[0]) != len(numels) or any(type(p) is not nn.Parameter for p in objs[0]):
         return _device_round_per_tensor(models, weights, layout)
     p0, b0 = objs
-    # while the reduce runs: the result's parameters over `flat` (nn.Parameter views made natively: what
-    # torch.Tensor._make_subclass(nn.Parameter, flat.as_strided(...), requires_grad) makes), models[0]'s
-    # buffers, the module tree
+    nums = _flat_plan(dtype, numels)[3]
     memo = {}
-    mod.param_views(flat, p0, offs, memo)
+    outs = (ctypes.c_void_p * len(numels)).from_buffer(mod.param_fresh(p0, memo))
+    ptrs = (ctypes.c_void_p * table.size).from_buffer(table)
+    _wsum.wsum_multi_ptrs(dtype, ptrs, outs, nums, weights, device, total_elems=sum(numels))
+    # while the reduce runs: models[0]'s buffers, the module tree
     _seed_buffers(b0, memo)
     return _clone_value(models[0], memo)
 
@@ -494,9 +488,15 @@ def _device_round_grouped(models: List[nn.Module], weights) -> "nn.Module | None
     if first is None:
         return None
     dtype, device, numels, table = first
-    offs, total, byte_offs, nums = _flat_plan(dtype, numels)
-    flat = torch.empty(total, dtype=dtype, device=device)
-    outs = (ctypes.c_void_p * len(numels)).from_buffer(byte_offs + flat.data_ptr())
+    # models[0]'s own objects and the result's fresh parameters (walk.cpp param_fresh), before the first
+    # launch writes into them
+    objs = mod.tensors(models[0], _PLAIN_SET) if hasattr(mod, "param_fresh") else None
+    if objs is None or len(objs[0]) != len(numels) or any(type(p) is not nn.Parameter for p in objs[0]):
+        return None
+    p0, b0 = objs
+    nums = _flat_plan(dtype, numels)[3]
+    memo = {}
+    outs = (ctypes.c_void_p * len(numels)).from_buffer(mod.param_fresh(p0, memo))
     _wsum.wsum_multi_ptrs(dtype, (ctypes.c_void_p * table.size).from_buffer(table), outs, nums,
                           weights[a0:b0_], device, total_elems=sum(numels))
     for a, b in bounds[1:]:
@@ -506,14 +506,6 @@ def _device_round_grouped(models: List[nn.Module], weights) -> "nn.Module | None
             return None
         _wsum.wsum_multi_ptrs(dtype, (ctypes.c_void_p * lay[3].size).from_buffer(lay[3]), outs, nums,
                               weights[a:b], device, acc_in=True)
-    # models[0]'s own objects, listed after the launches (the GPU starts sooner; a tree the result cannot
-    # be built over leaves `flat` unused and the general path handles the round)
-    objs = mod.tensors(models[0], _PLAIN_SET)
-    if objs is None or len(objs[0]) != len(numels) or any(type(p) is not nn.Parameter for p in objs[0]):
-        return None
-    p0, b0 = objs
-    memo = {}
-    mod.param_views(flat, p0, offs, memo)
     _seed_buffers(b0, memo)
     return _clone_value(models[0], memo)
 

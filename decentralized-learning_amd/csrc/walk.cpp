@@ -307,13 +307,41 @@ void param_views(const at::Tensor& flat, py::list params, const std::vector<int6
   }
 }
 
+// The result module's fresh parameters of a device round (fedavg._device_round: deepcopy(models[0]) of
+// fedavg.py:20, the reduce writing into them): for each of models[0]'s parameters p, an nn.Parameter over
+// a NEW tensor from the device's caching allocator with p's sizes, strides and dtype and p's
+// requires_grad — a storage of its own from the allocator, as deepcopy gives, so Tensor.record_stream,
+// CUDA IPC and pickling behave exactly as for a deepcopy (round 6; rounds 4-5 made
+// them aliases of one allocation, which the allocator did not know) — stored into the deepcopy memo as
+// memo[id(p)].  Returns their data pointers (the reduce's outputs), one uint64 each.  One TensorImpl and
+// one allocator call per parameter, no Python frame.
+py::array_t<uint64_t> param_fresh(py::list params, py::dict memo) {
+  const py::ssize_t n = PyList_GET_SIZE(params.ptr());
+  py::array_t<uint64_t> ptrs(n);
+  uint64_t* out = ptrs.mutable_data();
+  for (py::ssize_t i = 0; i < n; ++i) {
+    PyObject* o = PyList_GET_ITEM(params.ptr(), i);
+    if (!THPVariable_Check(o)) throw std::invalid_argument("param_fresh: not a tensor");
+    const at::Tensor& p = THPVariable_Unpack(o);
+    at::Tensor v = at::empty_strided(p.sizes(), p.strides(), at::TensorOptions().dtype(p.scalar_type()).device(p.device()));
+    v.set_requires_grad(p.requires_grad());
+    out[i] = reinterpret_cast<uint64_t>(v.data_ptr());
+    py::object w = py::reinterpret_steal<py::object>(THPVariable_Wrap(v, reinterpret_cast<PyTypeObject*>(ParameterClass)));
+    if (!w) throw py::error_already_set();
+    py::object id = py::reinterpret_steal<py::object>(PyLong_FromVoidPtr(o));
+    if (!id || PyDict_SetItem(memo.ptr(), id.ptr(), w.ptr()) < 0) throw py::error_already_set();
+  }
+  return ptrs;
+}
+
 // deepcopy of models[0]'s device buffers (fedavg.py:20 copies them, it does not average them) in one
-// gather per (device, dtype), stored into the deepcopy memo: for each entry of `buffers` not already in
-// `memo`, memo[id(buffer)] = a copy that is a view of one fresh allocation per group (views made first,
-// then one fused multi-tensor copy into them).  Entries that are not plain dense CPU or CUDA tensors
-// without grad, alone in their group, or sharing a storage with another buffer get no entry (the caller's
-// deepcopy copies them, keeping the sharing).  Replaces a Python pass over every buffer (108 BN buffers
-// of a google_speech ResNet-34: ~0.15 ms per round).
+// fused copy per (device, dtype), stored into the deepcopy memo: for each entry of `buffers` not already in
+// `memo`, memo[id(buffer)] = a fresh tensor from the device's allocator (a storage of its own, as deepcopy
+// gives: record_stream and IPC work on it; rounds 4-5 made the copies views of one allocation per group),
+// all of a group filled by ONE fused multi-tensor copy.  Entries that are not plain dense CPU or CUDA
+// tensors without grad, alone in their group, or sharing a storage with another buffer get no entry (the
+// caller's deepcopy copies them, keeping the sharing).  Replaces a Python pass over every buffer (108 BN
+// buffers of a google_speech ResNet-34: ~0.15 ms per round).
 void buffer_copies(py::list buffers, py::dict memo) {
   const py::ssize_t n = PyList_GET_SIZE(buffers.ptr());
   std::vector<std::pair<int, int>> keys;  // (device index, scalar type) of each group
@@ -351,20 +379,13 @@ void buffer_copies(py::list buffers, py::dict memo) {
   }
   for (const auto& mem : members) {
     if (mem.size() < 2) continue;
-    // one allocation, a contiguous view of it per buffer, then ONE fused multi-tensor copy
+    // a fresh allocator tensor per buffer, then ONE fused multi-tensor copy
     std::vector<at::Tensor> srcs, dsts;
     srcs.reserve(mem.size());
     dsts.reserve(mem.size());
-    int64_t total = 0;
     for (py::ssize_t i : mem) {
       srcs.push_back(THPVariable_Unpack(PyList_GET_ITEM(buffers.ptr(), i)));
-      total += srcs.back().numel();
-    }
-    const at::Tensor flat = at::empty({total}, srcs[0].options());
-    int64_t off = 0;
-    for (const at::Tensor& t : srcs) {
-      dsts.push_back(alias_of(flat, t.sizes(), t.strides(), off));  // contiguous source: contiguous strides
-      off += t.numel();
+      dsts.push_back(at::empty_strided(srcs.back().sizes(), srcs.back().strides(), srcs.back().options()));
     }
     at::_foreach_copy_(dsts, srcs);
     for (size_t j = 0; j < mem.size(); ++j) {
@@ -1293,6 +1314,7 @@ PYBIND11_MODULE(_dla_walk, m) {
   m.def("block_table", &block_table, py::arg("blocks"));
   m.def("fingerprint", &fingerprint, py::arg("model"), py::arg("plain"));
   m.def("param_views", &param_views, py::arg("flat"), py::arg("params"), py::arg("offsets"), py::arg("memo"));
+  m.def("param_fresh", &param_fresh, py::arg("params"), py::arg("memo"));
   m.def("buffer_copies", &buffer_copies, py::arg("buffers"), py::arg("memo"));
   m.def("clone_value", &clone_value, py::arg("v"), py::arg("memo"), py::arg("atomic"), py::arg("modules"),
         py::arg("fallback"), py::arg("odict"));

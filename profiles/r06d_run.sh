@@ -1,6 +1,7 @@
 #!/bin/bash
 # r06d: staged-on-arrival rows with the native parameter fingerprint, the call-site
-# tests through DeviceModelManager, and the granularity probe with the staggered-contiguous variant.
+# tests through DeviceModelManager, allocator-visible device results (the whole GPU suite), and the
+# granularity probe with the staggered-contiguous variant.
 set -o pipefail
 export TMPDIR=/tmp
 out=gpurun_out/r06d
@@ -14,6 +15,6 @@ run() {
   case $rc in 124|137|134|139) exit $rc;; esac
   return 0
 }
-run 600 python -u -m pytest tests/test_call_sites.py tests/test_fuzz_model_manager.py tests/test_wire.py -m gpu -x -q --timeout 300 --timeout-method thread -rs > $out/gpu_tests.log 2>&1
+run 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -rs > $out/gpu_tests.log 2>&1
 run 300 python -u profiles/r06_granularity_probe.py > $out/granularity.jsonl 2> $out/granularity.err
 run 900 python -u bench.py > $out/bench.log 2>&1

@@ -793,9 +793,17 @@ def test_walk_memo_seeding_on_cpu():
     for x in (a, b, c, d):
         y = memo[id(x)]
         assert torch.equal(x, y) and y.dtype == x.dtype and y.data_ptr() != x.data_ptr()
-    # one allocation per (device, dtype) group, a storage of its own per copy
-    assert memo[id(b)].data_ptr() == memo[id(a)].data_ptr() + 16 and memo[id(d)].data_ptr() == memo[id(c)].data_ptr() + 24
+    # (round 6) a fresh allocator tensor per copy, as deepcopy gives: a storage of its own at its own address
     assert [memo[id(x)].untyped_storage().nbytes() for x in (a, b, c, d)] == [16, 24, 24, 16]
+    assert all(memo[id(x)].untyped_storage().data_ptr() == memo[id(x)].data_ptr() for x in (a, b, c, d))
+    # param_fresh: the device round's fresh parameters, one allocator tensor each, their pointers returned
+    pf = [nn.Parameter(torch.randn(3, 4)), nn.Parameter(torch.randn(5), requires_grad=False)]
+    fm = {}
+    ptrs = mod.param_fresh(pf, fm)
+    f0, f1 = fm[id(pf[0])], fm[id(pf[1])]
+    assert type(f0) is nn.Parameter and f0.shape == (3, 4) and f0.stride() == (4, 1) and f0.requires_grad
+    assert not f1.requires_grad and list(ptrs) == [f0.data_ptr(), f1.data_ptr()]
+    assert f0.untyped_storage().nbytes() == 48 and f0.untyped_storage().data_ptr() == f0.data_ptr()
     import numpy as np
 
     pooled = torch.from_numpy(np.arange(8, dtype=np.float32))  # memory torch did not allocate

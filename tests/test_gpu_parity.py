@@ -1485,28 +1485,51 @@ def test_multi_table_back_to_back_rounds_reuse_slots_safely(dtype):
 
 
 def test_device_result_record_stream_and_sharing():
-    """The result of a device round: its parameters are parts of one allocation, each with a storage of
-    its own (walk.cpp alias_of).  Pinned here as INTEGRATION.md §2 documents it:
-    record_stream on a result parameter is accepted (and a no-op: the caching allocator skips memory it
-    did not hand out), every parameter pickles only its own bytes, and state_dict clones are ordinary
-    allocator tensors (what a caller sends to another process instead)."""
+    """The result of a device round is deepcopy(models[0]) (fedavg.py:20) down to its memory: every parameter
+    and buffer is a tensor of its own from the device's caching allocator (round 6, VERDICT r05 next 5;
+    rounds 4-5 made them parts of one allocation the allocator did not know, so record_stream was a silent
+    no-op).  Here record_stream PROTECTS a result parameter: used on a side stream and dropped, its memory is
+    not handed to the next allocation until the side stream has passed, and the side stream reads the
+    average, not what the next owner writes.  Every parameter pickles only its own bytes."""
     import pickle
 
     from accdfl_amd.core.gradient_aggregation.fedavg import FedAvg
 
-    models = [torch.nn.Sequential(torch.nn.Linear(300, 200), torch.nn.Linear(200, 10)).cuda() for _ in range(3)]
+    torch.manual_seed(3)
+    models = [torch.nn.Sequential(torch.nn.Linear(1024, 512), torch.nn.BatchNorm1d(512)).cuda() for _ in range(3)]
     out = FedAvg.aggregate(models, None)
-    side = torch.cuda.Stream()
-    for p in out.parameters():
-        p.record_stream(side)  # accepted
+    torch.cuda.synchronize()
+    assert out[0].weight.data_ptr() not in {m[0].weight.data_ptr() for m in models}
     sizes = [p.untyped_storage().nbytes() for p in out.parameters()]
     assert sizes == [p.numel() * p.element_size() for p in out.parameters()]
+    assert [p.untyped_storage().data_ptr() for p in out.parameters()] == [p.data_ptr() for p in out.parameters()]
     cpu = {k: v.cpu() for k, v in out.state_dict().items()}
     assert len(pickle.dumps(cpu)) == len(pickle.dumps({k: v.cpu() for k, v in models[0].state_dict().items()}))
-    clones = {k: v.clone() for k, v in out.state_dict().items()}
-    for k, v in clones.items():
-        assert v.untyped_storage().data_ptr() == v.data_ptr() and torch.equal(v, out.state_dict()[k])
+    want = out[0].weight.detach().clone()
+    n = want.numel()
+    # control: the allocator hands a freed block of this size straight to the next allocation on the stream
+    t = torch.empty(n, device="cuda")
+    ptr = t.data_ptr()
+    del t
+    t = torch.empty(n, device="cuda")
+    if t.data_ptr() != ptr:
+        pytest.skip("the caching allocator did not reuse a freed block here: the check below would prove nothing")
+    del t
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    dst = torch.empty(n, device="cuda")
+    w = out[0].weight
+    ptr = w.data_ptr()
+    with torch.cuda.stream(side):
+        torch.cuda._sleep(50_000_000)  # the side stream is busy ~ tens of ms before it reads the result
+        dst.copy_(w.detach().view(-1))
+    w.record_stream(side)
+    del w, out
+    junk = torch.empty(n, device="cuda")  # the current stream's next allocation of that size
+    assert junk.data_ptr() != ptr, "record_stream on a result parameter must keep its block from reuse"
+    junk.fill_(float("nan"))
     torch.cuda.synchronize()
+    assert torch.equal(dst.view_as(want), want)
 
 
 def test_grouped_device_round_with_a_late_mixed_dtype_model():
