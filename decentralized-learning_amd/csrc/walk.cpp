@@ -319,11 +319,32 @@ py::array_t<uint64_t> param_fresh(py::list params, py::dict memo) {
   const py::ssize_t n = PyList_GET_SIZE(params.ptr());
   py::array_t<uint64_t> ptrs(n);
   uint64_t* out = ptrs.mutable_data();
+  // the device's caching allocator itself (what at::empty calls after the dispatcher): one allocate() per
+  // parameter, its DataPtr — the allocator's own deleter and context, so record_stream finds the block —
+  // made into a storage and a TensorImpl here; ~0.5 us per parameter less than at::empty_strided
+  c10::optional<c10::DeviceGuard> guard;
+  at::Allocator* dev_alloc = nullptr;
+  c10::DispatchKeySet keys;
   for (py::ssize_t i = 0; i < n; ++i) {
     PyObject* o = PyList_GET_ITEM(params.ptr(), i);
     if (!THPVariable_Check(o)) throw std::invalid_argument("param_fresh: not a tensor");
     const at::Tensor& p = THPVariable_Unpack(o);
-    at::Tensor v = at::empty_strided(p.sizes(), p.strides(), at::TensorOptions().dtype(p.scalar_type()).device(p.device()));
+    at::Tensor v;
+    if (p.is_cuda() && p.is_contiguous() && p.layout() == at::kStrided) {
+      if (!guard || guard->current_device() != p.device()) {
+        guard.emplace(p.device());
+        dev_alloc = c10::GetAllocator(p.device().type());
+        keys = at::empty({0}, p.options().requires_grad(false)).key_set();
+      }
+      const size_t nbytes = static_cast<size_t>(p.numel()) * p.element_size();
+      c10::Storage st(c10::Storage::use_byte_size_t(), nbytes, dev_alloc->allocate(nbytes), dev_alloc,
+                      /*resizable=*/true);
+      auto impl = c10::make_intrusive<c10::TensorImpl>(std::move(st), keys, p.dtype());
+      impl->set_sizes_and_strides(p.sizes(), p.strides(), 0);
+      v = at::Tensor(std::move(impl));
+    } else {
+      v = at::empty_strided(p.sizes(), p.strides(), at::TensorOptions().dtype(p.scalar_type()).device(p.device()));
+    }
     v.set_requires_grad(p.requires_grad());
     out[i] = reinterpret_cast<uint64_t>(v.data_ptr());
     py::object w = py::reinterpret_steal<py::object>(THPVariable_Wrap(v, reinterpret_cast<PyTypeObject*>(ParameterClass)));

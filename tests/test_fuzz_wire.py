@@ -128,14 +128,48 @@ def test_wire_fuzz(seed):
 
 
 @pytest.mark.parametrize("numel", [1, 5, 1000])
-def test_tied_device_source_pickles_once(numel):
-    """One small DeviceSource (< 64 KiB: encoded through the CPU) listed under two keys (a tied parameter
-    of the averaged model): pickle.dumps of the equivalent dict ties the two entries, so the payload must
-    too.  (The large, out-of-band form is memoized by its placeholder and covered on the GPU.)"""
+@pytest.mark.parametrize("path", ["template", "general"])
+def test_tied_device_source_pickles_once(numel, path):
+    """One small DeviceSource (< 64 KiB) listed under two keys (a tied parameter of the averaged model):
+    pickle.dumps of the equivalent dict ties the two entries, so the payload must too — through the layout
+    template, and through the general path (an entry that is a view forces it; the small DeviceSource is
+    then encoded through the CPU, once)."""
     flat = torch.arange(numel + 3, dtype=torch.float32)
     src = wire.DeviceSource(flat, 3, (numel,))
     sd = OrderedDict([("a", src), ("b", src), ("c", torch.ones(2))])
+    if path == "general":
+        sd["d"] = torch.randn(4, 4)[1:]
+    assert (wire._template_plan(sd) is None) == (path == "general")
     got = pickle.loads(wire.dumps_state_dict(sd))
-    assert list(got) == ["a", "b", "c"]
+    assert list(got) == list(sd)
     assert torch.equal(got["a"], flat[3:]) and torch.equal(got["b"], flat[3:])
     assert got["a"].untyped_storage().data_ptr() == got["b"].untyped_storage().data_ptr()
+
+
+def test_payload_template_is_reused_across_rounds():
+    """dumps_state_dict's layout template (round 6): the same layout encoded round after round with new
+    values decodes — with the reference's own pickle.loads — to exactly that round's state dict (values,
+    dtypes, shapes, ties, _metadata); one template per layout; a layout with a view takes the general
+    path."""
+    from torch import nn
+
+    m = nn.Sequential(nn.Conv2d(3, 4, 3), nn.BatchNorm2d(4), nn.Linear(4, 2)).to(torch.bfloat16)
+    wire._TEMPLATES.clear()
+    for r in range(3):
+        with torch.no_grad():
+            for p in m.parameters():
+                p.add_(1.0)
+            m[1].running_mean.add_(r)
+        sd = m.state_dict()
+        sd["tied"] = sd["0.weight"]
+        got = pickle.loads(wire.dumps_state_dict(sd))
+        assert list(got) == list(sd)
+        for k in sd:
+            _same(sd[k], got[k], "round %d entry %s" % (r, k))
+        assert got["tied"] is got["0.weight"]
+        assert got._metadata == sd._metadata
+    assert len(wire._TEMPLATES) == 1
+    view = OrderedDict(a=torch.randn(4, 4)[1:], b=torch.randn(3))
+    assert wire._template_plan(view) is None
+    got = pickle.loads(wire.dumps_state_dict(view))
+    _same(view["a"], got["a"], "view")

@@ -449,8 +449,8 @@ def test_device_modules_of_real_layouts_through_fedavg(name, n, dtype):
 
 
 def test_device_round_result_pickles_like_a_deepcopy():
-    """The device round's result (parameters and buffer copies over one allocation each, walk.cpp
-    alias_of) has a storage per tensor, as deepcopy(models[0]) does: the reference's serialize_model
+    """The device round's result (parameters and buffer copies: one caching-allocator tensor each since
+    round 6, walk.cpp param_fresh / buffer_copies) has a storage per tensor, as deepcopy(models[0]) does: the reference's serialize_model
     (pickle.dumps(state_dict()), accdfl/core/models/__init__.py:9-10) writes each tensor's bytes once,
     not the whole allocation per tensor, and the payload decodes to the result's values."""
     import copy
@@ -478,7 +478,8 @@ def test_device_round_result_pickles_like_a_deepcopy():
         assert torch.equal(back[k], v), k
     ptrs = [p.data_ptr() for p in out.parameters()]
     assert len({p.untyped_storage().data_ptr() for p in out.parameters()}) == len(ptrs)  # a storage each
-    assert all(b - a > 0 for a, b in zip(ptrs, ptrs[1:]))  # over one allocation, in order
+    # (round 6) each from the device's caching allocator, as deepcopy makes them
+    assert all(p.untyped_storage().data_ptr() == p.data_ptr() for p in out.parameters())
 
 
 @pytest.mark.parametrize("dtype", ["f32", "bf16", "f64"])
