@@ -183,7 +183,7 @@ def _rccl_worker(rank, world, port, n_peers, n_elems, root, q, dtype, backend="n
         dev = torch.device("cuda", rank)
         torch.cuda.set_device(dev)
         dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
-    else:
+    else:  # "gloo": CPU tensors, the oracle reducer; "gloo-hip": CPU tensors, the libdlagg reducer on cuda:0
         dev = torch.device("cpu")
         dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -193,7 +193,7 @@ def _rccl_worker(rank, world, port, n_peers, n_elems, root, q, dtype, backend="n
         weights = [float(x) for x in np.random.default_rng(n_peers).dirichlet(np.ones(n_peers))]
         # RCCL: the libdlagg reducer (the sharding module's default)
         sh = BucketShardedFedAvg(n_elems, _TORCH[dtype], device=dev,
-                                 reducer=None if backend == "nccl" else _oracle_reducer(dtype))
+                                 reducer={"nccl": None, "gloo": _oracle_reducer(dtype), "gloo-hip": _hip_reducer}[backend])
         s, e = sh.local_range
         mine = _hashed_rows(range(n_peers), s, e, dtype)
         want = c_wsum(list(_to_bits(mine, dtype)) if dtype == "bf16" else list(mine.numpy()), weights, dtype)
@@ -244,6 +244,17 @@ def test_config_split_rehearsal_on_cpu(world, n_peers, n_elems, dtype):
     """The full-size RCCL cases' worker, its per-rank oracle check and the digest agreement, rehearsed
     over gloo on the CPU at the same world sizes and peer counts (1/500 and 1/1000 of the elements)."""
     _run_config_split(world, n_peers, n_elems, dtype, "gloo")
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("world,n_peers,n_elems,dtype", [(4, 64, 4_932_344, "f32"), (8, 128, 21_296_355, "bf16")])
+def test_config_split_full_size_hip_reducer_over_gloo(world, n_peers, n_elems, dtype):
+    """configs[3] and configs[4]'s splits at FULL model size on the one-GPU box: the same ranks, exchanges
+    and per-rank oracle check as the RCCL case, the collectives over gloo and every rank's bucket reduced by
+    the libdlagg kernel on the box's one GPU (the 8-rank HIP-reducer cases ran 1 M
+    elements per model, not configs[4]'s 21 296 355)."""
+    _run_config_split(world, n_peers, n_elems, dtype, "gloo-hip")
 
 
 def _run_config_split(world, n_peers, n_elems, dtype, backend):
