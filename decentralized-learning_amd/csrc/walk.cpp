@@ -333,8 +333,13 @@ py::array_t<uint64_t> param_fresh(py::list params, py::dict memo) {
     if (p.is_cuda() && p.is_contiguous() && p.layout() == at::kStrided) {
       if (!guard || guard->current_device() != p.device()) {
         guard.emplace(p.device());
-        dev_alloc = c10::GetAllocator(p.device().type());
-        keys = at::empty({0}, p.options().requires_grad(false)).key_set();
+        // the allocator torch's own device tensors come from (on ROCm, the HIP caching allocator behind
+        // the wrapper that labels its memory "cuda"; c10::GetAllocator(kCUDA) is the unwrapped one) and
+        // the dispatch keys of a plain device tensor
+        const at::Tensor probe = at::empty({0}, p.options().requires_grad(false));
+        dev_alloc = probe.storage().allocator();
+        keys = probe.key_set();
+        if (!dev_alloc) throw std::runtime_error("param_fresh: no device allocator");
       }
       const size_t nbytes = static_cast<size_t>(p.numel()) * p.element_size();
       c10::Storage st(c10::Storage::use_byte_size_t(), nbytes, dev_alloc->allocate(nbytes), dev_alloc,
