@@ -284,6 +284,38 @@ at::Tensor alias_of(const at::Tensor& flat, at::IntArrayRef sizes, at::IntArrayR
   return at::Tensor(std::move(impl));
 }
 
+// Fresh tensors like a given one (sizes, strides, dtype, device; no data) straight from the allocator torch's
+// own tensors of that device come from — one allocate() and one TensorImpl each, no dispatched op (~0.6 us
+// a tensor less than at::empty_strided).  The DataPtr is the allocator's own (its deleter and context), so
+// the caching allocator knows the block: record_stream and CUDA IPC work as on any torch tensor.  Dense
+// device tensors only; anything else through at::empty_strided.
+class FreshAlloc {
+ public:
+  at::Tensor like(const at::Tensor& p) {
+    if (!(p.is_cuda() && p.is_contiguous() && p.layout() == at::kStrided))
+      return at::empty_strided(p.sizes(), p.strides(), at::TensorOptions().dtype(p.scalar_type()).device(p.device()));
+    if (!guard_ || guard_->current_device() != p.device()) {
+      guard_.emplace(p.device());
+      // on ROCm the allocator behind the wrapper that labels its memory "cuda" (c10::GetAllocator(kCUDA)
+      // is the unwrapped HIP one, whose tensors would say "hip"), and a plain device tensor's dispatch keys
+      const at::Tensor probe = at::empty({0}, at::TensorOptions().dtype(p.scalar_type()).device(p.device()));
+      alloc_ = probe.storage().allocator();
+      keys_ = probe.key_set();
+      if (!alloc_) throw std::runtime_error("walk: no device allocator");
+    }
+    const size_t nbytes = static_cast<size_t>(p.numel()) * p.element_size();
+    c10::Storage st(c10::Storage::use_byte_size_t(), nbytes, alloc_->allocate(nbytes), alloc_, /*resizable=*/true);
+    auto impl = c10::make_intrusive<c10::TensorImpl>(std::move(st), keys_, p.dtype());
+    impl->set_sizes_and_strides(p.sizes(), p.strides(), 0);
+    return at::Tensor(std::move(impl));
+  }
+
+ private:
+  c10::optional<c10::DeviceGuard> guard_;
+  at::Allocator* alloc_ = nullptr;
+  c10::DispatchKeySet keys_;
+};
+
 // The result module's fresh parameters of a device round (fedavg._device_round: deepcopy(models[0]) of
 // fedavg.py:20 with every parameter over part of ONE allocation the reduce writes): for each of
 // models[0]'s parameters p and its element offset in `flat`, an nn.Parameter over alias_of(flat, p's
@@ -319,37 +351,12 @@ py::array_t<uint64_t> param_fresh(py::list params, py::dict memo) {
   const py::ssize_t n = PyList_GET_SIZE(params.ptr());
   py::array_t<uint64_t> ptrs(n);
   uint64_t* out = ptrs.mutable_data();
-  // the device's caching allocator itself (what at::empty calls after the dispatcher): one allocate() per
-  // parameter, its DataPtr — the allocator's own deleter and context, so record_stream finds the block —
-  // made into a storage and a TensorImpl here; ~0.5 us per parameter less than at::empty_strided
-  c10::optional<c10::DeviceGuard> guard;
-  at::Allocator* dev_alloc = nullptr;
-  c10::DispatchKeySet keys;
+  FreshAlloc fresh;
   for (py::ssize_t i = 0; i < n; ++i) {
     PyObject* o = PyList_GET_ITEM(params.ptr(), i);
     if (!THPVariable_Check(o)) throw std::invalid_argument("param_fresh: not a tensor");
     const at::Tensor& p = THPVariable_Unpack(o);
-    at::Tensor v;
-    if (p.is_cuda() && p.is_contiguous() && p.layout() == at::kStrided) {
-      if (!guard || guard->current_device() != p.device()) {
-        guard.emplace(p.device());
-        // the allocator torch's own device tensors come from (on ROCm, the HIP caching allocator behind
-        // the wrapper that labels its memory "cuda"; c10::GetAllocator(kCUDA) is the unwrapped one) and
-        // the dispatch keys of a plain device tensor
-        const at::Tensor probe = at::empty({0}, p.options().requires_grad(false));
-        dev_alloc = probe.storage().allocator();
-        keys = probe.key_set();
-        if (!dev_alloc) throw std::runtime_error("param_fresh: no device allocator");
-      }
-      const size_t nbytes = static_cast<size_t>(p.numel()) * p.element_size();
-      c10::Storage st(c10::Storage::use_byte_size_t(), nbytes, dev_alloc->allocate(nbytes), dev_alloc,
-                      /*resizable=*/true);
-      auto impl = c10::make_intrusive<c10::TensorImpl>(std::move(st), keys, p.dtype());
-      impl->set_sizes_and_strides(p.sizes(), p.strides(), 0);
-      v = at::Tensor(std::move(impl));
-    } else {
-      v = at::empty_strided(p.sizes(), p.strides(), at::TensorOptions().dtype(p.scalar_type()).device(p.device()));
-    }
+    at::Tensor v = fresh.like(p);
     v.set_requires_grad(p.requires_grad());
     out[i] = reinterpret_cast<uint64_t>(v.data_ptr());
     py::object w = py::reinterpret_steal<py::object>(THPVariable_Wrap(v, reinterpret_cast<PyTypeObject*>(ParameterClass)));
@@ -409,9 +416,10 @@ void buffer_copies(py::list buffers, py::dict memo) {
     std::vector<at::Tensor> srcs, dsts;
     srcs.reserve(mem.size());
     dsts.reserve(mem.size());
+    FreshAlloc fresh;
     for (py::ssize_t i : mem) {
       srcs.push_back(THPVariable_Unpack(PyList_GET_ITEM(buffers.ptr(), i)));
-      dsts.push_back(at::empty_strided(srcs.back().sizes(), srcs.back().strides(), srcs.back().options()));
+      dsts.push_back(fresh.like(srcs.back()));
     }
     at::_foreach_copy_(dsts, srcs);
     for (size_t j = 0; j < mem.size(); ++j) {

@@ -1,0 +1,21 @@
+#!/bin/bash
+# r06g: device-result buffers through the same allocator path as the parameters (walk.cpp FreshAlloc):
+# whole GPU suite + smoke, what the allocator-visible result costs (profiles/r06_result_alloc_probe.py),
+# the default bench.
+set -o pipefail
+export TMPDIR=/tmp
+out=gpurun_out/r06g
+mkdir -p $out
+run() {
+  local t=$1; shift
+  echo "$(date +%T) start: $*" >> $out/steps.log
+  timeout -k 10 "$t" "$@"
+  local rc=$?
+  echo "$(date +%T) rc=$rc: $*" >> $out/steps.log
+  case $rc in 124|137|134|139) exit $rc;; esac
+  return 0
+}
+run 900 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread -rs > $out/gpu_tests.log 2>&1
+run 120 python -u -c "import __graft_entry__ as g; g.smoke()" > $out/smoke.log 2>&1
+run 300 python -u profiles/r06_result_alloc_probe.py > $out/result_alloc.jsonl 2> $out/result_alloc.err
+run 900 python -u bench.py > $out/bench.log 2>&1
