@@ -537,8 +537,9 @@ def loads_state_dict(data, copy: bool = True, alloc: Optional[Callable[[int], to
         clones = collections.OrderedDict((k, v.clone()) for k, v in obj.items())
         storages = [v.untyped_storage().data_ptr() for v in obj.values() if v.numel()]
         # a clone is exact only for a tensor that is the whole of its own storage: same strides, offset 0,
-        # and the storage no larger than the tensor (pickle.loads keeps a view's storage and offset)
-        if len(set(storages)) == len(storages) and all(
+        # and the storage no larger than the tensor (pickle.loads keeps a view's storage and offset), and
+        # listed once (pickle.loads keeps one object under both keys, empty tensors included)
+        if len(set(storages)) == len(storages) and len({id(v) for v in obj.values()}) == len(obj) and all(
                 c.numel() == 0 or (c.stride() == v.stride() and v.storage_offset() == 0
                                    and v.untyped_storage().nbytes() == v.numel() * v.element_size())
                 for c, v in zip(clones.values(), obj.values())):
@@ -596,7 +597,7 @@ class StateDictScan:
         return _lib.walk_module().build_state_dict(buf, offsets.astype(np.int64), self.entries, self.storages,
                                                    collections.OrderedDict)
 
-    def row_layout(self, names: Sequence[str], dtype: torch.dtype, shapes: Sequence[tuple]):
+    def row_layout(self, names: Sequence[str], dtype: torch.dtype, shapes: Sequence[tuple], native: bool = True):
         """Where a PeerSlab row's parameters can come from in one piece: when the entries ``names``
         (``template.named_parameters()`` order) are dense tensors of ``dtype`` and ``shapes``, each the
         whole of a storage of its own, ``(offsets, total bytes, row bytes)`` — a byte offset per storage
@@ -604,6 +605,12 @@ class StateDictScan:
         other storage after them, 256-byte aligned.  None otherwise (a missing key, a view, a shared or
         mis-typed storage): the caller decodes through the general path."""
         dname = str(dtype).replace("torch.", "")
+        from accdfl_amd import _lib
+
+        mod = _lib.walk_module()
+        if native and hasattr(mod, "row_layout"):  # csrc/walk.cpp: the same rules, no Python frame per parameter
+            return mod.row_layout(self.entries, self.storages, names if type(names) is list else list(names), dname,
+                                  shapes if type(shapes) is list else [tuple(s) for s in shapes])
         offsets = np.full(len(self.storages), -1, dtype=np.int64)
         off = 0
         for name, shape in zip(names, shapes):

@@ -805,6 +805,7 @@ struct Scanner {
   Blocks& blocks;
   PyObject* odict_cls;
   std::vector<StorageRec> storages;
+  std::string prefix;  // the first checked blob's magic / protocol / sys-info pickles, byte for byte
 
   bool is_tagged(PyObject* o, PyObject* tag, Py_ssize_t n) const {
     return PyTuple_CheckExact(o) && PyTuple_GET_SIZE(o) == n && PyTuple_GET_ITEM(o, 0) == tag;
@@ -1179,14 +1180,31 @@ struct Scanner {
     PyObject* objs[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
     int64_t idx = -1;
     bool ok = magic != nullptr;
-    for (int i = 0; ok && i < 5; ++i) ok = (objs[i] = run(m, true)) != nullptr;
+    // The first three pickles (magic number, protocol, sys info) are the same bytes in every blob one
+    // torch wrote: once a blob's have been checked, a blob that starts with the same bytes skips them (the
+    // sys-info dict is most of a header's objects: ~2 us -> ~1 us per tensor)
+    const bool same_prefix = !prefix.empty() && static_cast<size_t>(hn) >= prefix.size() &&
+                             std::memcmp(hp, prefix.data(), prefix.size()) == 0;
+    int64_t prefix_end = 0;
+    if (same_prefix) {
+      m.pos = static_cast<int64_t>(prefix.size());
+      for (int i = 3; ok && i < 5; ++i) ok = (objs[i] = run(m, true)) != nullptr;
+    } else {
+      for (int i = 0; ok && i < 5; ++i) {
+        ok = (objs[i] = run(m, true)) != nullptr;
+        if (i == 2) prefix_end = m.pos;
+      }
+    }
     if (ok) {
-      PyObject* le = PyDict_CheckExact(objs[2]) ? PyDict_GetItemString(objs[2], "little_endian") : nullptr;
       PyObject* ps = objs[3];
-      ok = PyObject_RichCompareBool(objs[0], magic, Py_EQ) == 1 && PyLong_CheckExact(objs[1]) &&
-           PyLong_AsLong(objs[1]) == 1001 && le == Py_True && is_tagged(ps, T.pstorage, 4) &&
-           PyList_CheckExact(objs[4]) && PyList_GET_SIZE(objs[4]) == 1 &&
+      if (!same_prefix) {
+        PyObject* le = PyDict_CheckExact(objs[2]) ? PyDict_GetItemString(objs[2], "little_endian") : nullptr;
+        ok = PyObject_RichCompareBool(objs[0], magic, Py_EQ) == 1 && PyLong_CheckExact(objs[1]) &&
+             PyLong_AsLong(objs[1]) == 1001 && le == Py_True;
+      }
+      ok = ok && is_tagged(ps, T.pstorage, 4) && PyList_CheckExact(objs[4]) && PyList_GET_SIZE(objs[4]) == 1 &&
            PyObject_RichCompareBool(PyList_GET_ITEM(objs[4], 0), PyTuple_GET_ITEM(ps, 2), Py_EQ) == 1;
+      if (ok && !same_prefix && prefix.empty()) prefix.assign(hp, static_cast<size_t>(prefix_end));
       unsigned char b[8];
       if (ok && m.read(reinterpret_cast<char*>(b), 8)) {
         uint64_t saved = 0;
@@ -1214,7 +1232,7 @@ py::object scan_state_dict(py::array_t<int64_t, py::array::c_style> addrs, py::a
                            py::object odict_cls) {
   if (addrs.size() != lens.size()) throw std::invalid_argument("scan_state_dict: one length per block");
   wirescan::Blocks blocks(addrs.data(), lens.data(), static_cast<int64_t>(lens.size()));
-  wirescan::Scanner sc{blocks, odict_cls.ptr(), {}};
+  wirescan::Scanner sc{blocks, odict_cls.ptr(), {}, {}};
   PyObject* top = sc.run(blocks, false);
   if (!top) {
     PyErr_Clear();
@@ -1230,6 +1248,59 @@ py::object scan_state_dict(py::array_t<int64_t, py::array::c_style> addrs, py::a
   for (const auto& r : sc.storages)
     st.append(py::make_tuple(wirescan::kStorageTypes[r.type].dtype, r.numel, r.data_pos, r.nbytes));
   return py::make_tuple(t, st);
+}
+
+// StateDictScan.row_layout in native code: where a PeerSlab row's parameters come from in one piece.  When
+// the entries `names` (template.named_parameters() order) are dense tensors of dtype `dtype` and the sizes
+// `shapes`, each the whole of a storage of its own (storage offset 0, row-major strides, numel = the
+// storage's), returns (byte offset of every storage — those parameters back to back from byte 0, every
+// other storage after them 256-byte aligned —, total bytes, row bytes); else None.
+py::object row_layout(py::dict top, py::list storages, py::list names, std::string dtype, py::list shapes) {
+  const py::ssize_t ns = PyList_GET_SIZE(storages.ptr());
+  const py::ssize_t nn = PyList_GET_SIZE(names.ptr());
+  if (PyList_GET_SIZE(shapes.ptr()) != nn) throw std::invalid_argument("row_layout: one shape per name");
+  py::array_t<int64_t> offsets(ns);
+  int64_t* off = offsets.mutable_data();
+  for (py::ssize_t i = 0; i < ns; ++i) off[i] = -1;
+  PyObject* tensor_tag = wirescan::tags().tensor;
+  int64_t o = 0;
+  for (py::ssize_t i = 0; i < nn; ++i) {
+    PyObject* d = PyDict_GetItemWithError(top.ptr(), PyList_GET_ITEM(names.ptr(), i));  // borrowed
+    if (!d) {
+      if (PyErr_Occurred()) throw py::error_already_set();
+      return py::none();
+    }
+    if (!PyTuple_CheckExact(d) || PyTuple_GET_SIZE(d) != 6 || PyTuple_GET_ITEM(d, 0) != tensor_tag)
+      return py::none();
+    const long long sidx = PyLong_AsLongLong(PyTuple_GET_ITEM(d, 1));
+    if (sidx < 0 || sidx >= ns || off[sidx] >= 0 || PyLong_AsLongLong(PyTuple_GET_ITEM(d, 2)) != 0) return py::none();
+    PyObject* size = PyTuple_GET_ITEM(d, 3);
+    PyObject* stride = PyTuple_GET_ITEM(d, 4);
+    PyObject* want = PyList_GET_ITEM(shapes.ptr(), i);
+    if (!PyTuple_Check(want) || PyTuple_GET_SIZE(want) != PyTuple_GET_SIZE(size)) return py::none();
+    const Py_ssize_t nd = PyTuple_GET_SIZE(size);
+    int64_t numel = 1, expect = 1;
+    for (Py_ssize_t k = nd - 1; k >= 0; --k) {  // sizes equal the shape's, strides row-major
+      const long long sz = PyLong_AsLongLong(PyTuple_GET_ITEM(size, k));
+      if (sz != PyLong_AsLongLong(PyTuple_GET_ITEM(want, k)) || PyLong_AsLongLong(PyTuple_GET_ITEM(stride, k)) != expect)
+        return py::none();
+      expect *= sz;
+      numel *= sz;
+    }
+    if (PyErr_Occurred()) throw py::error_already_set();
+    py::tuple rec = py::reinterpret_borrow<py::tuple>(PyList_GET_ITEM(storages.ptr(), sidx));
+    if (rec[0].cast<std::string>() != dtype || rec[1].cast<int64_t>() != numel) return py::none();
+    off[sidx] = o;
+    o += rec[3].cast<int64_t>();
+  }
+  const int64_t row = o;
+  o = (o + 255) / 256 * 256;
+  for (py::ssize_t i = 0; i < ns; ++i) {
+    if (off[i] >= 0) continue;
+    off[i] = o;
+    o += (py::reinterpret_borrow<py::tuple>(PyList_GET_ITEM(storages.ptr(), i))[3].cast<int64_t>() + 255) / 256 * 256;
+  }
+  return py::make_tuple(offsets, o > 0 ? o : 1, row);
 }
 
 // The copies that gather storages out of the payload: storage i's `nbytes[i]` bytes from stream position
@@ -1353,6 +1424,8 @@ PYBIND11_MODULE(_dla_walk, m) {
   m.def("clone_value", &clone_value, py::arg("v"), py::arg("memo"), py::arg("atomic"), py::arg("modules"),
         py::arg("fallback"), py::arg("odict"));
   m.def("scan_state_dict", &scan_state_dict, py::arg("addrs"), py::arg("lens"), py::arg("odict_cls"));
+  m.def("row_layout", &row_layout, py::arg("top"), py::arg("storages"), py::arg("names"), py::arg("dtype"),
+        py::arg("shapes"));
   m.def("span_pieces", &span_pieces, py::arg("addrs"), py::arg("lens"), py::arg("src_pos"), py::arg("nbytes"),
         py::arg("dst"));
   m.def("build_state_dict", &build_state_dict, py::arg("buf"), py::arg("offsets"), py::arg("top"),

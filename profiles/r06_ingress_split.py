@@ -27,6 +27,10 @@ def main():
     from accdfl_amd.core.model_manager import DeviceModelManager
 
     dev = torch.device("cuda", 0)
+    if "--numa-bind" in sys.argv:  # as bench.py does per rank: the gather's threads near the GPU's PCIe root
+        from accdfl_amd.core.host_memory import bind_to_gpu_node
+
+        bind_to_gpu_node(dev)
     n = 16
     models, p = bench._layout_models("google_speech_resnet34", n, torch.bfloat16, pinned=False, seed=4200)
     view = pickle.dumps({"peer%d" % j: j for j in range(16)})

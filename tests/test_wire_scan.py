@@ -175,14 +175,15 @@ def _resnet8_like():
     return m
 
 
-def test_row_layout_puts_the_parameters_back_to_back():
+@pytest.mark.parametrize("native", [True, False])
+def test_row_layout_puts_the_parameters_back_to_back(native):
     from accdfl_amd.core import wire
 
     m = _resnet8_like()
     names = [n for n, _ in m.named_parameters()]
     shapes = [tuple(p.shape) for p in m.parameters()]
     sc = wire.scan_state_dict(wire.payload_blocks(wire.serialize_model(m), 60_000))
-    offsets, total, row = sc.row_layout(names, torch.float32, shapes)
+    offsets, total, row = sc.row_layout(names, torch.float32, shapes, native=native)
     buf = torch.zeros(total, dtype=torch.uint8)
     sc.gather(buf, offsets)
     want = torch.cat([p.detach().reshape(-1) for p in m.parameters()])
@@ -194,23 +195,90 @@ def test_row_layout_puts_the_parameters_back_to_back():
     others = [i for i in range(len(sc.storages)) if i not in param_storages]
     assert len(others) == len(list(m.buffers())) and all(offsets[i] % 256 == 0 and offsets[i] >= row for i in others)
     # not a row: another dtype, another shape, a key the payload lacks
-    assert sc.row_layout(names, torch.bfloat16, shapes) is None
-    assert sc.row_layout(names, torch.float32, [shapes[0][::-1]] + shapes[1:]) is None
-    assert sc.row_layout(names + ["missing"], torch.float32, shapes + [(1,)]) is None
+    assert sc.row_layout(names, torch.bfloat16, shapes, native=native) is None
+    assert sc.row_layout(names, torch.float32, [shapes[0][::-1]] + shapes[1:], native=native) is None
+    assert sc.row_layout(names + ["missing"], torch.float32, shapes + [(1,)], native=native) is None
 
 
-def test_row_layout_refuses_views_and_shared_storages():
+@pytest.mark.parametrize("native", [True, False])
+def test_row_layout_refuses_views_and_shared_storages(native):
     from accdfl_amd.core import wire
 
     base = torch.randn(6, 4)
     sd = collections.OrderedDict(a=base.t(), b=torch.randn(3))  # a strided view
     sc = wire.scan_state_dict(pickle.dumps(sd))
-    assert sc.row_layout(["a", "b"], torch.float32, [(4, 6), (3,)]) is None
+    assert sc.row_layout(["a", "b"], torch.float32, [(4, 6), (3,)], native=native) is None
     sd = collections.OrderedDict(a=base[1:], b=torch.randn(3))  # a storage offset
     sc = wire.scan_state_dict(pickle.dumps(sd))
-    assert sc.row_layout(["a", "b"], torch.float32, [(5, 4), (3,)]) is None
+    assert sc.row_layout(["a", "b"], torch.float32, [(5, 4), (3,)], native=native) is None
     t = torch.randn(3)
     sd = collections.OrderedDict(a=t, b=t)  # one tensor under two parameter names
     sc = wire.scan_state_dict(pickle.dumps(sd))
-    assert sc.row_layout(["a", "b"], torch.float32, [(3,), (3,)]) is None
-    assert sc.row_layout(["a"], torch.float32, [(3,)]) is not None
+    assert sc.row_layout(["a", "b"], torch.float32, [(3,), (3,)], native=native) is None
+    assert sc.row_layout(["a"], torch.float32, [(3,)], native=native) is not None
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_scan_of_mutated_payloads_agrees_with_the_python_decoder(seed):
+    """Untrusted bytes: seeded mutations of state-dict payloads (byte flips, deletions, insertions, small
+    field changes; as bytes and as block lists) never crash the native scan, and whatever it accepts the
+    Python decoder accepts too and decodes to the same state dict (dtypes, shapes, strides, storage
+    offsets and sizes, bits, ties, _metadata).  Everything else it leaves to the Python decoder."""
+    import warnings
+
+    from accdfl_amd.core import wire
+
+    rng = np.random.default_rng(900 + seed)
+    accepted = 0
+    for it in range(80):
+        sd, _ = fz._state_dict(np.random.default_rng(int(rng.integers(1 << 30))))
+        data = bytearray(pickle.dumps(sd) if rng.integers(2) else wire.dumps_state_dict(sd))
+        kind = int(rng.integers(4))
+        for _ in range(int(rng.integers(1, 4))):
+            if kind == 0 and data:
+                data[int(rng.integers(len(data)))] = int(rng.integers(256))
+            elif kind == 1 and data:
+                i = int(rng.integers(len(data)))
+                del data[i:i + int(rng.integers(1, 64))]
+            elif kind == 2:
+                i = int(rng.integers(len(data) + 1))
+                data[i:i] = bytes(rng.integers(0, 256, int(rng.integers(1, 16)), dtype=np.uint8))
+            elif data:
+                i = int(rng.integers(len(data)))
+                data[i] = (data[i] + int(rng.integers(1, 4))) & 255
+        data = bytes(data)
+        payload = wire.payload_blocks(data, int(rng.choice([7, 100, 4096, 60_000]))) if rng.integers(2) else data
+        sc = wire.scan_state_dict(payload)
+        if sc is None:
+            continue
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore")
+            ref = wire.loads_state_dict(data)  # must not raise: the native scan accepted the payload
+        _same_as_pickle(_build(sc), ref, "seed %d mutant %d" % (seed, it))
+        accepted += 1
+    assert accepted > 5  # the mutants include accepted ones (value bytes changed)
+
+
+@pytest.mark.parametrize("seed", range(fz.N_CASES))
+def test_native_row_layout_matches_the_python_rules(seed):
+    """walk.cpp row_layout against StateDictScan's Python rules on the fuzz state dicts: random subsets of
+    the keys in random order as the parameter names, their true shapes or perturbed ones, the true dtype
+    or another — the same offsets, total and row, or None from both."""
+    from accdfl_amd.core import wire
+
+    rng = np.random.default_rng(7000 + seed)
+    sd, _ = fz._state_dict(rng)
+    sc = wire.scan_state_dict(pickle.dumps(sd))
+    keys = list(sd)
+    for _ in range(6):
+        names = [keys[i] for i in rng.permutation(len(keys))[:int(rng.integers(1, len(keys) + 1))]]
+        shapes = [tuple(sd[k].shape) for k in names]
+        if rng.integers(3) == 0:
+            j = int(rng.integers(len(shapes)))
+            shapes[j] = shapes[j] + (1,)
+        dtype = sd[names[0]].dtype if rng.integers(4) else torch.float64
+        a = sc.row_layout(names, dtype, shapes, native=True)
+        b = sc.row_layout(names, dtype, shapes, native=False)
+        assert (a is None) == (b is None), (seed, names)
+        if a is not None:
+            assert np.array_equal(a[0], b[0]) and a[1:] == b[1:], (seed, names)
