@@ -579,7 +579,11 @@ class StateDictScan:
             return
         t0 = time.perf_counter() if GATHER_MS is not None else 0.0
         st = np.asarray([(p, n) for _, _, p, n in self.storages], dtype=np.int64).reshape(-1, 2)
-        dst = offsets.astype(np.int64) + buf.data_ptr()
+        offsets = np.asarray(offsets, dtype=np.int64)
+        if len(offsets) != len(st) or (offsets < 0).any() or int((offsets + st[:, 1]).max()) > buf.numel() \
+                or buf.dtype != torch.uint8 or buf.device.type != "cpu" or not buf.is_contiguous():
+            raise ValueError("StateDictScan.gather: offsets outside the buffer")
+        dst = offsets + buf.data_ptr()
         d, s, n = _lib.walk_module().span_pieces(self.addrs, self.lens, np.ascontiguousarray(st[:, 0]),
                                                  np.ascontiguousarray(st[:, 1]), dst)
         if len(n):

@@ -282,3 +282,31 @@ def test_native_row_layout_matches_the_python_rules(seed):
         assert (a is None) == (b is None), (seed, names)
         if a is not None:
             assert np.array_equal(a[0], b[0]) and a[1:] == b[1:], (seed, names)
+
+
+def test_gather_and_build_refuse_out_of_bounds():
+    """The native build checks every view against its storage whoever made the descriptions, and the
+    gather refuses offsets outside the destination buffer."""
+    from accdfl_amd import _lib
+    from accdfl_amd.core import wire
+
+    sd = collections.OrderedDict(a=torch.arange(10, dtype=torch.float32), b=torch.ones(3, dtype=torch.int64))
+    sc = wire.scan_state_dict(pickle.dumps(sd))
+    buf = torch.zeros(1024, dtype=torch.uint8)
+    with pytest.raises(ValueError):
+        sc.gather(buf, np.array([0, 1010], dtype=np.int64))
+    with pytest.raises(ValueError):
+        sc.gather(buf, np.array([-8, 256], dtype=np.int64))
+    offs = np.array([0, 256], dtype=np.int64)
+    sc.gather(buf, offs)
+    assert torch.equal(sc.state_dict(buf, offs)["a"], sd["a"])
+    tag, sidx, off, size, stride, rg = sc.entries["a"]
+    forged = collections.OrderedDict(a=(tag, sidx, off, (11,), stride, rg))  # one element past the storage
+    with pytest.raises(ValueError):
+        _lib.walk_module().build_state_dict(buf, offs, forged, sc.storages, collections.OrderedDict)
+    forged = collections.OrderedDict(a=(tag, sidx, 1, size, stride, rg))  # shifted by one
+    with pytest.raises(ValueError):
+        _lib.walk_module().build_state_dict(buf, offs, forged, sc.storages, collections.OrderedDict)
+    with pytest.raises(ValueError):
+        _lib.walk_module().build_state_dict(buf, np.array([0, 1020], dtype=np.int64), sc.entries, sc.storages,
+                                            collections.OrderedDict)
