@@ -235,15 +235,36 @@ def _parse_storage_blob(blob, alloc=None) -> torch.TypedStorage:
     return torch.TypedStorage(wrap_storage=data.untyped_storage(), dtype=dtype, _internal=True)
 
 
+_LEGACY_HEAD = pickle.dumps(_LEGACY_MAGIC, protocol=2)[:4]  # PROTO 2, LONG1 of 10 bytes: a legacy blob's start
+
+
 def _load_storage_blob(blob, alloc=None):
     try:
         return _parse_storage_blob(blob, alloc)
     except UnsafePayloadError:
         raise
-    except Exception:  # any other layout: torch's own safe loader
+    except Exception:  # any other layout (the zipfile format): torch's own safe loader
         if isinstance(blob, _Span):
             blob = blob.read(0, len(blob))
+        if bytes(memoryview(blob)[:4]) == _LEGACY_HEAD:
+            # a legacy blob the parser refused (its sizes disagree): torch's legacy loader would allocate
+            # the element count the header claims, whatever the blob holds
+            raise UnsafePayloadError("accdfl_amd: malformed legacy storage blob")
         return torch.load(io.BytesIO(blob), weights_only=True)
+
+
+def _check_lengths(flat: bytes) -> None:
+    """Every length an opcode of the pickle claims (BINBYTES8, BYTEARRAY8, BINUNICODE8, FRAME, ...) fits in
+    the bytes that follow it — checked before the restricted unpickler runs, since CPython's unpickler
+    allocates a claimed length before it reads (a few corrupt bytes must not make the decoder allocate
+    gigabytes).  pickletools.genops reads each argument and stops at the first that runs past the end."""
+    import pickletools
+
+    try:
+        for _ in pickletools.genops(flat):
+            pass
+    except Exception as e:
+        raise UnsafePayloadError("accdfl_amd: malformed model payload (%s)" % str(e)[:200])
 
 
 _ALLOWED = {
@@ -529,6 +550,7 @@ def loads_state_dict(data, copy: bool = True, alloc: Optional[Callable[[int], to
         obj = _vm_loads(data, alloc)
     except _Unsupported:
         flat = b"".join(memoryview(b) for b in data) if isinstance(data, (list, tuple)) else bytes(data)
+        _check_lengths(flat)
         obj = _StateDictUnpickler(io.BytesIO(flat)).load()
     if not isinstance(obj, dict) or not all(isinstance(k, str) and torch.is_tensor(v) for k, v in obj.items()):
         raise UnsafePayloadError("accdfl_amd: payload is not a state_dict")
