@@ -310,3 +310,29 @@ def test_gather_and_build_refuse_out_of_bounds():
     with pytest.raises(ValueError):
         _lib.walk_module().build_state_dict(buf, np.array([0, 1020], dtype=np.int64), sc.entries, sc.storages,
                                             collections.OrderedDict)
+
+
+def test_corrupt_lengths_are_refused_without_allocating_them():
+    """A few corrupt length bytes must not make either decoder allocate what they claim: a protocol-5
+    BYTEARRAY8 claiming 1 TiB, and a legacy storage blob whose element count claims 2^40 elements (torch's
+    legacy loader would allocate them) — both refused (UnsafePayloadError) by the Python decoder, None from
+    the native scan, in well under a second and without growing the process."""
+    import resource
+    import time
+
+    from accdfl_amd.core import wire
+
+    rss0 = resource.getrusage(resource.RUSAGE_SELF).ru_maxrss
+    huge = b"\x80\x05\x96" + (1 << 40).to_bytes(8, "little") + b"abc."
+    t = torch.arange(12345, dtype=torch.float32)
+    good = pickle.dumps(collections.OrderedDict(w=t))
+    field = t.numel().to_bytes(8, "little")
+    at = good.index(field, good.index(b"FloatStorage"))
+    bad = good[:at] + (1 << 40).to_bytes(8, "little") + good[at + 8:]
+    for payload in (huge, bad):
+        t0 = time.perf_counter()
+        assert wire.scan_state_dict(payload) is None
+        with pytest.raises(wire.UnsafePayloadError):
+            wire.loads_state_dict(payload)
+        assert time.perf_counter() - t0 < 5.0
+    assert resource.getrusage(resource.RUSAGE_SELF).ru_maxrss - rss0 < 512 * 1024  # KiB: < 512 MiB more
