@@ -270,7 +270,7 @@ class _Tied(nn.Module):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("peers_as", ["wire", "modules", "device_modules", "tied"])
+@pytest.mark.parametrize("peers_as", ["wire", "modules", "device_modules", "tied", "wire_tied"])
 def test_aggregate_serialized_straight_from_hbm(dtype, peers_as):
     """VERDICT r02 missing 4: aggregate_serialized copies the averaged parameters from HBM straight
     into the payload (wire.DeviceSource), without the result module; the payload decodes — with the
@@ -284,7 +284,7 @@ def test_aggregate_serialized_straight_from_hbm(dtype, peers_as):
     from accdfl_amd.core.gradient_aggregation import GradientAggregationMethod
     from accdfl_amd.core.model_manager import DeviceModelManager
 
-    mk = _Tied if peers_as == "tied" else _ConvBN
+    mk = _Tied if peers_as in ("tied", "wire_tied") else _ConvBN
     models = [mk(k + 1, dtype) for k in range(5)]
     if peers_as == "device_modules":
         models = [m.cuda() for m in models]
@@ -292,7 +292,7 @@ def test_aggregate_serialized_straight_from_hbm(dtype, peers_as):
     mm = DeviceModelManager(None, SimpleNamespace(gradient_aggregation=GradientAggregationMethod.FEDAVG),
                             template=mk(0, dtype), capacity=5)
     for k, m in enumerate(models):
-        if peers_as == "wire":
+        if peers_as in ("wire", "wire_tied"):  # a tied parameter: one tensor under two keys of the payload
             mm.process_incoming_serialized(b"p%d" % k, wire.payload_blocks(wire.serialize_model(m), 60_000))
         else:
             mm.process_incoming_trained_model(b"p%d" % k, m)
@@ -312,7 +312,7 @@ def test_aggregate_serialized_straight_from_hbm(dtype, peers_as):
         for k in want:
             assert got[k].dtype == want[k].dtype and got[k].shape == want[k].shape, k
             assert torch.equal(got[k].view(-1).view(torch.uint8), want[k].view(-1).view(torch.uint8)), k
-    if peers_as == "tied":
+    if peers_as in ("tied", "wire_tied"):
         got = wire.loads_state_dict(direct)
         assert torch.equal(got["head.weight"], got["enc.weight"])
         assert not torch.equal(got["enc.weight"], models[0].enc.weight.detach())  # the average, not peer 0's
