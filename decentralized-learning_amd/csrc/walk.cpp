@@ -1265,33 +1265,37 @@ py::object row_layout(py::dict top, py::list storages, py::list names, std::stri
   int64_t* off = offsets.mutable_data();
   for (py::ssize_t i = 0; i < ns; ++i) off[i] = -1;
   PyObject* tensor_tag = wirescan::tags().tensor;
+  auto none = []() -> py::object {  // not a row (a conversion that failed on the way leaves no error behind)
+    PyErr_Clear();
+    return py::none();
+  };
   int64_t o = 0;
   for (py::ssize_t i = 0; i < nn; ++i) {
     PyObject* d = PyDict_GetItemWithError(top.ptr(), PyList_GET_ITEM(names.ptr(), i));  // borrowed
     if (!d) {
       if (PyErr_Occurred()) throw py::error_already_set();
-      return py::none();
+      return none();
     }
     if (!PyTuple_CheckExact(d) || PyTuple_GET_SIZE(d) != 6 || PyTuple_GET_ITEM(d, 0) != tensor_tag)
-      return py::none();
+      return none();
     const long long sidx = PyLong_AsLongLong(PyTuple_GET_ITEM(d, 1));
-    if (sidx < 0 || sidx >= ns || off[sidx] >= 0 || PyLong_AsLongLong(PyTuple_GET_ITEM(d, 2)) != 0) return py::none();
+    if (sidx < 0 || sidx >= ns || off[sidx] >= 0 || PyLong_AsLongLong(PyTuple_GET_ITEM(d, 2)) != 0) return none();
     PyObject* size = PyTuple_GET_ITEM(d, 3);
     PyObject* stride = PyTuple_GET_ITEM(d, 4);
     PyObject* want = PyList_GET_ITEM(shapes.ptr(), i);
-    if (!PyTuple_Check(want) || PyTuple_GET_SIZE(want) != PyTuple_GET_SIZE(size)) return py::none();
+    if (!PyTuple_Check(want) || PyTuple_GET_SIZE(want) != PyTuple_GET_SIZE(size)) return none();
     const Py_ssize_t nd = PyTuple_GET_SIZE(size);
     int64_t numel = 1, expect = 1;
     for (Py_ssize_t k = nd - 1; k >= 0; --k) {  // sizes equal the shape's, strides row-major
       const long long sz = PyLong_AsLongLong(PyTuple_GET_ITEM(size, k));
       if (sz != PyLong_AsLongLong(PyTuple_GET_ITEM(want, k)) || PyLong_AsLongLong(PyTuple_GET_ITEM(stride, k)) != expect)
-        return py::none();
+        return none();
       expect *= sz;
       numel *= sz;
     }
     if (PyErr_Occurred()) throw py::error_already_set();
     py::tuple rec = py::reinterpret_borrow<py::tuple>(PyList_GET_ITEM(storages.ptr(), sidx));
-    if (rec[0].cast<std::string>() != dtype || rec[1].cast<int64_t>() != numel) return py::none();
+    if (rec[0].cast<std::string>() != dtype || rec[1].cast<int64_t>() != numel) return none();
     off[sidx] = o;
     o += rec[3].cast<int64_t>();
   }
