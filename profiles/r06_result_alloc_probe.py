@@ -51,6 +51,11 @@ def main():
         mod.param_views(flat, p0, offs, {})
     out["param_views_us"] = med(views)
     out["buffer_copies_us"] = med(lambda: mod.buffer_copies(b0, {}))
+    # its two halves: one allocator block per buffer (param_fresh makes the same blocks, as Parameters), and
+    # the fused copy into blocks made beforehand
+    out["buffer_blocks_only_us"] = med(lambda: mod.param_fresh(b0, {}))
+    dsts = [torch.empty_like(b) for b in b0]
+    out["foreach_copy_only_us"] = med(lambda: torch._foreach_copy_(dsts, b0))
     torch.cuda.synchronize()
     w = [float(x) for x in np.random.default_rng(1).dirichlet(np.ones(128))]
     for n in (16, 128):
