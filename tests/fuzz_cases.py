@@ -16,6 +16,7 @@ Each case is a list of peer nn.Modules and a weights argument drawn from one see
 
 expected(models, weights) restates the reference per parameter with the C oracle
 (oracle/fedavg_ref.c through c_oracle.py: test infrastructure only)."""
+import os
 import numpy as np
 import torch
 from torch import nn
@@ -29,7 +30,8 @@ _SPECIAL = [float("nan"), float("inf"), float("-inf"), -0.0, 0.0, 1e-45, -1e-42,
 _NUMELS = [0, 1, 2, 3, 4, 5, 7, 8, 15, 16, 17, 63, 64, 65, 255, 1000, 4097, 12_345, 65_537, 70_001]
 _PEERS = [1, 1, 2, 2, 3, 4, 5, 7, 8, 8, 9, 16, 17, 31, 33, 64, 128, 129, 130]
 
-N_CASES = 96
+# ACCDFL_AMD_FUZZ_SCALE=k runs k times the seeds (a long fuzz campaign; the suites keep the default)
+N_CASES = 96 * int(os.environ.get("ACCDFL_AMD_FUZZ_SCALE", "1"))
 
 
 class _Peer(nn.Module):

@@ -10,6 +10,7 @@ break 16-byte alignment, weights with IEEE specials, out aliasing peers[0].
   pieces at arbitrary element offsets from page-locked host memory or from the device.
 
 The reference (fedavg.py:20-25) is restated by oracle/fedavg_ref.c (c_oracle.py)."""
+import os
 import numpy as np
 import pytest
 import torch
@@ -26,7 +27,8 @@ UDT = {"f32": np.uint32, "bf16": np.uint16, "f16": np.uint16, "f64": np.uint64}
 ES = {"f32": 4, "bf16": 2, "f16": 2, "f64": 8}
 _SPECIAL = [float("nan"), float("inf"), float("-inf"), -0.0, 1e-45, 3e38, 6.5e4, 1e-8]
 _PEERS = [1, 2, 3, 5, 8, 9, 16, 17, 32, 33, 64, 100, 128, 129, 200, 256, 257]
-N_CASES = 80
+# ACCDFL_AMD_FUZZ_SCALE=k runs k times the seeds (a long fuzz campaign; the suites keep the default)
+N_CASES = 80 * int(os.environ.get("ACCDFL_AMD_FUZZ_SCALE", "1"))
 _BUDGET = 12_000_000  # peer elements per case (host memory and oracle time)
 
 

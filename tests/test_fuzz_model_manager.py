@@ -7,6 +7,7 @@ outgrow, 1-40 peers arriving as modules (host or device) or as serialize_model p
 memoryview or EVA-style block lists), a duplicate arrival that must be ignored (:43-45), weights None
 or random; two rounds per case.  aggregate_trained_models and aggregate_serialized are each checked
 bit for bit (NaN as NaN) against fedavg.py over the registry's models in first-arrival order."""
+import os
 import numpy as np
 import pytest
 import torch
@@ -17,7 +18,8 @@ from oracle.fedavg_oracle import same_bits
 
 pytestmark = pytest.mark.gpu
 
-N_CASES = 64
+# ACCDFL_AMD_FUZZ_SCALE=k runs k times the seeds (a long fuzz campaign; the suites keep the default)
+N_CASES = 64 * int(os.environ.get("ACCDFL_AMD_FUZZ_SCALE", "1"))
 
 
 class _Net(nn.Module):
