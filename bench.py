@@ -2211,6 +2211,9 @@ def main():
             result["wire_ingress"] = legs.run("wire_ingress", lambda L: wire_ingress(p, device))
             result["host_inclusive_small"] = legs.run("host_inclusive_small", lambda L: host_inclusive_small())
             result["host_inclusive_configs"] = legs.run("host_inclusive_configs", lambda L: host_inclusive_configs())
+            for cname, crow in result["host_inclusive_configs"].items():
+                if isinstance(crow, dict) and "staged_parity_ok" in crow:
+                    parity["staged on arrival == FedAvg.aggregate: " + cname] = crow["staged_parity_ok"]
 
             def dfl(L):
                 msgs = dfl_messages(n, p)
