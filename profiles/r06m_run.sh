@@ -2,6 +2,7 @@
 # r06m: the final round-6 tree's evidence: the whole GPU suite + smoke, the default N=1 bench, the rocprofv3 kernel
 # trace + FETCH / WRITE passes of the headline (profiles/collect.sh), and the 4- and 8-rank gloo rehearsals
 # (configs[3]'s and configs[4]'s world sizes) on the one GPU.
+# Plus the host/GPU split of a 16-model device round (profiles/r06_device_round_split.py).
 set -o pipefail
 export TMPDIR=/tmp
 out=gpurun_out/r06m
@@ -21,5 +22,6 @@ run 900 python -u bench.py > $out/bench.log 2>&1
 run 1000 bash profiles/collect.sh r06m --steps 20 --warmup 5 --no-cpu-baseline --no-host-inclusive --no-small
 cp gpurun_out/prof_r06m/summary/* gpurun_out/prof_r06m/trace.log $out/ 2>/dev/null
 rm -rf gpurun_out/prof_r06m
+run 120 python -u profiles/r06_device_round_split.py > $out/device_round_split.jsonl 2>&1
 run 900 python -u bench.py --gpus 4 --dist-backend gloo --steps 20 --warmup 5 > $out/gloo4.log 2>&1
 run 900 python -u bench.py --gpus 8 --dist-backend gloo --steps 20 --warmup 5 > $out/gloo8.log 2>&1
