@@ -427,14 +427,15 @@ def _device_round(models: List[nn.Module], weights, layout) -> "nn.Module | None
     peers, whatever the tensor count (fedavg.py:23-25).  Stream-ordered like any torch op.
 
     The host work around the launch is batched (a 16-model ResNet-34 round spent 2 ms
-    of Python around a 0.13 ms reduce): the result's parameters are made natively before the launch
-    (walk.cpp param_fresh: one caching-allocator tensor each, as deepcopy makes them, so record_stream
-    and CUDA IPC work on the result — round 6; rounds 4-5 made them parts of one allocation the
-    allocator did not know); models[0]'s device buffers are copied by one fused copy per dtype instead
+    of Python around a 0.13 ms reduce): the result's parameters are made natively, their blocks before
+    the launch and their Parameter objects while the reduce runs (walk.cpp param_blocks / param_wrap: one
+    caching-allocator tensor each, as deepcopy makes them, so record_stream and CUDA IPC work on the
+    result — round 6; rounds 4-5 made them parts of one allocation the allocator did not know);
+    models[0]'s device buffers are copied by one fused copy per dtype instead
     of one deepcopy dispatch per buffer; the module tree is cloned while the kernel runs."""
     dtype, device, numels, table = layout
     mod = _lib.walk_module()
-    if mod is None or not hasattr(mod, "param_fresh"):
+    if mod is None or not hasattr(mod, "param_blocks"):
         return _device_round_per_tensor(models, weights, layout)
     objs = mod.tensors(models[0], _PLAIN_SET)
     if objs is None or len(objs[0]) != len(numels) or any(type(p) is not nn.Parameter for p in objs[0]):
@@ -442,10 +443,12 @@ def _device_round(models: List[nn.Module], weights, layout) -> "nn.Module | None
     p0, b0 = objs
     nums = _flat_plan(dtype, numels)[3]
     memo = {}
-    outs = (ctypes.c_void_p * len(numels)).from_buffer(mod.param_fresh(p0, memo))
+    blocks, out_ptrs = mod.param_blocks(p0)
+    outs = (ctypes.c_void_p * len(numels)).from_buffer(out_ptrs)
     ptrs = (ctypes.c_void_p * table.size).from_buffer(table)
     _wsum.wsum_multi_ptrs(dtype, ptrs, outs, nums, weights, device, total_elems=sum(numels))
-    # while the reduce runs: models[0]'s buffers, the module tree
+    # while the reduce runs: the parameters' Python objects, models[0]'s buffers, the module tree
+    mod.param_wrap(blocks, p0, memo)
     _seed_buffers(b0, memo)
     return _clone_value(models[0], memo)
 
@@ -488,17 +491,19 @@ def _device_round_grouped(models: List[nn.Module], weights) -> "nn.Module | None
     if first is None:
         return None
     dtype, device, numels, table = first
-    # models[0]'s own objects and the result's fresh parameters (walk.cpp param_fresh), before the first
-    # launch writes into them
-    objs = mod.tensors(models[0], _PLAIN_SET) if hasattr(mod, "param_fresh") else None
+    # models[0]'s own objects and the result's fresh parameter blocks (walk.cpp param_blocks), before the
+    # first launch writes into them; their Parameter objects while it runs (param_wrap)
+    objs = mod.tensors(models[0], _PLAIN_SET) if hasattr(mod, "param_blocks") else None
     if objs is None or len(objs[0]) != len(numels) or any(type(p) is not nn.Parameter for p in objs[0]):
         return None
     p0, b0 = objs
     nums = _flat_plan(dtype, numels)[3]
     memo = {}
-    outs = (ctypes.c_void_p * len(numels)).from_buffer(mod.param_fresh(p0, memo))
+    blocks, out_ptrs = mod.param_blocks(p0)
+    outs = (ctypes.c_void_p * len(numels)).from_buffer(out_ptrs)
     _wsum.wsum_multi_ptrs(dtype, (ctypes.c_void_p * table.size).from_buffer(table), outs, nums,
                           weights[a0:b0_], device, total_elems=sum(numels))
+    mod.param_wrap(blocks, p0, memo)
     for a, b in bounds[1:]:
         # each later group checked against models[0]'s layout (shapes, dtype, device) in its own walk
         lay = _device_layout(models[a:b], ref=models[0])

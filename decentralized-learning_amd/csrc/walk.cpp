@@ -367,6 +367,47 @@ py::array_t<uint64_t> param_fresh(py::list params, py::dict memo) {
   return ptrs;
 }
 
+// param_fresh in two halves around the launch (fedavg._device_round): param_blocks takes the blocks from
+// the allocator (the reduce needs only their addresses), param_wrap turns them into the nn.Parameters of
+// the deepcopy memo while the reduce runs — the Python objects, autograd metadata and memo entries (~0.3 us
+// a parameter) leave the time before the launch.  Blocks a FreshParams still holds when it is dropped go
+// back to the allocator, ordered after the work queued on the stream they came from.
+struct FreshParams {
+  std::vector<at::Tensor> t;
+};
+
+py::tuple param_blocks(py::list params) {
+  const py::ssize_t n = PyList_GET_SIZE(params.ptr());
+  py::array_t<uint64_t> ptrs(n);
+  uint64_t* out = ptrs.mutable_data();
+  auto h = std::make_unique<FreshParams>();
+  h->t.reserve(n);
+  FreshAlloc fresh;
+  for (py::ssize_t i = 0; i < n; ++i) {
+    PyObject* o = PyList_GET_ITEM(params.ptr(), i);
+    if (!THPVariable_Check(o)) throw std::invalid_argument("param_blocks: not a tensor");
+    h->t.push_back(fresh.like(THPVariable_Unpack(o)));
+    out[i] = reinterpret_cast<uint64_t>(h->t.back().data_ptr());
+  }
+  return py::make_tuple(py::cast(std::move(h)), ptrs);
+}
+
+void param_wrap(FreshParams& h, py::list params, py::dict memo) {
+  const py::ssize_t n = PyList_GET_SIZE(params.ptr());
+  if (static_cast<size_t>(n) != h.t.size()) throw std::invalid_argument("param_wrap: one block per parameter");
+  for (py::ssize_t i = 0; i < n; ++i) {
+    PyObject* o = PyList_GET_ITEM(params.ptr(), i);
+    if (!THPVariable_Check(o)) throw std::invalid_argument("param_wrap: not a tensor");
+    at::Tensor& v = h.t[i];
+    v.set_requires_grad(THPVariable_Unpack(o).requires_grad());
+    py::object w = py::reinterpret_steal<py::object>(THPVariable_Wrap(v, reinterpret_cast<PyTypeObject*>(ParameterClass)));
+    if (!w) throw py::error_already_set();
+    py::object id = py::reinterpret_steal<py::object>(PyLong_FromVoidPtr(o));
+    if (!id || PyDict_SetItem(memo.ptr(), id.ptr(), w.ptr()) < 0) throw py::error_already_set();
+  }
+  h.t.clear();
+}
+
 // deepcopy of models[0]'s device buffers (fedavg.py:20 copies them, it does not average them) in one
 // fused copy per (device, dtype), stored into the deepcopy memo: for each entry of `buffers` not already in
 // `memo`, memo[id(buffer)] = a fresh tensor from the device's allocator (a storage of its own, as deepcopy
@@ -1439,6 +1480,9 @@ PYBIND11_MODULE(_dla_walk, m) {
   m.def("fingerprint", &fingerprint, py::arg("model"), py::arg("plain"));
   m.def("param_views", &param_views, py::arg("flat"), py::arg("params"), py::arg("offsets"), py::arg("memo"));
   m.def("param_fresh", &param_fresh, py::arg("params"), py::arg("memo"));
+  py::class_<FreshParams>(m, "FreshParams").def("__len__", [](const FreshParams& h) { return h.t.size(); });
+  m.def("param_blocks", &param_blocks, py::arg("params"));
+  m.def("param_wrap", &param_wrap, py::arg("blocks"), py::arg("params"), py::arg("memo"));
   m.def("buffer_copies", &buffer_copies, py::arg("buffers"), py::arg("memo"));
   m.def("clone_value", &clone_value, py::arg("v"), py::arg("memo"), py::arg("atomic"), py::arg("modules"),
         py::arg("fallback"), py::arg("odict"));

@@ -3,12 +3,15 @@ device models (110 parameters, 108 BN buffers each), the steps of fedavg._device
 the host (no synchronisation between them, as the product runs them), medians of 100 rounds:
   layout       — fedavg._device_layout (the native walk over every model: shapes, dtype, pointers);
   tensors      — walk.cpp tensors (models[0]'s parameter and buffer lists);
-  param_fresh  — the result's parameters, one caching-allocator block each (round 6);
+  blocks       — the result's parameters' caching-allocator blocks (walk.cpp param_blocks);
   launch       — dla_wsum_multi_table's host call (table upload + kernel launch);
+  wrap         — their nn.Parameter objects in the deepcopy memo (walk.cpp param_wrap), while the reduce runs;
   buffers      — walk.cpp buffer_copies (models[0]'s buffers, one block each + one fused copy);
   clone        — the module tree's containers (_clone_value);
   wait         — torch.cuda.synchronize() after the clone: the GPU time not hidden behind the host steps;
-plus the reduce alone (HIP events, back to back) and the whole FedAvg.aggregate call + synchronize."""
+plus the reduce alone (HIP events, back to back) and the whole FedAvg.aggregate call + synchronize; and, interleaved
+round by round, the whole sequence with the parameters made in one step before the launch (param_fresh, the
+round-6 form before param_blocks / param_wrap) against the two-step form."""
 import ctypes
 import json
 import os
@@ -37,7 +40,7 @@ def main():
     for _ in range(5):
         fa.FedAvg.aggregate(models, w)
     torch.cuda.synchronize()
-    keys = ("layout", "tensors", "param_fresh", "launch", "buffers", "clone", "wait")
+    keys = ("layout", "tensors", "blocks", "launch", "wrap", "buffers", "clone", "wait")
     split = {k: [] for k in keys}
     split["host"] = []
     results = []
@@ -49,11 +52,14 @@ def main():
         p0, b0 = mod.tensors(models[0], fa._PLAIN_SET)
         t.append(time.perf_counter())
         memo = {}
-        outs = (ctypes.c_void_p * len(numels)).from_buffer(mod.param_fresh(p0, memo))
+        blocks, out_ptrs = mod.param_blocks(p0)
+        outs = (ctypes.c_void_p * len(numels)).from_buffer(out_ptrs)
         t.append(time.perf_counter())
         nums = fa._flat_plan(dtype, numels)[3]
         _wsum.wsum_multi_ptrs(dtype, (ctypes.c_void_p * table.size).from_buffer(table), outs, nums, w, device,
                               total_elems=sum(numels))
+        t.append(time.perf_counter())
+        mod.param_wrap(blocks, p0, memo)
         t.append(time.perf_counter())
         fa._seed_buffers(b0, memo)
         t.append(time.perf_counter())
@@ -93,7 +99,33 @@ def main():
         torch.cuda.synchronize()
         ts.append(time.perf_counter() - t0)
     out["aggregate_us"] = round(statistics.median(ts) * 1e6, 1)
-    out["models"], out["parameters"], out["buffers"] = n, len(numels), len(mod.tensors(models[0], fa._PLAIN_SET)[1])
+
+    def seq(two_step):
+        t0 = time.perf_counter()
+        dtype, device, numels, table = fa._device_layout(models)
+        p0, b0 = mod.tensors(models[0], fa._PLAIN_SET)
+        memo = {}
+        if two_step:
+            blocks, out_ptrs = mod.param_blocks(p0)
+        else:
+            out_ptrs = mod.param_fresh(p0, memo)
+        outs = (ctypes.c_void_p * len(numels)).from_buffer(out_ptrs)
+        _wsum.wsum_multi_ptrs(dtype, (ctypes.c_void_p * table.size).from_buffer(table), outs,
+                              fa._flat_plan(dtype, numels)[3], w, device, total_elems=sum(numels))
+        if two_step:
+            mod.param_wrap(blocks, p0, memo)
+        fa._seed_buffers(b0, memo)
+        res = fa._clone_value(models[0], memo)
+        torch.cuda.synchronize()
+        return time.perf_counter() - t0, res
+    ab = {False: [], True: []}
+    for _ in range(100):
+        for two in (False, True):
+            ab[two].append(seq(two)[0])
+    out["one_step_us"] = round(statistics.median(ab[False]) * 1e6, 1)
+    out["two_step_us"] = round(statistics.median(ab[True]) * 1e6, 1)
+    out["n_models"], out["n_parameters"] = n, len(numels)
+    out["n_buffers"] = len(mod.tensors(models[0], fa._PLAIN_SET)[1])
     print(json.dumps(out), flush=True)
 
 

@@ -804,6 +804,17 @@ def test_walk_memo_seeding_on_cpu():
     assert type(f0) is nn.Parameter and f0.shape == (3, 4) and f0.stride() == (4, 1) and f0.requires_grad
     assert not f1.requires_grad and list(ptrs) == [f0.data_ptr(), f1.data_ptr()]
     assert f0.untyped_storage().nbytes() == 48 and f0.untyped_storage().data_ptr() == f0.data_ptr()
+    # param_blocks + param_wrap: the same in two halves (the blocks before the launch, the Parameters after)
+    blocks, bptrs = mod.param_blocks(pf)
+    assert len(blocks) == 2 and len(bptrs) == 2
+    bm = {}
+    mod.param_wrap(blocks, pf, bm)
+    assert len(blocks) == 0  # handed over
+    g0, g1 = bm[id(pf[0])], bm[id(pf[1])]
+    assert type(g0) is nn.Parameter and g0.shape == (3, 4) and g0.requires_grad and not g1.requires_grad
+    assert list(bptrs) == [g0.data_ptr(), g1.data_ptr()] and g0.untyped_storage().nbytes() == 48
+    with pytest.raises(ValueError):
+        mod.param_wrap(mod.param_blocks(pf)[0], pf[:1], {})
     import numpy as np
 
     pooled = torch.from_numpy(np.arange(8, dtype=np.float32))  # memory torch did not allocate
