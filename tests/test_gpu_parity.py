@@ -450,7 +450,7 @@ def test_device_modules_of_real_layouts_through_fedavg(name, n, dtype):
 
 def test_device_round_result_pickles_like_a_deepcopy():
     """The device round's result (parameters and buffer copies: one caching-allocator tensor each since
-    round 6, walk.cpp param_fresh / buffer_copies) has a storage per tensor, as deepcopy(models[0]) does: the reference's serialize_model
+    round 6, walk.cpp param_blocks / param_wrap / buffer_copies) has a storage per tensor, as deepcopy(models[0]) does: the reference's serialize_model
     (pickle.dumps(state_dict()), accdfl/core/models/__init__.py:9-10) writes each tensor's bytes once,
     not the whole allocation per tensor, and the payload decodes to the result's values."""
     import copy
