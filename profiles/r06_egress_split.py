@@ -1,0 +1,147 @@
+"""Round 6: where DeviceModelManager.aggregate_serialized spends its time for 16 google_speech ResNet-34
+bf16 peers staged from wire payloads (110 parameters, 108 BN buffers; a 42.7 MB payload out) — the steps
+of aggregate_serialized replayed one by one on the host (medians of 30 rounds):
+  uniform     — _uniform() (the registry still matches the staged rows);
+  structure   — the template's parameters() and state_dict(keep_vars=True), the first peer's state dict;
+  checks      — the offsets / key / device checks;
+  reduce      — slab._reduce_planned (host time of the launch);
+  entries     — the payload's OrderedDict (DeviceSources, the buffers converted to their dtype);
+  plan        — wire._template_plan (the layout signature, the cached template);
+  alloc       — the payload bytes object (uninitialised);
+  gaps        — the template's pickle pieces copied in (one batched memcpy);
+  device      — the parameters' bytes from HBM (chunked D2H through the bounce buffers + memcpys; it
+                first waits for the reduce);
+plus the whole aggregate_serialized call, the same fill into an already-faulted payload (a bytearray written
+before), and the D2H of the averaged row alone into a page-locked buffer."""
+import collections
+import json
+import os
+import pickle
+import statistics
+import sys
+import time
+from types import SimpleNamespace
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "decentralized-learning_amd")]
+import bench  # noqa: E402
+
+
+def main():
+    from accdfl_amd import _lib
+    from accdfl_amd.core import wire
+    from accdfl_amd.core.gradient_aggregation import GradientAggregationMethod
+    from accdfl_amd.core.model_manager import DeviceModelManager
+
+    dev = torch.device("cuda", 0)
+    if "--numa-bind" in sys.argv:
+        from accdfl_amd.core.host_memory import bind_to_gpu_node
+
+        bind_to_gpu_node(dev)
+    n = 16
+    models, p = bench._layout_models("google_speech_resnet34", n, torch.bfloat16, pinned=False, seed=4200)
+    msgs = [wire.payload_blocks(wire.serialize_model(m), bench.EVA_BLOCK) for m in models]
+    mm = DeviceModelManager(None, SimpleNamespace(gradient_aggregation=GradientAggregationMethod.FEDAVG), 0,
+                            capacity=n, template=models[0], device=dev)
+    for k, blocks in enumerate(msgs):
+        mm.process_incoming_serialized(b"p%d" % k, blocks)
+    mm.slab.copy_stream.synchronize()
+    w = [1.0 / n] * n
+    for _ in range(3):
+        mm.aggregate_serialized(w)
+    keys = ("uniform", "structure", "checks", "reduce", "entries", "plan", "alloc", "gaps", "device")
+    split = {k: [] for k in keys}
+    whole, warm, d2h = [], [], []
+    out_len = None
+    pinned = None
+    for _ in range(30):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        payload = mm.aggregate_serialized(w)
+        whole.append(time.perf_counter() - t0)
+        out_len = len(payload)
+        del payload
+        torch.cuda.synchronize()
+        t = [time.perf_counter()]
+        assert mm._uniform()
+        t.append(time.perf_counter())
+        entries = list(mm.incoming_trained_models.values())
+        first = entries[0]
+        structure = mm.template
+        params = list(structure.parameters())
+        state = structure.state_dict(keep_vars=True)
+        bufs = first.state_dict
+        t.append(time.perf_counter())
+        offsets = {id(q): (o, q.shape) for q, o in zip(params, mm.slab._offsets())}
+        param_keys = {k for k, v in state.items() if id(v) in offsets}
+        assert not any(v.device.type != "cpu" for v in state.values())
+        t.append(time.perf_counter())
+        with torch.no_grad():
+            flat = mm.slab._reduce_planned(w)
+        t.append(time.perf_counter())
+        sd = collections.OrderedDict()
+        for k, v in state.items():
+            if k in param_keys:
+                off, shape = offsets[id(v)]
+                sd[k] = wire.DeviceSource(flat, off, shape)
+            elif k in bufs and bufs[k].shape == v.shape:
+                sd[k] = bufs[k].detach().to(v.dtype)
+            else:
+                sd[k] = v.detach()
+        t.append(time.perf_counter())
+        tpl, sources = wire._template_plan(sd)
+        t.append(time.perf_counter())
+        out = wire._new_bytes(None, tpl.total)
+        t.append(time.perf_counter())
+        base = id(out) + wire._BYTES_DATA
+        dst, src, ln, devs = [], [], [], []
+        for g, o in zip(tpl.gaps, tpl.gap_off):
+            if g:
+                dst.append(base + o)
+                src.append(id(g) + wire._BYTES_DATA)
+                ln.append(len(g))
+        for v, o, nb in zip(sources, tpl.slot_off, tpl.slots):
+            if not nb:
+                continue
+            if isinstance(v, wire.DeviceSource):
+                devs.append((base + o, v))
+            else:
+                dst.append(base + o)
+                src.append(v.data_ptr())
+                ln.append(nb)
+        _lib.host_copy_batch(dst, src, ln)
+        t.append(time.perf_counter())
+        wire._copy_device_segments(devs)
+        t.append(time.perf_counter())
+        for k, a, b in zip(keys, t, t[1:]):
+            split[k].append(b - a)
+        # the same device copy into the payload just written (its pages faulted in)
+        t1 = time.perf_counter()
+        wire._copy_device_segments(devs)
+        warm.append(time.perf_counter() - t1)
+        # the averaged row alone, D2H into a page-locked buffer
+        if pinned is None:
+            pinned = torch.empty(flat.numel() * flat.element_size(), dtype=torch.uint8, pin_memory=True)
+        t1 = time.perf_counter()
+        pinned.copy_(flat.view(torch.uint8).view(-1)[:pinned.numel()], non_blocking=True)
+        torch.cuda.synchronize()
+        d2h.append(time.perf_counter() - t1)
+        del out
+    res = {k: round(statistics.median(v) * 1e3, 4) for k, v in split.items()}
+    res["sum_of_steps"] = round(sum(res[k] for k in keys), 4)
+    res["aggregate_serialized"] = round(statistics.median(whole) * 1e3, 4)
+    res["device_into_faulted_payload"] = round(statistics.median(warm) * 1e3, 4)
+    res["d2h_row_pinned"] = round(statistics.median(d2h) * 1e3, 4)
+    res["payload_MB"] = round(out_len / 1e6, 2)
+    res["row_MB"] = round(pinned.numel() / 1e6, 2)
+    res["numa_bound"] = "--numa-bind" in sys.argv
+    # the payload decodes to the averaged parameters (the reference's pickle.loads)
+    sd = pickle.loads(mm.aggregate_serialized(w))
+    res["decodes"] = len(sd) == len(models[0].state_dict())
+    print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()
