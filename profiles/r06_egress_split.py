@@ -11,9 +11,12 @@ of aggregate_serialized replayed one by one on the host (medians of 30 rounds):
   gaps        — the template's pickle pieces copied in (one batched memcpy);
   device      — the parameters' bytes from HBM (chunked D2H through the bounce buffers + memcpys; it
                 first waits for the reduce);
-plus the whole aggregate_serialized call, the same fill into an already-faulted payload (a bytearray written
-before), and the D2H of the averaged row alone into a page-locked buffer."""
+plus the whole aggregate_serialized call, the same device copy into the payload just written (its pages
+faulted in), the D2H of the averaged row alone into a page-locked buffer, and the whole fill (alloc + gaps +
+device) of a fresh payload with and without madvise(MADV_HUGEPAGE) on its range before it is touched,
+interleaved round by round (the box's transparent-hugepage settings are printed with the result)."""
 import collections
+import ctypes
 import json
 import os
 import pickle
@@ -129,7 +132,52 @@ def main():
         torch.cuda.synchronize()
         d2h.append(time.perf_counter() - t1)
         del out
+    libc = ctypes.CDLL(None, use_errno=True)
+    libc.madvise.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+
+    def fill(huge):
+        t1 = time.perf_counter()
+        out = wire._new_bytes(None, tpl.total)
+        base = id(out) + wire._BYTES_DATA
+        if huge:
+            a = (base + 4095) & ~4095
+            libc.madvise(a, (base + tpl.total - a) & ~4095, 14)  # MADV_HUGEPAGE
+        dst, src, ln, devs = [], [], [], []
+        for g, o in zip(tpl.gaps, tpl.gap_off):
+            if g:
+                dst.append(base + o)
+                src.append(id(g) + wire._BYTES_DATA)
+                ln.append(len(g))
+        for v, o, nb in zip(sources, tpl.slot_off, tpl.slots):
+            if nb and isinstance(v, wire.DeviceSource):
+                devs.append((base + o, v))
+            elif nb:
+                dst.append(base + o)
+                src.append(v.data_ptr())
+                ln.append(nb)
+        _lib.host_copy_batch(dst, src, ln)
+        wire._copy_device_segments(devs)
+        dt = time.perf_counter() - t1
+        return dt, out
+    fills = {False: [], True: []}
+    check = []
+    for _ in range(30):
+        for huge in (False, True):
+            dt, out = fill(huge)
+            fills[huge].append(dt)
+            check.append(out)
+            if len(check) > 2:
+                check.pop(0)
     res = {k: round(statistics.median(v) * 1e3, 4) for k, v in split.items()}
+    res["fill_fresh"] = round(statistics.median(fills[False]) * 1e3, 4)
+    res["fill_fresh_madv_hugepage"] = round(statistics.median(fills[True]) * 1e3, 4)
+    res["fills_identical"] = check[0] == check[1]
+    for f in ("enabled", "defrag"):
+        try:
+            with open("/sys/kernel/mm/transparent_hugepage/" + f) as fh:
+                res["thp_" + f] = fh.read().strip()
+        except OSError as e:
+            res["thp_" + f] = str(e)
     res["sum_of_steps"] = round(sum(res[k] for k in keys), 4)
     res["aggregate_serialized"] = round(statistics.median(whole) * 1e3, 4)
     res["device_into_faulted_payload"] = round(statistics.median(warm) * 1e3, 4)
