@@ -218,7 +218,7 @@ def test_row_layout_refuses_views_and_shared_storages(native):
     assert sc.row_layout(["a"], torch.float32, [(3,)], native=native) is not None
 
 
-@pytest.mark.parametrize("seed", range(4))
+@pytest.mark.parametrize("seed", range(4 * int(os.environ.get("ACCDFL_AMD_FUZZ_SCALE", "1"))))
 def test_scan_of_mutated_payloads_agrees_with_the_python_decoder(seed):
     """Untrusted bytes: seeded mutations of state-dict payloads (byte flips, deletions, insertions, small
     field changes; as bytes and as block lists) never crash the native scan, and whatever it accepts the
