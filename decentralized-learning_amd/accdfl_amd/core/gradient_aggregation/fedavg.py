@@ -1037,6 +1037,29 @@ _PLAIN_MODULE_SET: set = set()  # the classes _plain_module accepts, as the walk
 _NATIVE_CLONE = True
 
 
+def _setstate_full_state():
+    """The attribute names of a fresh nn.Module when this torch's nn.Module.__setstate__, given a state
+    holding all of them, only copies it into the module's __dict__ (its other lines add attributes old
+    checkpoints lack); the walk extension then sets such a state as the clone's __dict__ without calling
+    it.  None (always call it) when this torch's function does anything else with a full state."""
+    m = nn.Module()
+    state = {k: v for k, v in m.__dict__.items() if k != "_compiled_call_impl"}
+    y = nn.Module.__new__(nn.Module)
+    try:
+        nn.Module.__setstate__(y, dict(state))
+    except Exception:  # noqa: BLE001 — any other behaviour: keep the call
+        return None
+    d = y.__dict__
+    if list(d) != list(state) or any(d[k] is not v for k, v in state.items()):
+        return None
+    return tuple(state)
+
+
+_SETSTATE_FN = nn.Module.__dict__["__setstate__"]
+_FULL_STATE = _setstate_full_state()
+_SETSTATE_ARGS = (_SETSTATE_FN, _FULL_STATE) if _FULL_STATE is not None else (None, None)
+
+
 def _plain_module(cls: type) -> bool:
     ok = _plain_module_cls.get(cls)
     if ok is None:
@@ -1054,14 +1077,15 @@ def _clone_fallback(v, memo: dict):
     """The walk extension's fallback for an object its clone does not take itself: a module class not
     yet classified (classified now, then cloned natively), else copy.deepcopy with the same memo."""
     if _plain_module(type(v)):
-        return _lib.walk_module().clone_value(v, memo, _ATOMIC, _PLAIN_MODULE_SET, _clone_fallback, OrderedDict)
+        return _lib.walk_module().clone_value(v, memo, _ATOMIC, _PLAIN_MODULE_SET, _clone_fallback, OrderedDict,
+                                              *_SETSTATE_ARGS)
     return copy.deepcopy(v, memo)
 
 
 def _clone_value(v, memo: dict):
     mod = _lib.walk_module() if _NATIVE_CLONE else None
     if mod is not None:
-        return mod.clone_value(v, memo, _ATOMIC, _PLAIN_MODULE_SET, _clone_fallback, OrderedDict)
+        return mod.clone_value(v, memo, _ATOMIC, _PLAIN_MODULE_SET, _clone_fallback, OrderedDict, *_SETSTATE_ARGS)
     t = type(v)
     if t in _ATOMIC:
         return v

@@ -473,8 +473,10 @@ void buffer_copies(py::list buffers, py::dict memo) {
 // The module-tree clone (fedavg._clone_value, deepcopy's protocol restated) in native code.  Ctx: the
 // deepcopy memo (id -> copy), the set of types copied as themselves, the set of module classes cloned
 // here (fedavg._plain_module: torch's __getstate__, no other copy hook), `fallback(obj, memo)` (the
-// Python _clone_value, for every other object), collections.OrderedDict, and "_compiled_call_impl" (the
-// __dict__ entry a module clone leaves out).
+// Python _clone_value, for every other object), collections.OrderedDict, "_compiled_call_impl" (the
+// __dict__ entry a module clone leaves out), and — when fedavg found that torch's nn.Module.__setstate__
+// only updates __dict__ for a state holding every attribute a fresh module has — that function and those
+// attribute names (else both null).
 struct CloneCtx {
   PyObject* memo;
   PyObject* atomic;
@@ -482,6 +484,8 @@ struct CloneCtx {
   PyObject* fallback;
   PyObject* odict;
   PyObject* skip;
+  PyObject* setstate_fn;
+  PyObject* full_state;  // tuple of str
 };
 
 PyObject* clone_mapping(PyObject* v, const CloneCtx& c, bool module_state = false);
@@ -494,8 +498,27 @@ bool memo_put(PyObject* memo, PyObject* x, PyObject* y) {
   return rc == 0;
 }
 
+// y.__setstate__(state) is y.__dict__.update(state) on a fresh y: its class keeps torch's
+// nn.Module.__setstate__, and the state holds every attribute whose absence that function repairs.
+// 1 yes, 0 no, -1 error.
+int setstate_is_update(PyTypeObject* tp, PyObject* state, const CloneCtx& c) {
+  static PyObject* const setstate = PyUnicode_InternFromString("__setstate__");
+  if (!c.setstate_fn || _PyType_Lookup(tp, setstate) != c.setstate_fn) return 0;
+  const Py_ssize_t n = PyTuple_GET_SIZE(c.full_state);
+  if (PyDict_GET_SIZE(state) < n) return 0;
+  for (Py_ssize_t i = 0; i < n; ++i) {
+    const int has = PyDict_Contains(state, PyTuple_GET_ITEM(c.full_state, i));
+    if (has <= 0) return has;
+  }
+  return 1;
+}
+
 // A module of a class in ctx.modules, as copy._reconstruct does it: y = cls.__new__(cls), registered in
-// the memo, state = a clone of x.__dict__ without _compiled_call_impl, y.__setstate__(state).
+// the memo, state = a clone of x.__dict__ without _compiled_call_impl, y.__setstate__(state) — or, when
+// that call would only copy the state into y's empty __dict__ (setstate_is_update), the state made y's
+// __dict__ directly: the same entries in the same order, without a Python frame per module.  (The memo
+// then maps x.__dict__ to y's own __dict__ rather than to a detached copy of it: only an object that held
+// a module's __dict__ itself could tell.)
 PyObject* clone_module(PyObject* x, const CloneCtx& c) {
   PyTypeObject* tp = Py_TYPE(x);
   static PyObject* const no_args = PyTuple_New(0);
@@ -509,8 +532,23 @@ PyObject* clone_module(PyObject* x, const CloneCtx& c) {
   PyObject* d = PyObject_GenericGetDict(x, nullptr);
   PyObject* state = d ? clone_mapping(d, c, /*module_state=*/true) : nullptr;
   Py_XDECREF(d);
-  PyObject* r = state ? PyObject_CallMethodOneArg(y, setstate, state) : nullptr;
-  Py_XDECREF(state);
+  if (!state) {
+    Py_DECREF(y);
+    return nullptr;
+  }
+  const int update = setstate_is_update(tp, state, c);
+  PyObject** yd = update > 0 ? _PyObject_GetDictPtr(y) : nullptr;
+  if (yd && (!*yd || PyDict_GET_SIZE(*yd) == 0)) {
+    const int rc = PyObject_GenericSetDict(y, state, nullptr);
+    Py_DECREF(state);
+    if (rc < 0) {
+      Py_DECREF(y);
+      return nullptr;
+    }
+    return y;
+  }
+  PyObject* r = update >= 0 ? PyObject_CallMethodOneArg(y, setstate, state) : nullptr;
+  Py_DECREF(state);
   if (!r) {
     Py_DECREF(y);
     return nullptr;
@@ -613,7 +651,9 @@ PyObject* clone_mapping(PyObject* v, const CloneCtx& c, bool module_state) {
   // an empty OrderedDict (a module's hook dicts) iterates like a dict: no items() view needed
   const bool exact = PyDict_CheckExact(v);
   const bool plain_iter = exact || PyDict_GET_SIZE(v) == 0;
-  PyObject* y = exact ? PyDict_New() : PyObject_CallNoArgs(reinterpret_cast<PyObject*>(Py_TYPE(v)));
+  // an exact OrderedDict (the hook dicts, _parameters, _buffers, _modules) without a type call
+  const bool odict = !exact && PyODict_CheckExact(v);
+  PyObject* y = exact ? PyDict_New() : odict ? PyODict_New() : PyObject_CallNoArgs(reinterpret_cast<PyObject*>(Py_TYPE(v)));
   if (!y || !memo_put(c.memo, v, y)) {
     Py_XDECREF(y);
     return nullptr;
@@ -625,7 +665,7 @@ PyObject* clone_mapping(PyObject* v, const CloneCtx& c, bool module_state) {
     PyObject* kc = at ? Py_NewRef(k) : PyObject_CallFunctionObjArgs(c.fallback, k, c.memo, nullptr);
     if (!kc) return false;
     PyObject* ci = clone_one(x, c);
-    const int rc = ci ? (exact ? PyDict_SetItem(y, kc, ci) : PyObject_SetItem(y, kc, ci)) : -1;
+    const int rc = ci ? (exact ? PyDict_SetItem(y, kc, ci) : odict ? PyODict_SetItem(y, kc, ci) : PyObject_SetItem(y, kc, ci)) : -1;
     Py_DECREF(kc);
     Py_XDECREF(ci);
     return rc == 0;
@@ -679,11 +719,20 @@ PyObject* clone_mapping(PyObject* v, const CloneCtx& c, bool module_state) {
 // _clone_value, for every other object and for non-atomic keys (hashable: _clone_value copies them as
 // deepcopy does); `odict`: collections.OrderedDict.
 py::object clone_value(py::object v, py::dict memo, py::object atomic, py::object modules, py::object fallback,
-                       py::object odict) {
+                       py::object odict, py::object setstate_fn, py::object full_state) {
   if (!PyAnySet_Check(atomic.ptr()) || !PyAnySet_Check(modules.ptr()))
     throw std::invalid_argument("clone_value: sets of atomic types and module classes");
+  const bool fast = !setstate_fn.is_none();
+  if (fast) {
+    if (!PyTuple_Check(full_state.ptr())) throw std::invalid_argument("clone_value: full_state is a tuple of str");
+    for (Py_ssize_t i = 0; i < PyTuple_GET_SIZE(full_state.ptr()); ++i) {
+      PyObject* k = PyTuple_GET_ITEM(full_state.ptr(), i);
+      if (!PyUnicode_CheckExact(k)) throw std::invalid_argument("clone_value: full_state is a tuple of str");
+    }
+  }
   static PyObject* const skip = PyUnicode_InternFromString("_compiled_call_impl");
-  const CloneCtx c{memo.ptr(), atomic.ptr(), modules.ptr(), fallback.ptr(), odict.ptr(), skip};
+  const CloneCtx c{memo.ptr(), atomic.ptr(), modules.ptr(), fallback.ptr(), odict.ptr(), skip,
+                   fast ? setstate_fn.ptr() : nullptr, fast ? full_state.ptr() : nullptr};
   PyObject* y = clone_one(v.ptr(), c);
   if (!y) throw py::error_already_set();
   return py::reinterpret_steal<py::object>(y);
@@ -1485,7 +1534,7 @@ PYBIND11_MODULE(_dla_walk, m) {
   m.def("param_wrap", &param_wrap, py::arg("blocks"), py::arg("params"), py::arg("memo"));
   m.def("buffer_copies", &buffer_copies, py::arg("buffers"), py::arg("memo"));
   m.def("clone_value", &clone_value, py::arg("v"), py::arg("memo"), py::arg("atomic"), py::arg("modules"),
-        py::arg("fallback"), py::arg("odict"));
+        py::arg("fallback"), py::arg("odict"), py::arg("setstate_fn") = py::none(), py::arg("full_state") = py::none());
   m.def("scan_state_dict", &scan_state_dict, py::arg("addrs"), py::arg("lens"), py::arg("odict_cls"));
   m.def("row_layout", &row_layout, py::arg("top"), py::arg("storages"), py::arg("names"), py::arg("dtype"),
         py::arg("shapes"));

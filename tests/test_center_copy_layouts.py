@@ -271,3 +271,39 @@ def test_fedavg_result_of_reference_trees(kind, where):
         assert torch.equal(b, c) and b.data_ptr() != c.data_ptr(), n
     cpu_got = got if where == "cpu" else copy.deepcopy(got).cpu()
     assert _sd_pickle_len(cpu_got) == _sd_pickle_len(ref)
+
+
+class _OwnSetstate(nn.Module):
+    calls = 0
+
+    def __init__(self):
+        super().__init__()
+        self.lin = nn.Linear(2, 2)
+
+    def __setstate__(self, state):
+        type(self).calls += 1
+        super().__setstate__(state)
+
+
+def test_clone_sets_a_module_state_directly_only_where_setstate_would_just_copy_it():
+    """The native tree clone makes a module's cloned state its __dict__ without calling __setstate__ only
+    when the class keeps nn.Module.__setstate__ and the state holds every attribute a fresh module has
+    (fedavg._FULL_STATE, checked against this torch at import); a class with its own __setstate__, or a
+    module missing an attribute (an old checkpoint's), still gets the call — and every module's __dict__
+    matches copy.deepcopy's, key for key and in order."""
+    from accdfl_amd.core.gradient_aggregation import fedavg as fa
+
+    assert fa._FULL_STATE is not None and "_forward_hooks" in fa._FULL_STATE
+    old = nn.Linear(2, 2)
+    del old.__dict__["_backward_pre_hooks"]  # a module unpickled from an old checkpoint
+    m = nn.Sequential(nn.Linear(3, 3), _OwnSetstate(), old)
+    _OwnSetstate.calls = 0
+    ref = copy.deepcopy(m)
+    assert _OwnSetstate.calls == 1
+    c = fa._clone_value(m, {})
+    assert _OwnSetstate.calls == 2
+    for a, b, x in zip(c.modules(), ref.modules(), m.modules()):
+        assert type(a) is type(b) and list(a.__dict__) == list(b.__dict__)
+        assert a._forward_hooks is not x._forward_hooks and a._parameters is not x._parameters
+    assert "_backward_pre_hooks" in c[2].__dict__ and list(c[2].__dict__)[-1] == "_backward_pre_hooks"
+    assert all(torch.equal(p, q) for p, q in zip(c.parameters(), m.parameters()))
