@@ -35,7 +35,19 @@ def main():
     dev = torch.device("cuda", 0)
     mod = _lib.walk_module()
     n = 16
-    models, p = bench._device_layout_models("google_speech_resnet34", n, torch.bfloat16, dev)
+    if "--tree" in sys.argv:  # the reference's module tree (97 modules) instead of one ParameterList
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        from test_center_copy_layouts import tree_from_layout
+
+        models = []
+        for k in range(n):
+            t = tree_from_layout("google_speech_resnet34").to(torch.bfloat16)
+            with torch.no_grad():
+                for q in t.parameters():
+                    q.copy_(torch.randn(q.shape, generator=torch.Generator().manual_seed(k)) * 0.05)
+            models.append(t.to(dev))
+    else:
+        models, p = bench._device_layout_models("google_speech_resnet34", n, torch.bfloat16, dev)
     w = [float(x) for x in np.random.default_rng(1).dirichlet(np.ones(n))]
     for _ in range(5):
         fa.FedAvg.aggregate(models, w)
@@ -126,6 +138,7 @@ def main():
     out["two_step_us"] = round(statistics.median(ab[True]) * 1e6, 1)
     out["n_models"], out["n_parameters"] = n, len(numels)
     out["n_buffers"] = len(mod.tensors(models[0], fa._PLAIN_SET)[1])
+    out["n_modules"] = len(list(models[0].modules()))
     print(json.dumps(out), flush=True)
 
 
