@@ -495,13 +495,21 @@ struct CloneCtx {
   PyObject* skip;
   PyObject* setstate_fn;
   PyObject* full_state;  // tuple of str
+  bool scalar_atomic;    // str, int, bool, float and None are in `atomic`
 };
 
-PyObject* clone_mapping(PyObject* v, const CloneCtx& c, bool module_state = false);
-PyObject* clone_sequence(PyObject* x, const CloneCtx& c);
+// x is a str, int, bool, float or None: copied as itself, and never in the memo (deepcopy memoizes only
+// objects whose copy is a new object), so no memo lookup is needed for it.
+inline bool scalar(PyObject* x) {
+  return PyUnicode_CheckExact(x) || PyLong_CheckExact(x) || PyBool_Check(x) || PyFloat_CheckExact(x) || x == Py_None;
+}
 
-bool memo_put(PyObject* memo, PyObject* x, PyObject* y) {
-  PyObject* id = PyLong_FromVoidPtr(x);
+// `key`: id(x) as the caller already made it for its memo lookup (else made here)
+PyObject* clone_mapping(PyObject* v, const CloneCtx& c, bool module_state = false, PyObject* key = nullptr);
+PyObject* clone_sequence(PyObject* x, const CloneCtx& c, PyObject* key = nullptr);
+
+bool memo_put(PyObject* memo, PyObject* x, PyObject* y, PyObject* key = nullptr) {
+  PyObject* id = key ? Py_NewRef(key) : PyLong_FromVoidPtr(x);
   const int rc = id ? PyDict_SetItem(memo, id, y) : -1;
   Py_XDECREF(id);
   return rc == 0;
@@ -528,13 +536,13 @@ int setstate_is_update(PyTypeObject* tp, PyObject* state, const CloneCtx& c) {
 // __dict__ directly: the same entries in the same order, without a Python frame per module.  (The memo
 // then maps x.__dict__ to y's own __dict__ rather than to a detached copy of it: only an object that held
 // a module's __dict__ itself could tell.)
-PyObject* clone_module(PyObject* x, const CloneCtx& c) {
+PyObject* clone_module(PyObject* x, const CloneCtx& c, PyObject* key = nullptr) {
   PyTypeObject* tp = Py_TYPE(x);
   static PyObject* const no_args = PyTuple_New(0);
   static PyObject* const setstate = PyUnicode_InternFromString("__setstate__");
   PyObject* y = tp->tp_new(tp, no_args, nullptr);
   if (!y) return nullptr;
-  if (!memo_put(c.memo, x, y)) {
+  if (!memo_put(c.memo, x, y, key)) {
     Py_DECREF(y);
     return nullptr;
   }
@@ -571,20 +579,21 @@ PyObject* clone_module(PyObject* x, const CloneCtx& c) {
 // OrderedDict / tuple / list / empty set / plain module made here, else fallback(value, memo).  New
 // reference, or nullptr with the Python error set.
 PyObject* clone_one(PyObject* x, const CloneCtx& c) {
+  if (c.scalar_atomic && scalar(x)) return Py_NewRef(x);
   PyObject* key = PyLong_FromVoidPtr(x);
   if (!key) return nullptr;
+  const py::object keep = py::reinterpret_steal<py::object>(key);  // released on every return
   PyObject* hit = PyDict_GetItemWithError(c.memo, key);  // borrowed
-  Py_DECREF(key);
   if (hit) return Py_NewRef(hit);
   if (PyErr_Occurred()) return nullptr;
   const int at = PySet_Contains(c.atomic, reinterpret_cast<PyObject*>(Py_TYPE(x)));
   if (at < 0) return nullptr;
   if (at) return Py_NewRef(x);
-  if (PyDict_CheckExact(x) || Py_TYPE(x) == reinterpret_cast<PyTypeObject*>(c.odict)) return clone_mapping(x, c);
-  if (PyTuple_CheckExact(x) || PyList_CheckExact(x)) return clone_sequence(x, c);
+  if (PyDict_CheckExact(x) || Py_TYPE(x) == reinterpret_cast<PyTypeObject*>(c.odict)) return clone_mapping(x, c, false, key);
+  if (PyTuple_CheckExact(x) || PyList_CheckExact(x)) return clone_sequence(x, c, key);
   if (PySet_CheckExact(x) && PySet_GET_SIZE(x) == 0) {  // _non_persistent_buffers_set: a new empty set
     PyObject* y = PySet_New(nullptr);
-    if (!y || !memo_put(c.memo, x, y)) {
+    if (!y || !memo_put(c.memo, x, y, key)) {
       Py_XDECREF(y);
       return nullptr;
     }
@@ -592,17 +601,17 @@ PyObject* clone_one(PyObject* x, const CloneCtx& c) {
   }
   const int mod = PySet_Contains(c.modules, reinterpret_cast<PyObject*>(Py_TYPE(x)));
   if (mod < 0) return nullptr;
-  if (mod) return clone_module(x, c);
+  if (mod) return clone_module(x, c, key);
   return PyObject_CallFunctionObjArgs(c.fallback, x, c.memo, nullptr);
 }
 
 // A tuple or list (a conv's kernel_size / stride / padding, _reversed_padding_repeated_twice), as
 // copy.deepcopy copies them: a list is a new list registered in the memo before its items; a tuple is
 // itself when every item clones to itself (tuples of numbers), else a new tuple registered in the memo.
-PyObject* clone_sequence(PyObject* x, const CloneCtx& c) {
+PyObject* clone_sequence(PyObject* x, const CloneCtx& c, PyObject* key) {
   if (PyList_CheckExact(x)) {
     PyObject* y = PyList_New(0);
-    if (!y || !memo_put(c.memo, x, y)) {
+    if (!y || !memo_put(c.memo, x, y, key)) {
       Py_XDECREF(y);
       return nullptr;
     }
@@ -637,14 +646,14 @@ PyObject* clone_sequence(PyObject* x, const CloneCtx& c) {
     return Py_NewRef(x);
   }
   // an item's copy may have copied this tuple already (a cycle through a mutable item): use that one
-  PyObject* id = PyLong_FromVoidPtr(x);
+  PyObject* id = key ? Py_NewRef(key) : PyLong_FromVoidPtr(x);
   PyObject* prev = id ? PyDict_GetItemWithError(c.memo, id) : nullptr;
   Py_XDECREF(id);
   if (prev || PyErr_Occurred()) {
     Py_DECREF(y);
     return prev ? Py_NewRef(prev) : nullptr;
   }
-  if (!memo_put(c.memo, x, y)) {
+  if (!memo_put(c.memo, x, y, key)) {
     Py_DECREF(y);
     return nullptr;
   }
@@ -656,20 +665,22 @@ PyObject* clone_sequence(PyObject* x, const CloneCtx& c) {
 // a new mapping of the same type registered in the memo first (deepcopy's order, so a cycle finds it),
 // then every entry in iteration order with its value cloned by clone_one and a non-atomic key through
 // the fallback.
-PyObject* clone_mapping(PyObject* v, const CloneCtx& c, bool module_state) {
+PyObject* clone_mapping(PyObject* v, const CloneCtx& c, bool module_state, PyObject* key) {
   // an empty OrderedDict (a module's hook dicts) iterates like a dict: no items() view needed
   const bool exact = PyDict_CheckExact(v);
   const bool plain_iter = exact || PyDict_GET_SIZE(v) == 0;
   // an exact OrderedDict (the hook dicts, _parameters, _buffers, _modules) without a type call
   const bool odict = !exact && PyODict_CheckExact(v);
   PyObject* y = exact ? PyDict_New() : odict ? PyODict_New() : PyObject_CallNoArgs(reinterpret_cast<PyObject*>(Py_TYPE(v)));
-  if (!y || !memo_put(c.memo, v, y)) {
+  if (!y || !memo_put(c.memo, v, y, key)) {
     Py_XDECREF(y);
     return nullptr;
   }
   auto put = [&](PyObject* k, PyObject* x) -> bool {
-    if (module_state && PyUnicode_Check(k) && PyUnicode_Compare(k, c.skip) == 0) return true;
-    const int at = PySet_Contains(c.atomic, reinterpret_cast<PyObject*>(Py_TYPE(k)));
+    if (module_state && PyUnicode_Check(k) &&
+        (k == c.skip || (PyUnicode_GET_LENGTH(k) == PyUnicode_GET_LENGTH(c.skip) && PyUnicode_Compare(k, c.skip) == 0)))
+      return true;
+    const int at = c.scalar_atomic && PyUnicode_CheckExact(k) ? 1 : PySet_Contains(c.atomic, reinterpret_cast<PyObject*>(Py_TYPE(k)));
     if (at < 0) return false;
     PyObject* kc = at ? Py_NewRef(k) : PyObject_CallFunctionObjArgs(c.fallback, k, c.memo, nullptr);
     if (!kc) return false;
@@ -740,8 +751,14 @@ py::object clone_value(py::object v, py::dict memo, py::object atomic, py::objec
     }
   }
   static PyObject* const skip = PyUnicode_InternFromString("_compiled_call_impl");
+  bool scalar_atomic = true;
+  for (PyTypeObject* t : {&PyUnicode_Type, &PyLong_Type, &PyBool_Type, &PyFloat_Type, Py_TYPE(Py_None)}) {
+    const int has = PySet_Contains(atomic.ptr(), reinterpret_cast<PyObject*>(t));
+    if (has < 0) throw py::error_already_set();
+    scalar_atomic = scalar_atomic && has;
+  }
   const CloneCtx c{memo.ptr(), atomic.ptr(), modules.ptr(), fallback.ptr(), odict.ptr(), skip,
-                   fast ? setstate_fn.ptr() : nullptr, fast ? full_state.ptr() : nullptr};
+                   fast ? setstate_fn.ptr() : nullptr, fast ? full_state.ptr() : nullptr, scalar_atomic};
   PyObject* y = clone_one(v.ptr(), c);
   if (!y) throw py::error_already_set();
   return py::reinterpret_steal<py::object>(y);
