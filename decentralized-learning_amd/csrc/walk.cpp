@@ -496,6 +496,7 @@ struct CloneCtx {
   PyObject* setstate_fn;
   PyObject* full_state;  // tuple of str
   bool scalar_atomic;    // str, int, bool, float and None are in `atomic`
+  bool containers_not_atomic;  // dict and OrderedDict are not
 };
 
 // x is a str, int, bool, float or None: copied as itself, and never in the memo (deepcopy memoizes only
@@ -586,10 +587,14 @@ PyObject* clone_one(PyObject* x, const CloneCtx& c) {
   PyObject* hit = PyDict_GetItemWithError(c.memo, key);  // borrowed
   if (hit) return Py_NewRef(hit);
   if (PyErr_Occurred()) return nullptr;
-  const int at = PySet_Contains(c.atomic, reinterpret_cast<PyObject*>(Py_TYPE(x)));
-  if (at < 0) return nullptr;
-  if (at) return Py_NewRef(x);
-  if (PyDict_CheckExact(x) || Py_TYPE(x) == reinterpret_cast<PyTypeObject*>(c.odict)) return clone_mapping(x, c, false, key);
+  // the containers a module's __dict__ holds are never atomic (clone_value checks): no set lookup for them
+  const bool mapping = PyDict_CheckExact(x) || Py_TYPE(x) == reinterpret_cast<PyTypeObject*>(c.odict);
+  if (!(mapping && c.containers_not_atomic)) {
+    const int at = PySet_Contains(c.atomic, reinterpret_cast<PyObject*>(Py_TYPE(x)));
+    if (at < 0) return nullptr;
+    if (at) return Py_NewRef(x);
+  }
+  if (mapping) return clone_mapping(x, c, false, key);
   if (PyTuple_CheckExact(x) || PyList_CheckExact(x)) return clone_sequence(x, c, key);
   if (PySet_CheckExact(x) && PySet_GET_SIZE(x) == 0) {  // _non_persistent_buffers_set: a new empty set
     PyObject* y = PySet_New(nullptr);
@@ -757,8 +762,15 @@ py::object clone_value(py::object v, py::dict memo, py::object atomic, py::objec
     if (has < 0) throw py::error_already_set();
     scalar_atomic = scalar_atomic && has;
   }
+  bool containers_not_atomic = true;
+  for (PyObject* t : {reinterpret_cast<PyObject*>(&PyDict_Type), odict.ptr()}) {
+    const int has = PySet_Contains(atomic.ptr(), t);
+    if (has < 0) throw py::error_already_set();
+    containers_not_atomic = containers_not_atomic && !has;
+  }
   const CloneCtx c{memo.ptr(), atomic.ptr(), modules.ptr(), fallback.ptr(), odict.ptr(), skip,
-                   fast ? setstate_fn.ptr() : nullptr, fast ? full_state.ptr() : nullptr, scalar_atomic};
+                   fast ? setstate_fn.ptr() : nullptr, fast ? full_state.ptr() : nullptr, scalar_atomic,
+                   containers_not_atomic};
   PyObject* y = clone_one(v.ptr(), c);
   if (!y) throw py::error_already_set();
   return py::reinterpret_steal<py::object>(y);
