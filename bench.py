@@ -1186,7 +1186,51 @@ def device_module_configs(device, reps=10):
         del inp
         torch.cuda.empty_cache()
         res[name] = row
+    res[TREE_CONFIG] = device_tree_round(device, reps)
     return res
+
+
+# the simulators' device models are the reference's module trees, not one ParameterList per model
+TREE_CONFIG = "configs[4] google_speech ResNet-34, 16 peers, bf16 (reference module tree)"
+
+
+def device_tree_round(device, reps=10):
+    """FedAvg.aggregate on 16 device-resident google_speech ResNet-34 models built as the reference's
+    module tree (97 modules; tests/test_center_copy_layouts.py tree_from_layout, from the layouts the
+    reference's create_model gives), holding the same values as the ParameterList models of
+    device_module_configs: end to end and the layout walk, and ``parity_ok`` — the tree round's result
+    equals the ParameterList round's, every parameter bit for bit."""
+    from accdfl_amd.core.gradient_aggregation import fedavg as fa
+
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from test_center_copy_layouts import tree_from_layout
+
+    log("device modules: " + TREE_CONFIG)
+    flat, p = _device_layout_models("google_speech_resnet34", 16, torch.bfloat16, device)
+    trees = []
+    for fm in flat:
+        t = tree_from_layout("google_speech_resnet34").to(device=device, dtype=torch.bfloat16)
+        with torch.no_grad():
+            for q, src in zip(t.parameters(), fm.parameters()):
+                q.copy_(src)
+        trees.append(t)
+    w = [float(x) for x in np.random.default_rng(16).dirichlet(np.ones(16))]
+
+    def e2e():
+        fa.FedAvg.aggregate(trees, w)
+        torch.cuda.synchronize()
+
+    row = {"peers": 16, "params": p, "dtype": "bf16", "modules": len(list(trees[0].modules())),
+           "tensors": len(list(trees[0].parameters())), "end_to_end_ms": _median_ms(e2e, reps),
+           "layout_walk_ms": _median_ms(lambda: fa._device_layout(trees), reps)}
+    got, want = fa.FedAvg.aggregate(trees, w), fa.FedAvg.aggregate(flat, w)
+    torch.cuda.synchronize()
+    row["parity_ok"] = all(torch.equal(a.detach().view(torch.int16), b.detach().view(torch.int16))
+                           for a, b in zip(got.parameters(), want.parameters()))
+    row["parity"] = "every parameter of the tree round's result == the ParameterList round's, bit for bit"
+    del flat, trees, got, want
+    torch.cuda.empty_cache()
+    return row
 
 
 def cpu_layout_configs(budget_s=2.0):
@@ -2206,6 +2250,8 @@ def main():
             result["baseline_configs"] = legs.run("baseline_configs", lambda L: baseline_configs(device))
             result["device_module_configs"] = legs.run("device_module_configs",
                                                        lambda L: device_module_configs(device))
+            parity["device round of reference module trees == ParameterList layout"] = \
+                result["device_module_configs"].get(TREE_CONFIG, {}).get("parity_ok")
         if not args.no_host_inclusive and args.dtype == "f32":
             result["host_inclusive"] = legs.run("host_inclusive", lambda L: host_inclusive(n, p))
             result["wire_ingress"] = legs.run("wire_ingress", lambda L: wire_ingress(p, device))
