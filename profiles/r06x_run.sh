@@ -1,8 +1,6 @@
 #!/bin/bash
 # r06x: the 4x fuzz campaign (FedAvg.aggregate, C ABI, DeviceModelManager against the C oracle) on the
 # final tree, after the walk / tree-clone changes.
-
-
 set -o pipefail
 export TMPDIR=/tmp
 out=gpurun_out/r06x
