@@ -1,5 +1,5 @@
 #!/bin/bash
-# r06z: the final round-6 tree's evidence (after the walk / clone changes): the whole GPU suite + smoke, the default N=1 bench, the rocprofv3 kernel
+# r06z: the final round-6 tree's evidence (after the worker-thread parameter blocks): the whole GPU suite + smoke, the default N=1 bench, the rocprofv3 kernel
 # trace + FETCH / WRITE passes of the headline (profiles/collect.sh), and the 4- and 8-rank gloo rehearsals
 # (configs[3]'s and configs[4]'s world sizes) on the one GPU.
 # Plus the host/GPU split of a 16-model device round (profiles/r06_device_round_split.py).
