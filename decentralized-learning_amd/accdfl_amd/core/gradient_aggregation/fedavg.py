@@ -420,24 +420,7 @@ def _flat_plan(dtype, numels: List[int]):
     return plan
 
 
-_ASYNC_BLOCKS = True  # the result's parameter blocks taken on the walk extension's worker thread (A/B knob)
-
-
-def _start_blocks(model0: nn.Module):
-    """(models[0]'s (parameters, buffers), the result's parameter blocks being taken on the walk extension's
-    worker thread) — started before the round's layout walk, so the allocator's ~0.4 us a block overlaps
-    it (walk.cpp param_blocks_start); None when the extension cannot list models[0]'s tensors yet (its
-    classes are classified by the first walk) or they are not all plain nn.Parameters."""
-    mod = _lib.walk_module()
-    if mod is None or not _ASYNC_BLOCKS or not hasattr(mod, "param_blocks_start"):
-        return None
-    objs = mod.tensors(model0, _PLAIN_SET)
-    if objs is None or not objs[0] or any(type(p) is not nn.Parameter for p in objs[0]):
-        return None
-    return objs, mod.param_blocks_start(objs[0])
-
-
-def _device_round(models: List[nn.Module], weights, layout, started=None) -> "nn.Module | None":
+def _device_round(models: List[nn.Module], weights, layout) -> "nn.Module | None":
     """The whole aggregate for device-resident models of one layout: deepcopy(models[0]) with fresh
     parameters (fedavg.py:20), then every parameter of every model folded straight into them by
     dla_wsum_multi(_table) from one pointer table — one launch per 128-peer pass for rounds of many
@@ -454,19 +437,13 @@ def _device_round(models: List[nn.Module], weights, layout, started=None) -> "nn
     mod = _lib.walk_module()
     if mod is None or not hasattr(mod, "param_blocks"):
         return _device_round_per_tensor(models, weights, layout)
-    if started is not None:  # models[0]'s tensors and the blocks, taken while the layout was walked
-        objs, blocks = started
-        out_ptrs = mod.param_blocks_finish(blocks)
-        if len(objs[0]) != len(numels):
-            return _device_round_per_tensor(models, weights, layout)
-    else:
-        objs = mod.tensors(models[0], _PLAIN_SET)
-        if objs is None or len(objs[0]) != len(numels) or any(type(p) is not nn.Parameter for p in objs[0]):
-            return _device_round_per_tensor(models, weights, layout)
-        blocks, out_ptrs = mod.param_blocks(objs[0])
+    objs = mod.tensors(models[0], _PLAIN_SET)
+    if objs is None or len(objs[0]) != len(numels) or any(type(p) is not nn.Parameter for p in objs[0]):
+        return _device_round_per_tensor(models, weights, layout)
     p0, b0 = objs
     nums = _flat_plan(dtype, numels)[3]
     memo = {}
+    blocks, out_ptrs = mod.param_blocks(p0)
     outs = (ctypes.c_void_p * len(numels)).from_buffer(out_ptrs)
     ptrs = (ctypes.c_void_p * table.size).from_buffer(table)
     _wsum.wsum_multi_ptrs(dtype, ptrs, outs, nums, weights, device, total_elems=sum(numels))
@@ -500,7 +477,7 @@ def _group_bounds(n: int) -> List[tuple]:
     return out
 
 
-def _device_round_grouped(models: List[nn.Module], weights, started=None) -> "nn.Module | None":
+def _device_round_grouped(models: List[nn.Module], weights) -> "nn.Module | None":
     """_device_round for a round of many device-resident models, launched group by group
     (_group_bounds): each group is walked (its own pointer table) and its fold launched at once, the
     groups after the first continuing the fold in the result (dla_wsum_multi_table_acc) — list order
@@ -514,22 +491,15 @@ def _device_round_grouped(models: List[nn.Module], weights, started=None) -> "nn
     if first is None:
         return None
     dtype, device, numels, table = first
-    # models[0]'s own objects and the result's fresh parameter blocks (walk.cpp param_blocks; taken on the
-    # worker thread while the first group was walked, when started), before the first launch writes into
-    # them; their Parameter objects while it runs (param_wrap)
-    if started is not None:
-        objs, blocks = started
-        out_ptrs = mod.param_blocks_finish(blocks)
-        if len(objs[0]) != len(numels):
-            return None
-    else:
-        objs = mod.tensors(models[0], _PLAIN_SET) if hasattr(mod, "param_blocks") else None
-        if objs is None or len(objs[0]) != len(numels) or any(type(p) is not nn.Parameter for p in objs[0]):
-            return None
-        blocks, out_ptrs = mod.param_blocks(objs[0])
+    # models[0]'s own objects and the result's fresh parameter blocks (walk.cpp param_blocks), before the
+    # first launch writes into them; their Parameter objects while it runs (param_wrap)
+    objs = mod.tensors(models[0], _PLAIN_SET) if hasattr(mod, "param_blocks") else None
+    if objs is None or len(objs[0]) != len(numels) or any(type(p) is not nn.Parameter for p in objs[0]):
+        return None
     p0, b0 = objs
     nums = _flat_plan(dtype, numels)[3]
     memo = {}
+    blocks, out_ptrs = mod.param_blocks(p0)
     outs = (ctypes.c_void_p * len(numels)).from_buffer(out_ptrs)
     _wsum.wsum_multi_ptrs(dtype, (ctypes.c_void_p * table.size).from_buffer(table), outs, nums,
                           weights[a0:b0_], device, total_elems=sum(numels))
@@ -1226,15 +1196,13 @@ class FedAvg(GradientAggregation):
                     if done is not None:
                         return done
                 else:
-                    started = _start_blocks(models[0]) if p_first is not None and p_first.is_cuda else None
                     if len(models) >= _GROUP_MIN and p_first is not None and p_first.is_cuda:
-                        done = _device_round_grouped(models, list(weights), started)
+                        done = _device_round_grouped(models, list(weights))
                         if done is not None:
                             return done
-                        started = None  # its blocks went with the grouped attempt
                     dev_layout = _device_layout(models)
                     if dev_layout is not None:
-                        done = _device_round(models, list(weights), dev_layout, started)
+                        done = _device_round(models, list(weights), dev_layout)
                         if done is not None:
                             return done
             center_model = _center_copy(models[0])

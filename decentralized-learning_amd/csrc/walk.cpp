@@ -27,15 +27,8 @@
 #include <torch/csrc/autograd/python_variable.h>
 #include <pybind11/numpy.h>
 
-#include <unistd.h>
-
 #include <algorithm>
-#include <condition_variable>
 #include <cstdint>
-#include <exception>
-#include <memory>
-#include <mutex>
-#include <thread>
 #include <cstring>
 #include <stdexcept>
 #include <string>
@@ -388,84 +381,8 @@ py::array_t<uint64_t> param_fresh(py::list params, py::dict memo) {
 // the deepcopy memo while the reduce runs — the Python objects, autograd metadata and memo entries (~0.3 us
 // a parameter) leave the time before the launch.  Blocks a FreshParams still holds when it is dropped go
 // back to the allocator, ordered after the work queued on the stream they came from.
-//
-// param_blocks_start / param_blocks_finish take the same blocks on a worker thread instead, while the
-// caller's thread walks the round's models (the allocator needs no GIL: ~0.35-0.45 us a block, 36-48 us
-// for a ResNet-34, otherwise spent before the launch).  The worker adopts the caller's current device and
-// stream, so the blocks belong to that stream exactly as if the caller had allocated them.
-struct BlockJob {
-  std::vector<at::Tensor> likes;  // models[0]'s parameters: sizes, strides, dtype, device
-  c10::Stream stream;
-  std::vector<at::Tensor> out;
-  std::exception_ptr err;
-  bool done = false;
-  std::mutex mu;
-  std::condition_variable cv;
-  explicit BlockJob(c10::Stream s) : stream(s) {}
-};
-
-void run_block_job(BlockJob& job) {
-  try {
-    c10::StreamGuard guard(job.stream);
-    FreshAlloc fresh;
-    job.out.reserve(job.likes.size());
-    for (const at::Tensor& p : job.likes) job.out.push_back(fresh.like(p));
-  } catch (...) {
-    job.err = std::current_exception();
-    job.out.clear();
-  }
-  job.likes.clear();
-  std::lock_guard<std::mutex> g(job.mu);
-  job.done = true;
-  job.cv.notify_all();
-}
-
-// One persistent worker (leaked on purpose: no join at exit), one job at a time; a forked child has
-// none and runs its jobs on the calling thread.
-class BlockWorker {
- public:
-  static BlockWorker& get() {
-    static BlockWorker* w = new BlockWorker;
-    return *w;
-  }
-  // false: not taken (a forked child, or the worker busy): the caller runs the job itself
-  bool submit(const std::shared_ptr<BlockJob>& job) {
-    if (getpid() != pid_) return false;
-    std::lock_guard<std::mutex> g(mu_);
-    if (pending_) return false;
-    if (!thread_started_) {
-      std::thread([this] { loop(); }).detach();
-      thread_started_ = true;
-    }
-    pending_ = job;
-    cv_.notify_one();
-    return true;
-  }
-
- private:
-  void loop() {
-    for (;;) {
-      std::shared_ptr<BlockJob> job;
-      {
-        std::unique_lock<std::mutex> g(mu_);
-        cv_.wait(g, [this] { return pending_ != nullptr; });
-        job = pending_;
-      }
-      run_block_job(*job);
-      std::lock_guard<std::mutex> g(mu_);
-      pending_.reset();
-    }
-  }
-  const pid_t pid_ = getpid();
-  std::mutex mu_;
-  std::condition_variable cv_;
-  std::shared_ptr<BlockJob> pending_;
-  bool thread_started_ = false;
-};
-
 struct FreshParams {
   std::vector<at::Tensor> t;
-  std::shared_ptr<BlockJob> job;  // param_blocks_start's, until param_blocks_finish
 };
 
 py::tuple param_blocks(py::list params) {
@@ -484,55 +401,7 @@ py::tuple param_blocks(py::list params) {
   return py::make_tuple(py::cast(std::move(h)), ptrs);
 }
 
-// The blocks for `params` (models[0]'s parameters, all on one HIP device) taken on the worker thread;
-// param_blocks_finish waits for them.  Parameters that are not dense device tensors: taken here, now.
-std::unique_ptr<FreshParams> param_blocks_start(py::list params) {
-  const py::ssize_t n = PyList_GET_SIZE(params.ptr());
-  auto h = std::make_unique<FreshParams>();
-  std::vector<at::Tensor> likes;
-  likes.reserve(n);
-  bool device_only = n > 0;
-  for (py::ssize_t i = 0; i < n; ++i) {
-    PyObject* o = PyList_GET_ITEM(params.ptr(), i);
-    if (!THPVariable_Check(o)) throw std::invalid_argument("param_blocks_start: not a tensor");
-    likes.push_back(THPVariable_Unpack(o));
-    const at::Tensor& p = likes.back();
-    device_only = device_only && p.is_cuda() && p.is_contiguous() && p.layout() == at::kStrided &&
-                  p.device() == likes.front().device();
-  }
-  if (!device_only) {
-    FreshAlloc fresh;
-    for (const at::Tensor& p : likes) h->t.push_back(fresh.like(p));
-    return h;
-  }
-  const c10::Device dev = likes.front().device();
-  c10::impl::VirtualGuardImpl impl(dev.type());
-  auto job = std::make_shared<BlockJob>(impl.getStream(dev));
-  job->likes = std::move(likes);
-  if (!BlockWorker::get().submit(job)) run_block_job(*job);
-  h->job = std::move(job);
-  return h;
-}
-
-py::array_t<uint64_t> param_blocks_finish(FreshParams& h) {
-  if (h.job) {
-    std::shared_ptr<BlockJob> job = std::move(h.job);
-    {
-      py::gil_scoped_release nogil;  // the allocator may call back into Python (its OOM / trace hooks)
-      std::unique_lock<std::mutex> g(job->mu);
-      job->cv.wait(g, [&] { return job->done; });
-    }
-    if (job->err) std::rethrow_exception(job->err);
-    h.t = std::move(job->out);
-  }
-  py::array_t<uint64_t> ptrs(static_cast<py::ssize_t>(h.t.size()));
-  uint64_t* out = ptrs.mutable_data();
-  for (size_t i = 0; i < h.t.size(); ++i) out[i] = reinterpret_cast<uint64_t>(h.t[i].data_ptr());
-  return ptrs;
-}
-
 void param_wrap(FreshParams& h, py::list params, py::dict memo) {
-  if (h.job) throw std::invalid_argument("param_wrap: call param_blocks_finish first");
   const py::ssize_t n = PyList_GET_SIZE(params.ptr());
   if (static_cast<size_t>(n) != h.t.size()) throw std::invalid_argument("param_wrap: one block per parameter");
   for (py::ssize_t i = 0; i < n; ++i) {
@@ -1700,8 +1569,6 @@ PYBIND11_MODULE(_dla_walk, m) {
   m.def("param_fresh", &param_fresh, py::arg("params"), py::arg("memo"));
   py::class_<FreshParams>(m, "FreshParams").def("__len__", [](const FreshParams& h) { return h.t.size(); });
   m.def("param_blocks", &param_blocks, py::arg("params"));
-  m.def("param_blocks_start", &param_blocks_start, py::arg("params"));
-  m.def("param_blocks_finish", &param_blocks_finish, py::arg("blocks"));
   m.def("param_wrap", &param_wrap, py::arg("blocks"), py::arg("params"), py::arg("memo"));
   m.def("buffer_copies", &buffer_copies, py::arg("buffers"), py::arg("memo"));
   m.def("clone_value", &clone_value, py::arg("v"), py::arg("memo"), py::arg("atomic"), py::arg("modules"),

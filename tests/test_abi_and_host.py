@@ -815,13 +815,6 @@ def test_walk_memo_seeding_on_cpu():
     assert list(bptrs) == [g0.data_ptr(), g1.data_ptr()] and g0.untyped_storage().nbytes() == 48
     with pytest.raises(ValueError):
         mod.param_wrap(mod.param_blocks(pf)[0], pf[:1], {})
-    # param_blocks_start / _finish: the same blocks (host tensors are taken at once; device ones on the
-    # worker thread); param_wrap refuses blocks not finished
-    started = mod.param_blocks_start(pf)
-    sptrs = mod.param_blocks_finish(started)
-    sm = {}
-    mod.param_wrap(started, pf, sm)
-    assert list(sptrs) == [sm[id(pf[0])].data_ptr(), sm[id(pf[1])].data_ptr()] and sm[id(pf[0])].shape == (3, 4)
     import numpy as np
 
     pooled = torch.from_numpy(np.arange(8, dtype=np.float32))  # memory torch did not allocate
