@@ -516,6 +516,8 @@ bool memo_put(PyObject* memo, PyObject* x, PyObject* y, PyObject* key = nullptr)
   return rc == 0;
 }
 
+// (_PyType_Lookup and _PyObject_GetDictPtr below are CPython's own, exported by the 3.10 this extension
+// is built against; the build id ties the .so to that interpreter's headers.)
 // y.__setstate__(state) is y.__dict__.update(state) on a fresh y: its class keeps torch's
 // nn.Module.__setstate__, and the state holds every attribute whose absence that function repairs.
 // 1 yes, 0 no, -1 error.

@@ -307,3 +307,26 @@ def test_clone_sets_a_module_state_directly_only_where_setstate_would_just_copy_
         assert a._forward_hooks is not x._forward_hooks and a._parameters is not x._parameters
     assert "_backward_pre_hooks" in c[2].__dict__ and list(c[2].__dict__)[-1] == "_backward_pre_hooks"
     assert all(torch.equal(p, q) for p, q in zip(c.parameters(), m.parameters()))
+
+
+def test_full_state_check_refuses_a_setstate_that_does_more(monkeypatch):
+    """fedavg._setstate_full_state enables the direct-__dict__ clone only when nn.Module.__setstate__, given
+    a fresh module's full state, leaves exactly that state: a __setstate__ that adds or replaces anything
+    turns it off."""
+    from accdfl_amd.core.gradient_aggregation import fedavg as fa
+
+    orig = nn.Module.__setstate__
+
+    def adds(self, state):
+        orig(self, state)
+        self.__dict__["_extra"] = None
+
+    def replaces(self, state):
+        orig(self, state)
+        self.__dict__["training"] = not state["training"]
+
+    for fn in (adds, replaces):
+        monkeypatch.setattr(nn.Module, "__setstate__", fn)
+        assert fa._setstate_full_state() is None
+    monkeypatch.setattr(nn.Module, "__setstate__", orig)
+    assert fa._setstate_full_state() == fa._FULL_STATE
